@@ -1,0 +1,651 @@
+// engine.cpp — device-resident Gemma forward for MI355X (the performance path).
+//
+// Keeps the whole token on the GPU: weights tiled in HBM, the activation never leaves the device,
+// the greedy token is fed back on the device, and one decode step (18 layers x 5 kernels + the
+// logits/argmax kernel + the advance kernel) is captured once in a hipGraph and replayed.
+// It computes exactly the graph src/gemma_model.cpp:665-747 builds, op for op (see the per-kernel
+// citations in kernels.h / matvec.hip / ops.hip), with the fusions listed in DESIGN.md §Kernels.
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gemma_hpc.h"
+#include "kernels.h"
+
+namespace ghip {
+
+// ---- error state ------------------------------------------------------------------------------
+static thread_local std::string g_err;
+void set_error(const std::string &m) { g_err = m; }
+const std::string &last_error() { return g_err; }
+
+// ---- host-side constant tables (product code; independent of oracle/) -------------------------
+static inline uint32_t fbits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float bitsf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+uint16_t host_f32_to_f16(float f) {  // IEEE RNE, subnormals, inf/nan
+    const uint32_t x = fbits(f);
+    const uint16_t sign = (uint16_t)((x >> 16) & 0x8000);
+    const uint32_t ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00 | (ax > 0x7f800000u ? 0x200 | ((ax >> 13) & 0x3ff) : 0));
+    if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00);
+    if (ax < 0x38800000u) {
+        if (ax < 0x33000000u) return sign;
+        const uint32_t e = ax >> 23, m = (ax & 0x7fffff) | 0x800000, shift = 126 - e;
+        uint32_t q = m >> shift;
+        const uint32_t rem = m & ((1u << shift) - 1), half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (q & 1))) q++;
+        return (uint16_t)(sign | q);
+    }
+    uint32_t r = (ax >> 13) - (112u << 10);
+    const uint32_t rem = ax & 0x1fff;
+    if (rem > 0x1000 || (rem == 0x1000 && (r & 1))) r++;
+    return (uint16_t)(sign | r);
+}
+
+float host_f16_to_f32(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000) << 16, exp = (h >> 10) & 0x1f, mant = h & 0x3ff;
+    if (exp == 0) {
+        const float v = (float)mant * 5.9604644775390625e-08f;
+        return mant == 0 ? bitsf(sign) : (sign ? -v : v);
+    }
+    if (exp == 31) return bitsf(sign | 0x7f800000u | (mant << 13));
+    return bitsf(sign | ((exp + 112) << 23) | (mant << 13));
+}
+
+// ggml_init tables: exp and gelu over every fp16 pattern
+static void build_f16_tables(std::vector<uint16_t> &exp_t, std::vector<uint16_t> &gelu_t) {
+    exp_t.resize(65536);
+    gelu_t.resize(65536);
+    for (int i = 0; i < 65536; ++i) {
+        const float f = host_f16_to_f32((uint16_t)i);
+        exp_t[i] = host_f32_to_f16(expf(f));
+        const float inner = 1.0f + 0.044715f * f * f;
+        const float t = tanhf(0.79788456080286535587989211986876f * f * inner);
+        gelu_t[i] = host_f32_to_f16(0.5f * f * (1.0f + t));
+    }
+}
+
+// rope NEOX cos/sin: theta = (float)p, theta *= powf(base, -2/n_dims) per pair
+static void build_rope(int ctx, int hd, float base, std::vector<float> &c, std::vector<float> &s) {
+    const int half = hd / 2;
+    c.resize((size_t)ctx * half);
+    s.resize((size_t)ctx * half);
+    const float theta_scale = powf(base, -2.0f / hd);
+    for (int p = 0; p < ctx; ++p) {
+        float theta = (float)p;
+        for (int i = 0; i < half; ++i) {
+            c[(size_t)p * half + i] = cosf(theta) * 1.0f;
+            s[(size_t)p * half + i] = sinf(theta) * 1.0f;
+            theta *= theta_scale;
+        }
+    }
+}
+
+// ---- synthetic weight keys (DESIGN.md §Synthetic weights; mirrors oracle/gemma_cpu.cpp) -------
+static inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static inline uint64_t tensor_key(uint64_t seed, int tid) { return splitmix64(seed ^ ((uint64_t)tid << 40)); }
+static inline float synth_scale(double stdv) { return (float)(stdv * 1.7320508075688772 / 65536.0); }
+enum { TID_EMBD = 0, TID_OUT_NORM = 1 };
+static inline int tid_layer(int il, int k) { return 16 + il * 16 + k; }
+enum { L_ATTN_NORM = 0, L_Q = 1, L_K = 2, L_V = 3, L_O = 4, L_FFN_NORM = 5, L_GATE = 6, L_UP = 7, L_DOWN = 8 };
+
+tiled_mat alloc_tiled(int type, int64_t rows, int64_t K, hipStream_t s) {
+    tiled_mat m;
+    m.type = type;
+    m.rows = rows;
+    m.K = K;
+    m.nb = K / 32;
+    m.n_rt = (rows + 7) / 8;
+    const int bt = type == T_Q4_0 ? 8 : 4;
+    m.n_bt = (m.nb + bt - 1) / bt;
+    GHIP_FATAL(hipMalloc(&m.qs, m.qs_bytes()));
+    GHIP_FATAL(hipMalloc(&m.sc, m.sc_bytes()));
+    // zero on the SAME stream as the generator / repack that fills it (non-blocking streams do
+    // not order against the null stream)
+    GHIP_FATAL(hipMemsetAsync(m.qs, 0, m.qs_bytes(), s));
+    GHIP_FATAL(hipMemsetAsync(m.sc, 0, m.sc_bytes(), s));
+    return m;
+}
+void free_tiled(tiled_mat &m) {
+    if (m.qs) (void)hipFree(m.qs);
+    if (m.sc) (void)hipFree(m.sc);
+    m.qs = m.sc = nullptr;
+}
+// rows [r0, r0+n) of a tiled matrix (r0, n multiples of 8) as its own tiled_mat view
+static tiled_mat sub_rows(const tiled_mat &m, int64_t r0, int64_t n) {
+    tiled_mat v = m;
+    const int sb = m.type == T_Q4_0 ? 16 : 8;
+    v.rows = n;
+    v.n_rt = (n + 7) / 8;
+    v.qs = m.qs + (r0 / 8) * m.n_bt * 1024;
+    v.sc = m.sc + (r0 / 8) * m.n_bt * 8 * sb;
+    return v;
+}
+
+}  // namespace ghip
+
+using namespace ghip;
+
+struct layer_dev {
+    float *attn_norm = nullptr, *ffn_norm = nullptr;
+    tiled_mat qkv, o, gate, up, down;
+};
+
+struct gemma_engine {
+    gemma_hip_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int qw = 0, kvw = 0, qkv_rows = 0;
+    tiled_mat embd;
+    float *out_norm = nullptr;
+    std::vector<layer_dev> layers;
+    uint16_t *kc = nullptr, *vc = nullptr;  // [L][ctx][kvw], [L][kvw][ctx]
+    uint16_t *exp_tab = nullptr, *gelu_tab = nullptr;
+    float *rope_cos = nullptr, *rope_sin = nullptr;
+    // activations
+    float *x = nullptr, *qkv = nullptr, *attn = nullptr, *sa = nullptr, *h = nullptr, *logits = nullptr;
+    unsigned long long *key = nullptr;
+    int *pos = nullptr, *token = nullptr, *hist = nullptr, *nfix = nullptr;
+    int n_prompt = 0;
+    int host_pos = 0;  // mirror of *pos (steps are deterministic)
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    // launch geometry
+    int ks_small = 4, ks_down = 8;
+    int grid_big = 2048;
+    // prefill scratch (lazily allocated)
+    void *pf_scratch = nullptr;
+    size_t pf_bytes = 0;
+    float *dbg = nullptr;  // per-layer taps [L][qkv_rows + qw + E] (debug steps only)
+};
+
+// largest power-of-two K split <= target that divides the block-tile count
+static int pick_ks(int64_t n_bt, int target) {
+    int ks = target;
+    while (ks > 1 && n_bt % ks) ks >>= 1;
+    return ks;
+}
+
+static int enqueue_step(gemma_engine *e) {
+    const gemma_hip_config &c = e->cfg;
+    const int wt = c.wtype;
+    hipStream_t s = e->stream;
+    const int E = c.n_embd;
+    for (int il = 0; il < c.n_layer; ++il) {
+        layer_dev &L = e->layers[il];
+        // K1: [embed | rms_norm*attn_norm] + quantize -> Wq|Wk|Wv   (:677-696)
+        mv_args a;
+        a.qs = L.qkv.qs; a.sc = L.qkv.sc; a.rows = L.qkv.rows; a.n_rt = L.qkv.n_rt; a.n_bt = L.qkv.n_bt;
+        a.nb = L.qkv.nb;
+        a.norm_w = L.attn_norm; a.eps = c.eps; a.y = e->qkv;
+        int pro = PRO_NORM;
+        if (il == 0) {
+            pro = PRO_EMBED;
+            a.x = e->hist; a.tok_pos = e->pos;
+            a.emb_qs = e->embd.qs; a.emb_sc = e->embd.sc; a.emb_n_bt = e->embd.n_bt;
+            a.emb_scale = sqrtf((float)E);
+            a.emb_out = e->x;
+        } else {
+            a.x = e->x;
+        }
+        if (launch_matvec(wt, pick_ks(L.qkv.n_bt, e->ks_small), pro, EPI_STORE, a, (int)L.qkv.n_rt, s)) return -1;
+        // K2: rope + scale + kv store + KQ + softmax + KQV  (:698-718, :454-518)
+        attn_args t;
+        t.qkv = e->qkv;
+        t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
+        t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
+        t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.exp_tab = e->exp_tab;
+        t.pos = e->pos; t.out = e->attn;
+        t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
+        t.q_scale = 1.0f / sqrtf((float)c.head_dim);
+        if (launch_attn_decode(t, s)) return -1;
+        const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
+        if (e->dbg) GHIP_CHECK(hipMemcpyAsync(e->dbg + tap, e->qkv, (size_t)e->qkv_rows * 4, hipMemcpyDeviceToDevice, s));
+        if (e->dbg)
+            GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows, e->attn, (size_t)e->qw * 4, hipMemcpyDeviceToDevice, s));
+        // K3: quantize(attn) -> Wo, + inpL  (:493, :723)
+        mv_args b;
+        b.qs = L.o.qs; b.sc = L.o.sc; b.rows = L.o.rows; b.n_rt = L.o.n_rt; b.n_bt = L.o.n_bt; b.nb = L.o.nb;
+        b.x = e->attn; b.y = e->sa; b.resid = e->x;
+        if (launch_matvec(wt, pick_ks(L.o.n_bt, e->ks_small), PRO_F32, EPI_ADD, b, (int)L.o.n_rt, s)) return -1;
+        // K4: rms_norm*ffn_norm + quantize -> gate & up -> gelu(gate)*up  (:724, :446-449)
+        mv_args g;
+        g.qs = L.gate.qs; g.sc = L.gate.sc; g.qs2 = L.up.qs; g.sc2 = L.up.sc;
+        g.rows = L.gate.rows; g.n_rt = L.gate.n_rt; g.n_bt = L.gate.n_bt; g.nb = L.gate.nb;
+        g.x = e->sa; g.norm_w = L.ffn_norm; g.eps = c.eps; g.y = e->h;
+        g.gelu_tab = e->gelu_tab; g.gelu_clamp = c.gelu_clamp;
+        if (launch_matvec(wt, 1, PRO_NORM, EPI_GELU_MUL, g, (int)std::min<int64_t>((L.gate.n_rt + 3) / 4, e->grid_big), s))
+            return -1;
+        // K5: quantize(h) -> Wdown, + sa  (:450, :731)
+        mv_args d;
+        d.qs = L.down.qs; d.sc = L.down.sc; d.rows = L.down.rows; d.n_rt = L.down.n_rt; d.n_bt = L.down.n_bt;
+        d.nb = L.down.nb;
+        d.x = e->h; d.y = e->x; d.resid = e->sa;
+        if (launch_matvec(wt, pick_ks(L.down.n_bt, e->ks_down), PRO_F32, EPI_ADD, d, (int)L.down.n_rt, s)) return -1;
+        if (e->dbg)
+            GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows + e->qw, e->x, (size_t)E * 4, hipMemcpyDeviceToDevice, s));
+    }
+    // K6: rms_norm*output_norm + quantize -> tied output -> logits + argmax  (:736-740, :532-546)
+    mv_args o;
+    o.qs = e->embd.qs; o.sc = e->embd.sc; o.rows = e->embd.rows; o.n_rt = e->embd.n_rt; o.n_bt = e->embd.n_bt;
+    o.nb = e->embd.nb;
+    o.x = e->x; o.norm_w = e->out_norm; o.eps = c.eps; o.y = e->logits; o.argmax_key = e->key;
+    if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, (int)std::min<int64_t>((e->embd.n_rt + 3) / 4, e->grid_big), s))
+        return -1;
+    // K7: token feedback (greedy_sample -> input.push_back, :282-285), position += 1
+    // the prompt is never overwritten: hist writes only land at positions >= n_prompt
+    return launch_advance(e->key, e->token, e->pos, e->hist, c.n_ctx, e->nfix, e->key, s);
+}
+
+extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int device) {
+    set_error("");
+    const gemma_hip_config &c = *cfg;
+    if (c.head_dim % 32 || c.n_embd % 32 || c.n_ff % 32 || c.n_ctx % 32 || c.n_head % c.n_head_kv ||
+        (c.wtype != T_Q4_0 && c.wtype != T_Q8_0)) {
+        set_error("gemma_engine_create: unsupported config");
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        set_error("gemma_engine_create: hipSetDevice failed");
+        return nullptr;
+    }
+    auto *e = new gemma_engine();
+    e->cfg = c;
+    e->device = device;
+    GHIP_FATAL(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    e->qw = c.n_head * c.head_dim;
+    e->kvw = c.n_head_kv * c.head_dim;
+    e->qkv_rows = e->qw + 2 * e->kvw;
+    if (const char *v = getenv("GHIP_KS_SMALL")) e->ks_small = atoi(v);
+    if (const char *v = getenv("GHIP_KS_DOWN")) e->ks_down = atoi(v);
+    const int wt = c.wtype;
+    const uint64_t seed = c.seed;
+    hipStream_t s = e->stream;
+    // weights: synthetic generator straight into the tiled layout (matches oracle/gemma_cpu.cpp)
+    e->embd = alloc_tiled(wt, c.n_vocab, c.n_embd, s);
+    launch_synth_tiled(e->embd, tensor_key(seed, TID_EMBD), synth_scale(1.0 / sqrt((double)c.n_embd)), 0, s);
+    GHIP_FATAL(hipMalloc(&e->out_norm, (size_t)c.n_embd * 4));
+    launch_synth_norm(e->out_norm, c.n_embd, tensor_key(seed, TID_OUT_NORM), synth_scale(0.05), s);
+    e->layers.resize(c.n_layer);
+    const double se = 1.0 / sqrt((double)c.n_embd), sq = 1.0 / sqrt((double)e->qw), sf = 1.0 / sqrt((double)c.n_ff);
+    for (int il = 0; il < c.n_layer; ++il) {
+        layer_dev &L = e->layers[il];
+        GHIP_FATAL(hipMalloc(&L.attn_norm, (size_t)c.n_embd * 4));
+        GHIP_FATAL(hipMalloc(&L.ffn_norm, (size_t)c.n_embd * 4));
+        launch_synth_norm(L.attn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_ATTN_NORM)), synth_scale(0.05), s);
+        launch_synth_norm(L.ffn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_FFN_NORM)), synth_scale(0.05), s);
+        L.qkv = alloc_tiled(wt, e->qkv_rows, c.n_embd, s);
+        launch_synth_tiled(sub_rows(L.qkv, 0, e->qw), tensor_key(seed, tid_layer(il, L_Q)), synth_scale(se), 0, s);
+        launch_synth_tiled(sub_rows(L.qkv, e->qw, e->kvw), tensor_key(seed, tid_layer(il, L_K)), synth_scale(se), 0, s);
+        launch_synth_tiled(sub_rows(L.qkv, e->qw + e->kvw, e->kvw), tensor_key(seed, tid_layer(il, L_V)),
+                           synth_scale(se), 0, s);
+        L.o = alloc_tiled(wt, c.n_embd, e->qw, s);
+        launch_synth_tiled(L.o, tensor_key(seed, tid_layer(il, L_O)), synth_scale(4.0 * sq), 0, s);
+        L.gate = alloc_tiled(wt, c.n_ff, c.n_embd, s);
+        launch_synth_tiled(L.gate, tensor_key(seed, tid_layer(il, L_GATE)), synth_scale(se), 0, s);
+        L.up = alloc_tiled(wt, c.n_ff, c.n_embd, s);
+        launch_synth_tiled(L.up, tensor_key(seed, tid_layer(il, L_UP)), synth_scale(se), 0, s);
+        L.down = alloc_tiled(wt, c.n_embd, c.n_ff, s);
+        launch_synth_tiled(L.down, tensor_key(seed, tid_layer(il, L_DOWN)), synth_scale(4.0 * sf), 0, s);
+    }
+    // caches, tables, activations
+    const size_t kv_elems = (size_t)c.n_layer * c.n_ctx * e->kvw;
+    GHIP_FATAL(hipMalloc(&e->kc, kv_elems * 2));
+    GHIP_FATAL(hipMalloc(&e->vc, kv_elems * 2));
+    GHIP_FATAL(hipMemsetAsync(e->kc, 0, kv_elems * 2, s));
+    GHIP_FATAL(hipMemsetAsync(e->vc, 0, kv_elems * 2, s));
+    std::vector<uint16_t> et, gt;
+    build_f16_tables(et, gt);
+    std::vector<float> rc, rs;
+    build_rope(c.n_ctx, c.head_dim, c.rope_base, rc, rs);
+    GHIP_FATAL(hipMalloc(&e->exp_tab, 65536 * 2));
+    GHIP_FATAL(hipMalloc(&e->gelu_tab, 65536 * 2));
+    GHIP_FATAL(hipMalloc(&e->rope_cos, rc.size() * 4));
+    GHIP_FATAL(hipMalloc(&e->rope_sin, rs.size() * 4));
+    GHIP_FATAL(hipMemcpy(e->exp_tab, et.data(), 65536 * 2, hipMemcpyHostToDevice));
+    GHIP_FATAL(hipMemcpy(e->gelu_tab, gt.data(), 65536 * 2, hipMemcpyHostToDevice));
+    GHIP_FATAL(hipMemcpy(e->rope_cos, rc.data(), rc.size() * 4, hipMemcpyHostToDevice));
+    GHIP_FATAL(hipMemcpy(e->rope_sin, rs.data(), rs.size() * 4, hipMemcpyHostToDevice));
+    GHIP_FATAL(hipMalloc(&e->x, (size_t)c.n_embd * 4));
+    GHIP_FATAL(hipMalloc(&e->qkv, (size_t)e->qkv_rows * 4));
+    GHIP_FATAL(hipMalloc(&e->attn, (size_t)e->qw * 4));
+    GHIP_FATAL(hipMalloc(&e->sa, (size_t)c.n_embd * 4));
+    GHIP_FATAL(hipMalloc(&e->h, (size_t)c.n_ff * 4));
+    GHIP_FATAL(hipMalloc(&e->logits, (size_t)c.n_vocab * 4));
+    GHIP_FATAL(hipMalloc(&e->key, 8));
+    GHIP_FATAL(hipMalloc(&e->pos, 4));
+    GHIP_FATAL(hipMalloc(&e->token, 4));
+    GHIP_FATAL(hipMalloc(&e->nfix, 4));
+    GHIP_FATAL(hipMalloc(&e->hist, (size_t)(c.n_ctx + 1) * 4));
+    GHIP_FATAL(hipMemsetAsync(e->key, 0, 8, s));
+    GHIP_FATAL(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
+    GHIP_FATAL(hipStreamSynchronize(s));
+    if (!last_error().empty()) {
+        gemma_engine_free(e);
+        return nullptr;
+    }
+    return e;
+}
+
+extern "C" void gemma_engine_free(gemma_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    (void)hipStreamSynchronize(e->stream);
+    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
+    if (e->graph) (void)hipGraphDestroy(e->graph);
+    free_tiled(e->embd);
+    for (auto &L : e->layers) {
+        free_tiled(L.qkv); free_tiled(L.o); free_tiled(L.gate); free_tiled(L.up); free_tiled(L.down);
+        (void)hipFree(L.attn_norm); (void)hipFree(L.ffn_norm);
+    }
+    void *bufs[] = {e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
+                    e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf_scratch};
+    for (void *p : bufs)
+        if (p) (void)hipFree(p);
+    (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+extern "C" int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_prompt) {
+    set_error("");
+    const gemma_hip_config &c = e->cfg;
+    if (n_prompt <= 0 || n_prompt >= c.n_ctx) {
+        set_error("gemma_engine_begin: prompt length out of range");
+        return -1;
+    }
+    (void)hipSetDevice(e->device);
+    hipStream_t s = e->stream;
+    const size_t kv_bytes = (size_t)c.n_layer * c.n_ctx * e->kvw * 2;
+    GHIP_CHECK(hipMemsetAsync(e->kc, 0, kv_bytes, s));
+    GHIP_CHECK(hipMemsetAsync(e->vc, 0, kv_bytes, s));
+    GHIP_CHECK(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
+    GHIP_CHECK(hipMemcpyAsync(e->hist, prompt, (size_t)n_prompt * 4, hipMemcpyHostToDevice, s));
+    GHIP_CHECK(hipMemsetAsync(e->pos, 0, 4, s));
+    GHIP_CHECK(hipMemsetAsync(e->key, 0, 8, s));
+    GHIP_CHECK(hipMemcpyAsync(e->nfix, &n_prompt, 4, hipMemcpyHostToDevice, s));
+    GHIP_CHECK(hipStreamSynchronize(s));
+    e->n_prompt = n_prompt;
+    e->host_pos = 0;
+    return 0;
+}
+
+static int ensure_graph(gemma_engine *e) {
+    if (e->graph_exec) return 0;
+    GHIP_CHECK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeRelaxed));
+    const int r = enqueue_step(e);
+    hipGraph_t g = nullptr;
+    const hipError_t ce = hipStreamEndCapture(e->stream, &g);
+    if (r != 0) return -1;
+    if (ce != hipSuccess) {
+        set_error(std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+        return -1;
+    }
+    e->graph = g;
+    GHIP_CHECK(hipGraphInstantiate(&e->graph_exec, g, nullptr, nullptr, 0));
+    return 0;
+}
+
+extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_graph) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    const gemma_hip_config &c = e->cfg;
+    if (e->host_pos + n >= c.n_ctx) {
+        set_error("gemma_engine_step: context full");
+        return -1;
+    }
+    if (use_graph && !e->graph_exec) {
+        // first eager step sets the kernels' LDS attributes before capture
+        if (enqueue_step(e)) return -1;
+        GHIP_CHECK(hipStreamSynchronize(e->stream));
+        if (logits) GHIP_CHECK(hipMemcpy(logits, e->logits, (size_t)c.n_vocab * 4, hipMemcpyDeviceToHost));
+        e->host_pos += 1;
+        if (logits) logits += c.n_vocab;
+        n -= 1;
+        if (ensure_graph(e)) return -1;
+    }
+    for (int i = 0; i < n; ++i) {
+        if (use_graph) GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
+        else if (enqueue_step(e)) return -1;
+        if (logits) {
+            GHIP_CHECK(hipMemcpyAsync(logits + (size_t)i * c.n_vocab, e->logits, (size_t)c.n_vocab * 4,
+                                      hipMemcpyDeviceToHost, e->stream));
+            GHIP_CHECK(hipStreamSynchronize(e->stream));
+        }
+        e->host_pos += 1;
+    }
+    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gemma_engine_sync(gemma_engine *e) {
+    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gemma_engine_tokens(gemma_engine *e, int32_t *out, int cap) {
+    const int n = std::min(cap, e->host_pos + 1);
+    GHIP_CHECK(hipMemcpy(out, e->hist, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return n;
+}
+
+extern "C" int gemma_engine_pos(gemma_engine *e) { return e->host_pos; }
+
+extern "C" int64_t gemma_engine_tensor(gemma_engine *e, int tid, void *dst, int64_t cap) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    const gemma_hip_config &c = e->cfg;
+    auto copy_f32 = [&](const float *p, int64_t n) -> int64_t {
+        if (cap < n * 4) return -1;
+        GHIP_CHECK(hipMemcpy(dst, p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        return n * 4;
+    };
+    auto copy_mat = [&](const tiled_mat &m) -> int64_t {
+        const int64_t bytes = m.rows * m.nb * (m.type == T_Q4_0 ? 18 : 34);
+        if (cap < bytes) return -1;
+        uint8_t *tmp = nullptr;
+        GHIP_CHECK(hipMalloc(&tmp, (size_t)bytes));
+        if (launch_untile(m, tmp, e->stream)) return -1;
+        GHIP_CHECK(hipStreamSynchronize(e->stream));
+        GHIP_CHECK(hipMemcpy(dst, tmp, (size_t)bytes, hipMemcpyDeviceToHost));
+        GHIP_CHECK(hipFree(tmp));
+        return bytes;
+    };
+    if (tid == TID_EMBD) return copy_mat(e->embd);
+    if (tid == TID_OUT_NORM) return copy_f32(e->out_norm, c.n_embd);
+    const int il = (tid - 16) / 16, k = (tid - 16) % 16;
+    if (tid < 16 || il >= c.n_layer) return -1;
+    layer_dev &L = e->layers[il];
+    switch (k) {
+        case L_ATTN_NORM: return copy_f32(L.attn_norm, c.n_embd);
+        case L_FFN_NORM: return copy_f32(L.ffn_norm, c.n_embd);
+        case L_Q: return copy_mat(sub_rows(L.qkv, 0, e->qw));
+        case L_K: return copy_mat(sub_rows(L.qkv, e->qw, e->kvw));
+        case L_V: return copy_mat(sub_rows(L.qkv, e->qw + e->kvw, e->kvw));
+        case L_O: return copy_mat(L.o);
+        case L_GATE: return copy_mat(L.gate);
+        case L_UP: return copy_mat(L.up);
+        case L_DOWN: return copy_mat(L.down);
+    }
+    return -1;
+}
+
+// ---- hipEvent timing of one hot kernel on the engine stream (bench.py roofline leg) -----------
+extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, double *algo_bytes) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    const gemma_hip_config &c = e->cfg;
+    const int wt = c.wtype;
+    layer_dev &L = e->layers[0];
+    const double act_q8 = 34.0 / 32.0;  // bytes per activation element after quantization
+    mv_args a;
+    int ks = 1, pro = PRO_F32, epi = EPI_STORE, grid = 1;
+    double bytes = 0;
+    auto set_mat = [&](const tiled_mat &m) {
+        a.qs = m.qs; a.sc = m.sc; a.rows = m.rows; a.n_rt = m.n_rt; a.n_bt = m.n_bt; a.nb = m.nb;
+    };
+    switch (which) {
+        case 0:
+            set_mat(L.gate);
+            a.qs2 = L.up.qs; a.sc2 = L.up.sc;
+            a.x = e->sa; a.norm_w = L.ffn_norm; a.eps = c.eps; a.y = e->h; a.gelu_tab = e->gelu_tab;
+            pro = PRO_NORM; epi = EPI_GELU_MUL;
+            grid = (int)std::min<int64_t>((L.gate.n_rt + 3) / 4, e->grid_big);
+            bytes = (double)L.gate.algo_bytes() + L.up.algo_bytes() + c.n_embd * 4.0 * 2 + c.n_ff * 4.0;
+            break;
+        case 1:
+            set_mat(L.down);
+            a.x = e->h; a.y = e->x; a.resid = e->sa; ks = pick_ks(L.down.n_bt, e->ks_down); epi = EPI_ADD;
+            grid = (int)L.down.n_rt;
+            bytes = (double)L.down.algo_bytes() + c.n_ff * 4.0 + c.n_embd * 8.0;
+            break;
+        case 2:
+            set_mat(L.qkv);
+            a.x = e->x; a.norm_w = L.attn_norm; a.eps = c.eps; a.y = e->qkv; ks = pick_ks(L.qkv.n_bt, e->ks_small); pro = PRO_NORM;
+            grid = (int)L.qkv.n_rt;
+            bytes = (double)L.qkv.algo_bytes() + c.n_embd * 8.0 + e->qkv_rows * 4.0;
+            break;
+        case 3:
+            set_mat(L.o);
+            a.x = e->attn; a.y = e->sa; a.resid = e->x; ks = pick_ks(L.o.n_bt, e->ks_small); epi = EPI_ADD;
+            grid = (int)L.o.n_rt;
+            bytes = (double)L.o.algo_bytes() + e->qw * 4.0 + c.n_embd * 8.0;
+            break;
+        case 4:
+            set_mat(e->embd);
+            a.x = e->x; a.norm_w = e->out_norm; a.eps = c.eps; a.y = e->logits; a.argmax_key = e->key;
+            pro = PRO_NORM; epi = EPI_ARGMAX;
+            grid = (int)std::min<int64_t>((e->embd.n_rt + 3) / 4, e->grid_big);
+            bytes = (double)e->embd.algo_bytes() + c.n_embd * 8.0 + c.n_vocab * 4.0;
+            break;
+        case 5:
+            break;
+        default:
+            set_error("gemma_engine_time: bad kernel id");
+            return -1.0;
+    }
+    (void)act_q8;
+    hipEvent_t t0, t1;
+    GHIP_FATAL(hipEventCreate(&t0));
+    GHIP_FATAL(hipEventCreate(&t1));
+    auto run = [&]() -> int {
+        if (which == 5) {
+            if (ensure_graph(e)) return -1;
+            GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
+            return 0;
+        }
+        return launch_matvec(wt, ks, pro, epi, a, grid, e->stream);
+    };
+    if (which == 5) {
+        // whole step replays advance the position: keep within the context
+        if (e->host_pos + 2 * iters + 4 >= c.n_ctx) {
+            set_error("gemma_engine_time: context too small for step timing");
+            return -1.0;
+        }
+    }
+    for (int i = 0; i < 3; ++i)
+        if (run()) return -1.0;
+    GHIP_FATAL(hipEventRecord(t0, e->stream));
+    for (int i = 0; i < iters; ++i)
+        if (run()) return -1.0;
+    GHIP_FATAL(hipEventRecord(t1, e->stream));
+    GHIP_FATAL(hipEventSynchronize(t1));
+    if (which == 5) e->host_pos += iters + 3;
+    float ms = 0;
+    GHIP_FATAL(hipEventElapsedTime(&ms, t0, t1));
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    if (algo_bytes) *algo_bytes = bytes;
+    return (double)ms * 1000.0 / iters;
+}
+
+extern "C" int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *logits_all) {
+    (void)e; (void)logits_last; (void)logits_all;
+    set_error("gemma_engine_prefill: MFMA prefill not built yet");
+    return -1;
+}
+
+// one eager step with per-layer taps copied to host: [L][qkv | attn | x_out]
+extern "C" int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    const gemma_hip_config &c = e->cfg;
+    const size_t per = (size_t)e->qkv_rows + e->qw + c.n_embd;
+    GHIP_CHECK(hipMalloc(&e->dbg, per * c.n_layer * 4));
+    const int r = enqueue_step(e);
+    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    if (r == 0) {
+        GHIP_CHECK(hipMemcpy(host_taps, e->dbg, per * c.n_layer * 4, hipMemcpyDeviceToHost));
+        if (logits) GHIP_CHECK(hipMemcpy(logits, e->logits, (size_t)c.n_vocab * 4, hipMemcpyDeviceToHost));
+        e->host_pos += 1;
+    }
+    GHIP_CHECK(hipFree(e->dbg));
+    e->dbg = nullptr;
+    return r;
+}
+
+// ---- per-op test entry: the decode attention kernel on host buffers ---------------------------
+// qkv [H*hd + 2*Hkv*hd] f32; kc [ctx][Hkv*hd], vc [Hkv*hd][ctx] f16 (updated in place at pos)
+extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos, int H, int Hkv, int hd,
+                                      int ctx, float rope_base, float *out, float *dbg_w, uint16_t *dbg_p,
+                                      float *dbg_inv) {
+    set_error("");
+    const size_t qkv_n = (size_t)(H + 2 * Hkv) * hd, cache_n = (size_t)ctx * Hkv * hd;
+    std::vector<uint16_t> et, gt;
+    build_f16_tables(et, gt);
+    std::vector<float> rc, rs;
+    build_rope(ctx, hd, rope_base, rc, rs);
+    float *d_qkv, *d_out, *d_c, *d_s;
+    uint16_t *d_k, *d_v, *d_e;
+    int *d_pos;
+    float *d_dw = nullptr, *d_di = nullptr;
+    uint16_t *d_dp = nullptr;
+    if (dbg_w) GHIP_CHECK(hipMalloc(&d_dw, (size_t)H * ctx * 4));
+    if (dbg_p) GHIP_CHECK(hipMalloc(&d_dp, (size_t)H * ctx * 2));
+    if (dbg_inv) GHIP_CHECK(hipMalloc(&d_di, (size_t)H * 4));
+    GHIP_CHECK(hipMalloc(&d_qkv, qkv_n * 4));
+    GHIP_CHECK(hipMalloc(&d_out, (size_t)H * hd * 4));
+    GHIP_CHECK(hipMalloc(&d_c, rc.size() * 4));
+    GHIP_CHECK(hipMalloc(&d_s, rs.size() * 4));
+    GHIP_CHECK(hipMalloc(&d_k, cache_n * 2));
+    GHIP_CHECK(hipMalloc(&d_v, cache_n * 2));
+    GHIP_CHECK(hipMalloc(&d_e, 65536 * 2));
+    GHIP_CHECK(hipMalloc(&d_pos, 4));
+    GHIP_CHECK(hipMemcpy(d_qkv, qkv, qkv_n * 4, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_c, rc.data(), rc.size() * 4, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_s, rs.data(), rs.size() * 4, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_k, kc, cache_n * 2, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_v, vc, cache_n * 2, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_e, et.data(), 65536 * 2, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_pos, &pos, 4, hipMemcpyHostToDevice));
+    attn_args a;
+    a.qkv = d_qkv; a.kc = d_k; a.vc = d_v; a.rope_cos = d_c; a.rope_sin = d_s; a.exp_tab = d_e; a.pos = d_pos;
+    a.out = d_out; a.H = H; a.Hkv = Hkv; a.hd = hd; a.ctx = ctx; a.q_scale = 1.0f / sqrtf((float)hd);
+    a.dbg_w = d_dw; a.dbg_p = d_dp; a.dbg_inv = d_di;
+    const int r = launch_attn_decode(a, nullptr);
+    GHIP_CHECK(hipDeviceSynchronize());
+    if (r == 0) {
+        GHIP_CHECK(hipMemcpy(out, d_out, (size_t)H * hd * 4, hipMemcpyDeviceToHost));
+        GHIP_CHECK(hipMemcpy(kc, d_k, cache_n * 2, hipMemcpyDeviceToHost));
+        GHIP_CHECK(hipMemcpy(vc, d_v, cache_n * 2, hipMemcpyDeviceToHost));
+        if (dbg_w) GHIP_CHECK(hipMemcpy(dbg_w, d_dw, (size_t)H * ctx * 4, hipMemcpyDeviceToHost));
+        if (dbg_p) GHIP_CHECK(hipMemcpy(dbg_p, d_dp, (size_t)H * ctx * 2, hipMemcpyDeviceToHost));
+        if (dbg_inv) GHIP_CHECK(hipMemcpy(dbg_inv, d_di, (size_t)H * 4, hipMemcpyDeviceToHost));
+    }
+    void *bufs[] = {d_qkv, d_out, d_c, d_s, d_k, d_v, d_e, d_pos, d_dw, d_dp, d_di};
+    for (void *p : bufs)
+        if (p) (void)hipFree(p);
+    return r;
+}

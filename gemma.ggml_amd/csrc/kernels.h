@@ -1,0 +1,83 @@
+// kernels.h — launch wrappers for the gfx950 kernels (host-callable, no torch types).
+#pragma once
+
+#include "common.h"
+
+namespace ghip {
+
+// ---- decode matvec (matvec.hip) ----------------------------------------------------------------
+// Prologue: how the activation column is turned into the LDS Q8_0 image.
+enum mv_pro : int {
+    PRO_F32 = 0,    // x: f32[K] -> quantize_row_q8_0 (AVX2 semantics)
+    PRO_NORM = 1,   // x: f32[K] -> rms_norm(x)*norm_w (A.5) -> quantize
+    PRO_Q8 = 2,     // x: ggml block_q8_0[K/32] (the C-ABI `wdata`, already converted by ggml INIT)
+    PRO_EMBED = 3,  // x: int32 sequence, token = x[*tok_pos]; embedding row (tiled) * emb_scale -> norm
+};
+enum mv_epi : int {
+    EPI_STORE = 0,     // y[r] = dot
+    EPI_ADD = 1,       // y[r] = dot + resid[r]          (ggml_add, src/gemma_model.cpp:723,731)
+    EPI_GELU_MUL = 2,  // y[r] = gelu(dotA) * dotB       (src/gemma_model.cpp:446-449)
+    EPI_ARGMAX = 3,    // y[r] = dot and argmax key      (greedy_sample, :532-546)
+};
+
+struct mv_args {
+    const uint8_t *qs = nullptr, *sc = nullptr;    // weights (tiled)
+    const uint8_t *qs2 = nullptr, *sc2 = nullptr;  // second matrix for EPI_GELU_MUL (ffn_up)
+    int64_t rows = 0, n_rt = 0, n_bt = 0, nb = 0;  // nb = K/32
+    const void *x = nullptr;                       // activation (see mv_pro)
+    int64_t x_col_stride = 0;                      // bytes between columns (multi-column launch)
+    const float *norm_w = nullptr;
+    float eps = 0.f;
+    // PRO_EMBED: embedding source
+    const int *tok_pos = nullptr;
+    const uint8_t *emb_qs = nullptr, *emb_sc = nullptr;
+    int64_t emb_n_bt = 0;
+    float emb_scale = 1.f;
+    float *emb_out = nullptr;                      // if set, block 0 writes the scaled embedding row
+    // epilogue
+    float *y = nullptr;
+    int64_t y_col_stride = 0;                      // floats between columns
+    const float *resid = nullptr;
+    const uint16_t *gelu_tab = nullptr;
+    int gelu_clamp = 0;
+    unsigned long long *argmax_key = nullptr;
+    int ncols = 1;
+};
+
+// ks: waves that split one row tile's K range (ordered carry hand-off); 1 = one wave per tile.
+int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int grid_x, hipStream_t s);
+size_t matvec_lds_bytes(int wtype, int ks, int64_t n_bt, int64_t segment_tiles);
+
+// ---- weights (ops.hip) ------------------------------------------------------------------------
+// ggml row-major blocks (host layout) already on device -> tiled layout
+int launch_repack(const tiled_mat &m, const uint8_t *src_rowmajor, int64_t row_bytes, hipStream_t s);
+// synthetic generator: same integer stream + reference quantizer as oracle/gemma_cpu.cpp
+int launch_synth_tiled(const tiled_mat &m, uint64_t key, float scale, int64_t row_offset, hipStream_t s);
+int launch_synth_norm(float *dst, int64_t n, uint64_t key, float scale, hipStream_t s);
+int launch_untile(const tiled_mat &m, uint8_t *dst_rowmajor, hipStream_t s);
+
+// ---- small decode ops (ops.hip) -----------------------------------------------------------------
+struct attn_args {
+    const float *qkv;       // [q(H*hd) | k(Hkv*hd) | v(Hkv*hd)] for one token
+    uint16_t *kc, *vc;      // layer caches: K [ctx][Hkv*hd], V [Hkv*hd][ctx] (f16 bits)
+    const float *rope_cos, *rope_sin;  // [ctx][hd/2]
+    const uint16_t *exp_tab;
+    const int *pos;         // device scalar (position of this token)
+    float *out;             // [H*hd]
+    int H, Hkv, hd, ctx;
+    float q_scale;
+    float *dbg_w = nullptr;      // optional debug taps: [H][ctx] scores, [H][ctx] fp16 P, [H] inv
+    uint16_t *dbg_p = nullptr;
+    float *dbg_inv = nullptr;
+};
+int launch_attn_decode(const attn_args &a, hipStream_t s);
+int launch_embed(const uint8_t *qs, const uint8_t *sc, int wtype, int64_t n_bt, const int *token, float scale,
+                 float *out, int64_t E, hipStream_t s);
+int launch_advance(const unsigned long long *key, int *token, int *pos, int *hist, int hist_cap, const int *n_fixed,
+                   unsigned long long *key_reset, hipStream_t s);
+
+// ---- generic ggml-op kernels used by the C-ABI and the ggml-compatible executor ----------------
+int launch_mul_mat_f16(const uint16_t *src0, int64_t nb01_elems, int64_t ne01, const uint16_t *src1,
+                       int64_t row_size_elems, int64_t ncols, int64_t K, float *dst, hipStream_t s);
+
+}  // namespace ghip

@@ -1,0 +1,184 @@
+"""ctypes binding of libgemma_hip.so — the MI355X hot path behind the C-ABI in include/gemma_hpc.h.
+
+Product-side host mirror: it only forwards to the HIP library and never falls back to CPU code.
+Loading fails loudly if the library is missing or was not built for gfx950.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libgemma_hip.so")
+
+GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
+
+# exported symbols (checked against include/gemma_hpc.h by tests/test_capi_symbols.py)
+EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
+           "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
+           "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
+           "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync"]
+
+
+def build():
+    subprocess.run(["make", "-s", "-j8", "-C", PKG_DIR], check=True)
+
+
+class GemmaConfig(C.Structure):
+    _fields_ = [("n_layer", C.c_int), ("n_embd", C.c_int), ("n_head", C.c_int), ("n_head_kv", C.c_int),
+                ("head_dim", C.c_int), ("n_ff", C.c_int), ("n_vocab", C.c_int), ("n_ctx", C.c_int),
+                ("wtype", C.c_int), ("eps", C.c_float), ("rope_base", C.c_float), ("seed", C.c_uint64),
+                ("gelu_clamp", C.c_int)]
+
+
+class GgmlTensor(C.Structure):
+    """struct ggml_tensor as declared in include/ggml.h (only `data` is read by mul_mat)."""
+    _fields_ = [("type", C.c_int), ("backend", C.c_int), ("buffer", C.c_void_p), ("ne", C.c_int64 * 4),
+                ("nb", C.c_size_t * 4), ("op", C.c_int32), ("op_params", C.c_int32 * 16), ("flags", C.c_int32),
+                ("grad", C.c_void_p), ("src", C.c_void_p * 10), ("perf_runs", C.c_int), ("perf_cycles", C.c_int64),
+                ("perf_time_us", C.c_int64), ("view_src", C.c_void_p), ("view_offs", C.c_size_t),
+                ("data", C.c_void_p), ("name", C.c_char * 64), ("extra", C.c_void_p), ("padding", C.c_char * 8)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libgemma_hip.so not built ({LIB_PATH}); run `make -C {PKG_DIR}` or "
+                           "__graft_entry__.build() — there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, i64 = C.c_void_p, C.c_int64
+    L.mul_mat.restype = None
+    L.mul_mat.argtypes = [i64, i64, i64, i64, i64, i64, i64, C.c_size_t, i64, vp, vp, vp, vp, C.c_int, vp]
+    L.hpc_init.restype = C.c_int
+    L.hpc_init.argtypes = [C.c_int]
+    L.hpc_register_weight.restype = C.c_int
+    L.hpc_register_weight.argtypes = [vp, C.c_int, i64, i64, C.c_size_t]
+    L.hpc_last_error.restype = C.c_int
+    L.hpc_last_error.argtypes = [C.c_char_p, C.c_size_t]
+    L.hpc_set_error_mode.argtypes = [C.c_int]
+    L.hpc_weight_cache_entries.restype = C.c_int
+    L.hpc_set_matvec_ks.argtypes = [C.c_int]
+    L.gemma_engine_debug_step.restype = C.c_int
+    L.gemma_engine_debug_step.argtypes = [vp, vp, vp]
+    L.gemma_engine_create.restype = vp
+    L.gemma_engine_create.argtypes = [C.POINTER(GemmaConfig), C.c_int]
+    L.gemma_engine_free.argtypes = [vp]
+    L.gemma_engine_begin.restype = C.c_int
+    L.gemma_engine_begin.argtypes = [vp, vp, C.c_int]
+    L.gemma_engine_step.restype = C.c_int
+    L.gemma_engine_step.argtypes = [vp, C.c_int, vp, C.c_int]
+    L.gemma_engine_tokens.restype = C.c_int
+    L.gemma_engine_tokens.argtypes = [vp, vp, C.c_int]
+    L.gemma_engine_pos.restype = C.c_int
+    L.gemma_engine_pos.argtypes = [vp]
+    L.gemma_engine_prefill.restype = C.c_int
+    L.gemma_engine_prefill.argtypes = [vp, vp, vp]
+    L.gemma_engine_tensor.restype = C.c_int64
+    L.gemma_engine_tensor.argtypes = [vp, C.c_int, vp, i64]
+    L.gemma_engine_time.restype = C.c_double
+    L.gemma_engine_time.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    L.gemma_engine_sync.restype = C.c_int
+    L.gemma_engine_sync.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def last_error():
+    buf = C.create_string_buffer(1024)
+    lib().hpc_last_error(buf, 1024)
+    return buf.value.decode()
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def mul_mat(src0_bytes, src0_type, ne01, nb01, shared_edge, wdata, row_size, ncols, ne1=None, nb1=None, nb2=None):
+    """Call the drop-in `mul_mat` (src/hpc.h:22-32 signature) on host buffers; returns dst [ncols][ne01]."""
+    L = lib()
+    ne1 = ncols if ne1 is None else ne1
+    nb1 = ne01 * 4 if nb1 is None else nb1
+    nb2 = nb1 * ne1 if nb2 is None else nb2
+    ne12 = ncols // ne1
+    span = max((c % ne1) * nb1 + (c // ne1) * nb2 for c in range(ncols)) + ne01 * 4
+    raw = np.zeros((span + 3) // 4, dtype=np.float32)
+    dst = raw
+    t0, t1 = GgmlTensor(), GgmlTensor()
+    t0.data = src0_bytes.ctypes.data
+    t0.type = src0_type
+    t1.data = dst.ctypes.data
+    t1.type = GGML_TYPE_F32
+    L.mul_mat(ne01, ne1, ne12, nb01, ne1, nb1, nb2, row_size, shared_edge, C.byref(t0), None, C.byref(t1), None,
+              src0_type, _p(wdata))
+    out = np.empty((ncols, ne01), dtype=np.float32)
+    for c in range(ncols):
+        off = ((c % ne1) * nb1 + (c // ne1) * nb2) // 4
+        out[c] = raw[off:off + ne01]
+    return out
+
+
+class Engine:
+    def __init__(self, shape, n_ctx=512, wtype=GGML_TYPE_Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0,
+                 gelu_clamp=0, device=0):
+        self.cfg = GemmaConfig(n_ctx=n_ctx, wtype=wtype, eps=eps, rope_base=rope_base, seed=seed,
+                               gelu_clamp=gelu_clamp, **shape)
+        self.L = lib()
+        self.h = self.L.gemma_engine_create(C.byref(self.cfg), device)
+        if not self.h:
+            raise RuntimeError("gemma_engine_create failed: " + last_error())
+
+    def close(self):
+        if self.h:
+            self.L.gemma_engine_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, r, what):
+        if r != 0:
+            raise RuntimeError(f"{what} failed: {last_error()}")
+
+    def begin(self, prompt):
+        p = np.ascontiguousarray(prompt, dtype=np.int32)
+        self._chk(self.L.gemma_engine_begin(self.h, _p(p), len(p)), "begin")
+
+    def step(self, n, want_logits=False, use_graph=True):
+        lg = np.zeros((n, self.cfg.n_vocab), dtype=np.float32) if want_logits else None
+        self._chk(self.L.gemma_engine_step(self.h, n, _p(lg) if want_logits else None, 1 if use_graph else 0), "step")
+        return lg
+
+    def tokens(self):
+        out = np.zeros(self.cfg.n_ctx + 1, dtype=np.int32)
+        n = self.L.gemma_engine_tokens(self.h, _p(out), len(out))
+        return out[:n]
+
+    def prefill(self, want_all=False):
+        last = np.zeros(self.cfg.n_vocab, dtype=np.float32)
+        tok = self.L.gemma_engine_prefill(self.h, _p(last), None)
+        if tok < 0:
+            raise RuntimeError("prefill failed: " + last_error())
+        return tok, last
+
+    def tensor(self, tid, nbytes):
+        out = np.zeros(nbytes, dtype=np.uint8)
+        n = self.L.gemma_engine_tensor(self.h, tid, _p(out), nbytes)
+        if n < 0:
+            raise RuntimeError("tensor failed: " + last_error())
+        return out[:n]
+
+    def time_kernel(self, which, iters):
+        b = C.c_double()
+        us = self.L.gemma_engine_time(self.h, which, iters, C.byref(b))
+        if us < 0:
+            raise RuntimeError("time failed: " + last_error())
+        return us, b.value

@@ -1,0 +1,87 @@
+/*
+ * gemma_hpc.h — the C-ABI drop-in boundary of the MI355X hot path (libgemma_hip.so).
+ *
+ * Plain C types and pointers only; no torch types.  Every entry point names the reference
+ * interface it replaces.  Host side: the reference's forked ggml calls `mul_mat` from
+ * ggml_compute_forward_mul_mat's COMPUTE phase; the performance path keeps the
+ * whole Gemma token on the device (gemma_engine_*, the `hpc_graph_compute` role of SURVEY §8(b)).
+ */
+#ifndef GEMMA_HPC_H
+#define GEMMA_HPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ggml.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- narrow drop-in: replaces src/hpc.h:22-32 / src/hpc.cpp:216-390 ------------------------
+ * Same signature and argument meaning.  dst[(c % ne1)*nb1 + (c / ne1)*nb2 + r*4] =
+ * vec_dot(shared_edge, src0 + r*nb01, wdata + c*row_size) for r < ne01, c < ne11*ne12, with the
+ * dot computed on the GPU in ggml's AVX2 lane order (bit-identical to the CPU path).
+ * src0_type: GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 (wdata = block_q8_0 rows) or GGML_TYPE_F16
+ * (wdata = fp16 rows).  `vec_dot` is accepted for link compatibility and not called.
+ * Quantized src0 is uploaded + re-tiled once and cached by (src0->data, shape) — weights are
+ * immutable for the program's lifetime (src/gemma_model.cpp:24-27); F16 src0 (KV-cache views)
+ * is uploaded on every call.  Errors: no return value (as the reference); the message is kept
+ * for hpc_last_error() and, unless hpc_set_error_mode(0), the process exits(1) like
+ * src/hpc.cpp:163-166 / src/opencl.cpp:13-17.                                                   */
+void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, int64_t ne1, int64_t nb1, int64_t nb2,
+             size_t row_size, int64_t shared_edge, struct ggml_tensor *src0, struct ggml_tensor *src1,
+             struct ggml_tensor *dst, ggml_vec_dot_t vec_dot, enum ggml_type src0_type, const char *wdata);
+
+/* ---- device-dispatch lifecycle: replaces src/opencl.h:22-38 (init_opencl, get_kernel,
+ * create_buffer, enqueue_kernel, wait_queue_finish, release_buffer_in_set) -------------------- */
+int hpc_init(int device);                 /* init_opencl (src/opencl.cpp:350-356); 0 = ok        */
+void hpc_shutdown(void);                  /* frees the weight cache and the device scratch        */
+int hpc_register_weight(const void *host, int type, int64_t ne00, int64_t ne01, size_t nb01);
+int hpc_last_error(char *buf, size_t len);/* length of the last error message (0 = none)          */
+void hpc_set_error_mode(int exit_on_error);
+int hpc_weight_cache_entries(void);
+void hpc_set_matvec_ks(int ks);          /* K-split of the quantized matvec (1/2/4/8; tests) */
+
+/* ---- device-resident Gemma engine (performance path; SURVEY §8(b) hpc_graph_compute role) ---- */
+typedef struct gemma_hip_config {
+    int n_layer, n_embd, n_head, n_head_kv, head_dim, n_ff, n_vocab, n_ctx;
+    int wtype; /* GGML_TYPE_Q4_0 or GGML_TYPE_Q8_0 (all matrices, incl. token_embd/output) */
+    float eps, rope_base;
+    uint64_t seed;
+    int gelu_clamp;
+} gemma_hip_config;
+
+typedef struct gemma_engine gemma_engine;
+
+gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int device);
+void gemma_engine_free(gemma_engine *e);
+/* start a sequence: KV cache cleared, prompt stored on the device */
+int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_prompt);
+/* run n steps of the ordered (bit-exact) per-token pass starting at the current position;
+ * step i processes sequence[pos] and appends the greedy token once the prompt is consumed.
+ * logits (n_vocab floats per step) are copied out when logits != NULL. use_graph: replay a
+ * captured hipGraph per step (no host sync between steps when logits == NULL). */
+int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_graph);
+int gemma_engine_tokens(gemma_engine *e, int32_t *out, int cap); /* sequence so far; returns len */
+int gemma_engine_pos(gemma_engine *e);
+/* batched prefill on MFMA (tolerance path): processes the whole prompt,
+ * writes the last row's logits (and all rows if logits_all), returns the greedy token */
+int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *logits_all);
+/* weights back in ggml row-major layout (tests); tid as in DESIGN.md §Synthetic weights */
+int64_t gemma_engine_tensor(gemma_engine *e, int tid, void *dst, int64_t cap);
+/* time `iters` launches of one hot kernel with hipEvents on the engine stream; returns avg µs and
+ * the algorithmic bytes (or int-ops) per launch.  which: 0 = ffn gate/up matvec, 1 = ffn down,
+ * 2 = qkv, 3 = attn out, 4 = output/logits, 5 = whole decode step (graph) */
+double gemma_engine_time(gemma_engine *e, int which, int iters, double *algo_bytes);
+int gemma_engine_sync(gemma_engine *e);
+/* debugging: one eager step with per-layer taps [n_layer][qkv | attn_out | layer_out] */
+int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
+/* per-op test entry: one decode-attention block on host buffers (caches updated in place) */
+int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos, int H, int Hkv, int hd, int ctx,
+                           float rope_base, float *out, float *dbg_w, uint16_t *dbg_p, float *dbg_inv);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,143 @@
+"""GPU parity: the HIP hot path (libgemma_hip.so, through the C-ABI) against the CPU oracle.
+
+Bar: bit-exact for the ordered decode path and for the `mul_mat` drop-in —
+integer block sums are exact and every fp32 operation is performed in the oracle's order.
+"""
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+
+gpu = pytest.mark.gpu
+
+
+def _engine(shape, **kw):
+    import gemma_hip as G
+    return G.Engine(shape, **kw)
+
+
+TIDS_TINY = [0, 1] + [16 + il * 16 + k for il in range(2) for k in range(9)]
+
+
+@gpu
+@pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
+def test_synthetic_weights_match_oracle(wtype):
+    m = O.Model(O.make_config(O.TINY, n_ctx=128, wtype=wtype))
+    e = _engine(O.TINY, n_ctx=128, wtype=wtype)
+    for tid in TIDS_TINY:
+        ref = m.tensor(tid)
+        got = e.tensor(tid, ref.size)
+        assert got.size == ref.size, tid
+        assert np.array_equal(got, ref), f"tensor {tid} differs"
+
+
+def _check_decode(shape, n_prompt, n_decode, n_ctx, wtype=O.Q4_0, use_graph=True):
+    m = O.Model(O.make_config(shape, n_ctx=n_ctx, wtype=wtype))
+    prompt = O.make_prompt(n_prompt, shape["n_vocab"])
+    seq_ref, lg_ref = m.generate(prompt, n_decode)
+    e = _engine(shape, n_ctx=n_ctx, wtype=wtype)
+    e.begin(prompt)
+    lg = e.step(n_prompt + n_decode, want_logits=True, use_graph=use_graph)
+    toks = e.tokens()
+    assert list(toks[: len(seq_ref)]) == list(seq_ref)
+    got = lg[n_prompt - 1:]
+    assert got.shape == lg_ref.shape
+    bad = np.argwhere(got.view(np.uint32) != lg_ref.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} logits differ, first {bad[:5]} max abs {np.abs(got - lg_ref).max()}"
+
+
+@gpu
+@pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_decode_tiny_bitexact(wtype, use_graph):
+    _check_decode(O.TINY, n_prompt=7, n_decode=40, n_ctx=128, wtype=wtype, use_graph=use_graph)
+
+
+@gpu
+def test_decode_tiny_gqa_bitexact():
+    shape = dict(O.TINY, n_head=4, n_head_kv=2, n_embd=1024)
+    _check_decode(shape, n_prompt=5, n_decode=12, n_ctx=64)
+
+
+@gpu
+def test_decode_gemma2b_bitexact():
+    O.lib().orc_set_threads(16)
+    _check_decode(O.GEMMA_2B, n_prompt=6, n_decode=4, n_ctx=256)
+
+
+def _rand_f32(rng, *shape, scale=1.0):
+    return (rng.standard_normal(shape) * scale).astype(np.float32)
+
+
+@gpu
+@pytest.mark.parametrize("ks", [1, 2, 4, 8])
+@pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
+@pytest.mark.parametrize("rows,k,ncols", [(8, 256, 1), (2048, 2048, 1), (256, 16384, 1), (40, 96, 3), (1000, 2048, 5),
+                                          (13, 64, 2)])
+def test_mul_mat_quant_bitexact(wtype, rows, k, ncols, ks):
+    import gemma_hip as G
+    rng = np.random.default_rng(rows * 7 + k + ncols)
+    W = O.quantize(_rand_f32(rng, rows, k, scale=0.05), "q4_0_ref" if wtype == O.Q4_0 else "q8_0_ref")
+    X = _rand_f32(rng, ncols, k)
+    wdata, rs = O.mul_mat_init(wtype, X)
+    ref = O.mul_mat(W, wtype, rows, W.shape[1], k, wdata, rs, ncols)
+    G.lib().hpc_set_error_mode(0)
+    G.lib().hpc_set_matvec_ks(ks)
+    try:
+        got = G.mul_mat(W, wtype, rows, W.shape[1], k, wdata, rs, ncols)
+    finally:
+        G.lib().hpc_set_matvec_ks(1)
+    bad = np.argwhere(got.view(np.uint32) != ref.view(np.uint32))
+    assert bad.size == 0, (len(bad), bad[:8], np.abs(got - ref).max())
+
+
+@gpu
+@pytest.mark.parametrize("rows,k,ncols", [(64, 256, 8), (256, 96, 16), (33, 512, 3), (512, 256, 1)])
+def test_mul_mat_f16_bitexact(rows, k, ncols):
+    import gemma_hip as G
+    rng = np.random.default_rng(rows + k)
+    src0 = O.fp32_to_fp16_bits(_rand_f32(rng, rows * k)).reshape(rows, k)
+    X = _rand_f32(rng, ncols, k)
+    wdata, rs = O.mul_mat_init(O.F16, X)
+    ref = O.mul_mat(src0, O.F16, rows, k * 2, k, wdata, rs, ncols)
+    got = G.mul_mat(src0, O.F16, rows, k * 2, k, wdata, rs, ncols)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+
+
+@gpu
+def test_mul_mat_dst_strides_and_cache():
+    """ggml dst addressing (c % ne1)*nb1 + (c / ne1)*nb2 (src/hpc.cpp:22-37) and the weight cache."""
+    import gemma_hip as G
+    rng = np.random.default_rng(5)
+    rows, k, ne1, ne12 = 24, 128, 3, 2
+    W = O.quantize(_rand_f32(rng, rows, k, scale=0.1), "q4_0_ref")
+    X = _rand_f32(rng, ne1 * ne12, k)
+    wdata, rs = O.mul_mat_init(O.Q4_0, X)
+    ref = O.mul_mat(W, O.Q4_0, rows, W.shape[1], k, wdata, rs, ne1 * ne12)
+    nb1 = rows * 4 + 16          # padded rows in dst
+    nb2 = nb1 * ne1 + 64
+    n0 = G.lib().hpc_weight_cache_entries()
+    out = G.mul_mat(W, O.Q4_0, rows, W.shape[1], k, wdata, rs, ne1 * ne12, ne1=ne1, nb1=nb1, nb2=nb2)
+    assert G.lib().hpc_weight_cache_entries() == n0 + 1
+    del out  # mul_mat helper returns a packed view; check the raw strided buffer below
+    import ctypes as C
+    dst = np.zeros(nb2 * ne12 // 4, dtype=np.float32)
+    t0, t1 = G.GgmlTensor(), G.GgmlTensor()
+    t0.data = W.ctypes.data
+    t1.data = dst.ctypes.data
+    G.lib().mul_mat(rows, ne1, ne12, W.shape[1], ne1, nb1, nb2, rs, k, C.byref(t0), None, C.byref(t1), None, O.Q4_0,
+                    wdata.ctypes.data_as(C.c_void_p))
+    for c in range(ne1 * ne12):
+        off = ((c % ne1) * nb1 + (c // ne1) * nb2) // 4
+        assert np.array_equal(dst[off:off + rows].view(np.uint32), ref[c].view(np.uint32))
+    assert G.lib().hpc_weight_cache_entries() == n0 + 1  # cached: no second upload
+
+
+@gpu
+def test_unsupported_type_reports_error():
+    import gemma_hip as G
+    G.lib().hpc_set_error_mode(0)
+    src = np.zeros(1024, dtype=np.uint8)
+    w = np.zeros(1024, dtype=np.uint8)
+    G.mul_mat(src, 12, 4, 144, 256, w, 292, 1)  # GGML_TYPE_Q4_K: not on this path yet
+    assert "kernel is null" in G.last_error()
