@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""bench.py — decode (and prefill) throughput of the MI355X hot path, BASELINE config 2.
+
+One *step* = one greedy decode token of Gemma-2B Q4_0 at batch 1 through the device-resident engine
+(all 18 layers: fused norm+quantize+matvec kernels, decode attention, logits+argmax, token feedback;
+one hipGraph replay), after a 128-token synthetic prompt.  Weights are synthetic (seeded, Gemma-2B
+shapes, generated on the GPU; DESIGN.md §Synthetic weights) — no checkpoint is available offline.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--profile-out PATH]
+
+N > 1: one process per GPU (torch.distributed.run), every rank runs its own replica of the
+single-stream decode ("replicas" until the row-split TP engine lands);
+value = tokens over all ranks / max-over-ranks time.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gemma.ggml_amd", "python"))
+
+METRIC = "decode tok/s + prefill tok/s, Gemma-2B Q4_0, 1/2/4/8 MI355X; %HBM roofline"
+GEMMA_2B = dict(n_layer=18, n_embd=2048, n_head=8, n_head_kv=1, head_dim=256, n_ff=16384, n_vocab=256000)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
+KERNEL_NAMES = {0: "ffn gate/up matvec (+norm, +gelu*mul)", 1: "ffn down matvec (+resid)",
+                2: "qkv matvec (+norm)", 3: "attn-out matvec (+resid)", 4: "logits matvec (+argmax)"}
+KERNEL_CALLS_PER_TOKEN = {0: 18, 1: 18, 2: 18, 3: 18, 4: 1}
+
+
+def make_prompt(n, n_vocab, seed=1):
+    """Synthetic prompt: BOS=2 then uniform ids in [3, n_vocab) (DESIGN.md §Synthetic inputs)."""
+    M = (1 << 64) - 1
+
+    def sm(x):
+        x = (x + 0x9E3779B97F4A7C15) & M
+        z = x
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    base = sm(seed)
+    return [2] + [3 + sm((base + i) & M) % (n_vocab - 3) for i in range(1, n)]
+
+
+def cpu_baseline(n_prompt=8, n_decode=24, threads=4):
+    """Oracle (CPU restatement of the reference CPU + thread_pool path) on the host cores.
+
+    Bounded sample: Gemma-2B Q4_0 synthetic weights, an n_prompt-token PREFILL (logits for every
+    row, as the reference graph computes them) then n_decode greedy DECODE steps, mul_mat on a
+    `threads`-worker pool (src/macro.h:21 N_THREADS_MUL_MAT_CPU = 4), other ops on one thread."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+    import numpy as np
+    import oracle_ctypes as O
+    cfg = O.make_config(GEMMA_2B, n_ctx=256)
+    m = O.Model(cfg)
+    prompt = np.array(make_prompt(n_prompt, GEMMA_2B["n_vocab"]), dtype=np.int32)
+    toks = np.zeros(n_prompt + n_decode + 2, dtype=np.int32)
+    pre = C.c_double()
+    dec_s = O.lib().orc_bench_run(m.h, O.ptr(prompt), n_prompt, n_decode, threads, O.ptr(toks), C.byref(pre))
+    m.close()
+    return {"value": round(n_decode / dec_s, 3), "unit": "tok/s", "cores": threads, "kind": "port",
+            "sample": f"Gemma-2B Q4_0 synthetic weights, {n_prompt}-token prefill then {n_decode} greedy decode "
+                      f"steps on {threads} mul_mat worker threads (oracle/ restatement of src/hpc.cpp + "
+                      f"src/thread_pool.cpp, AVX2 vec_dot); nproc={os.cpu_count()}",
+            "prefill_tok_s": round(n_prompt / pre.value, 3)}
+
+
+def load_traffic(kernel_id):
+    """HBM bytes per launch of the roofline kernel from the committed PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("per_launch_bytes", {}).get(str(kernel_id))
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--prompt", type=int, default=128)
+    ap.add_argument("--ctx", type=int, default=512)
+    ap.add_argument("--wtype", choices=["q4_0", "q8_0"], default="q4_0")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--kernel-iters", type=int, default=50)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+        dist = dist_mod
+        dist.init_process_group(backend="gloo", init_method="env://")
+    import torch
+
+    import gemma_hip as G
+    wtype = G.GGML_TYPE_Q4_0 if args.wtype == "q4_0" else G.GGML_TYPE_Q8_0
+    if args.prompt + args.warmup + args.steps + 8 >= args.ctx:
+        args.ctx = ((args.prompt + args.warmup + args.steps + 64) // 32 + 1) * 32
+
+    def barrier_sync():
+        torch.cuda.synchronize(local_rank) if torch.cuda.is_available() else None
+        if dist is not None:
+            dist.barrier()
+
+    eng = G.Engine(GEMMA_2B, n_ctx=args.ctx, wtype=wtype, device=local_rank)
+    prompt = make_prompt(args.prompt, GEMMA_2B["n_vocab"])
+    eng.begin(prompt)
+    # prompt pass on the ordered (bit-exact) per-token path; timed as the serial prefill figure
+    t0 = time.perf_counter()
+    eng.step(args.prompt, use_graph=True)
+    prefill_serial_s = time.perf_counter() - t0
+    prefill_tok_s = None
+    eng.step(args.warmup, use_graph=True)
+
+    barrier_sync()
+    t0 = time.perf_counter()
+    eng.step(args.steps, use_graph=True)
+    eng.L.gemma_engine_sync(eng.h)
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # roofline leg: each hot matvec timed alone with hipEvents on the engine stream
+    kern = {}
+    for k in (0, 1, 2, 3, 4):
+        us, algo = eng.time_kernel(k, args.kernel_iters)
+        kern[k] = (us, algo)
+    dominant = max(kern, key=lambda k: kern[k][0] * KERNEL_CALLS_PER_TOKEN[k])
+    us, algo = kern[dominant]
+    achieved = algo / (us * 1e-6) / 1e9
+    traffic = load_traffic(dominant)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            cpu = cpu_baseline()
+        except Exception as ex:  # the CPU baseline is reported, never the target
+            cpu = {"value": None, "error": str(ex)}
+    eng.close()
+
+    if rank == 0:
+        n_tok = args.steps * world
+        line = {
+            "metric": METRIC,
+            "value": round(n_tok / dt, 2),
+            "unit": "tok/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "i8xi8->i32, f32 accumulate (Q4_0 weights x Q8_0 activations)",
+            "data": "synthetic (seeded Gemma-2B-shaped Q4_0 weights generated on device; synthetic prompt)",
+            "config": {"workload": f"Gemma-2B {args.wtype.upper()} greedy decode, batch 1, after a "
+                                   f"{args.prompt}-token prompt (BASELINE config 2); ordered bit-exact path",
+                       "n_ctx": args.ctx, "prompt": args.prompt, "parallelism": f"replicas x{world}"},
+            "decode_tok_s": round(n_tok / dt, 2),
+            "prefill_tok_s": prefill_tok_s,
+            "prefill_serial_tok_s": round(args.prompt / prefill_serial_s, 2),
+            "roofline": {"bound": "hbm", "kernel": KERNEL_NAMES[dominant], "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "avg_us": round(us, 3), "algo_bytes": int(algo)},
+            "kernels_us": {KERNEL_NAMES[k]: round(v[0], 3) for k, v in kern.items()},
+            "token_weight_bytes": 1409679360 if args.wtype == "q4_0" else 2662727680,
+            "cpu_baseline": cpu,
+        }
+        line["token_hbm_frac"] = round(line["token_weight_bytes"] * line["value"] / world / 1e9 / HBM_PEAK_GBS, 4)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -23,3 +23,69 @@ __device__ __forceinline__ float pin(float x) {
 __device__ __forceinline__ uint32_t f2h(float f) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)pin(f)); }
 
 }  // namespace ghip
+
+namespace ghip {
+
+// ---- DPP lane moves (VALU, ~no latency) instead of ds_bpermute shuffles ----------------------
+// dpp_ctrl: quad_perm [1,0,3,2] = xor 1 (0xB1); [2,3,0,1] = xor 2 (0x4E); row_shl:4 = 0x104
+// (lane i reads lane i+4 of its 16-lane row); row_half_mirror = 0x141; row_mirror = 0x140.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+// ggml hsum_float_8 over lanes 8g..8g+7: ((a0+a4)+(a2+a6)) + ((a1+a5)+(a3+a7)); exact pairs.
+// The result is valid in lane 8g (and 8g+1); float addition is commutative bit for bit.
+__device__ __forceinline__ float fold8_dpp(float v) {
+    v = v + dpp_f<0x104>(v);  // lanes 0..3 of each 8-group: a_l + a_{l+4}
+    v = v + dpp_f<0x4E>(v);   // xor 2
+    v = v + dpp_f<0xB1>(v);   // xor 1
+    return v;
+}
+
+// ggml F16 reduce of accumulator rows held by the 4 lanes of a quad: (acc0+acc2) + (acc1+acc3)
+__device__ __forceinline__ float quad_fold_dpp(float v) {
+    v = v + dpp_f<0x4E>(v);  // xor 2
+    v = v + dpp_f<0xB1>(v);  // xor 1
+    return v;
+}
+
+// order-free all-reduce over the 64 lanes (max of floats / sum of u64 pieces)
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    v = fmaxf(v, dpp_f<0x140>(v));
+    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    // integer sum is exact in any order; reduce 32-bit halves with carries via 64-bit adds
+    unsigned long long t;
+    t = ((unsigned long long)dpp_u<0xB1>((uint32_t)(v >> 32)) << 32) | dpp_u<0xB1>((uint32_t)v);
+    v += t;
+    t = ((unsigned long long)dpp_u<0x4E>((uint32_t)(v >> 32)) << 32) | dpp_u<0x4E>((uint32_t)v);
+    v += t;
+    t = ((unsigned long long)dpp_u<0x141>((uint32_t)(v >> 32)) << 32) | dpp_u<0x141>((uint32_t)v);
+    v += t;
+    t = ((unsigned long long)dpp_u<0x140>((uint32_t)(v >> 32)) << 32) | dpp_u<0x140>((uint32_t)v);
+    v += t;
+    unsigned long long s = 0;
+#pragma unroll
+    for (int r = 0; r < 64; r += 16) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, r);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), r);
+        s += ((unsigned long long)hi << 32) | lo;
+    }
+    return s;
+}
+
+}  // namespace ghip

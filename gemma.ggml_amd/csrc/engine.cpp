@@ -243,11 +243,11 @@ static int enqueue_step(gemma_engine *e) {
     o.qs = e->embd.qs; o.sc = e->embd.sc; o.rows = e->embd.rows; o.n_rt = e->embd.n_rt; o.n_bt = e->embd.n_bt;
     o.nb = e->embd.nb;
     o.x = e->x; o.norm_w = e->out_norm; o.eps = c.eps; o.y = e->logits; o.argmax_key = e->key;
-    if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, (int)std::min<int64_t>((e->embd.n_rt + 3) / 4, e->grid_big), s))
-        return -1;
+    const int lg_grid = (int)std::min<int64_t>((e->embd.n_rt + 3) / 4, e->grid_big);
+    if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, lg_grid, s)) return -1;
     // K7: token feedback (greedy_sample -> input.push_back, :282-285), position += 1
     // the prompt is never overwritten: hist writes only land at positions >= n_prompt
-    return launch_advance(e->key, e->token, e->pos, e->hist, c.n_ctx, e->nfix, e->key, s);
+    return launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, s);
 }
 
 extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int device) {
@@ -271,6 +271,7 @@ extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int de
     e->qkv_rows = e->qw + 2 * e->kvw;
     if (const char *v = getenv("GHIP_KS_SMALL")) e->ks_small = atoi(v);
     if (const char *v = getenv("GHIP_KS_DOWN")) e->ks_down = atoi(v);
+    if (const char *v = getenv("GHIP_GRID_BIG")) e->grid_big = atoi(v);
     const int wt = c.wtype;
     const uint64_t seed = c.seed;
     hipStream_t s = e->stream;
@@ -325,12 +326,12 @@ extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int de
     GHIP_FATAL(hipMalloc(&e->sa, (size_t)c.n_embd * 4));
     GHIP_FATAL(hipMalloc(&e->h, (size_t)c.n_ff * 4));
     GHIP_FATAL(hipMalloc(&e->logits, (size_t)c.n_vocab * 4));
-    GHIP_FATAL(hipMalloc(&e->key, 8));
+    GHIP_FATAL(hipMalloc(&e->key, (size_t)e->grid_big * 8));  // per-workgroup argmax keys
     GHIP_FATAL(hipMalloc(&e->pos, 4));
     GHIP_FATAL(hipMalloc(&e->token, 4));
     GHIP_FATAL(hipMalloc(&e->nfix, 4));
     GHIP_FATAL(hipMalloc(&e->hist, (size_t)(c.n_ctx + 1) * 4));
-    GHIP_FATAL(hipMemsetAsync(e->key, 0, 8, s));
+    GHIP_FATAL(hipMemsetAsync(e->key, 0, (size_t)e->grid_big * 8, s));
     GHIP_FATAL(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
     GHIP_FATAL(hipStreamSynchronize(s));
     if (!last_error().empty()) {
@@ -374,7 +375,7 @@ extern "C" int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_
     GHIP_CHECK(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
     GHIP_CHECK(hipMemcpyAsync(e->hist, prompt, (size_t)n_prompt * 4, hipMemcpyHostToDevice, s));
     GHIP_CHECK(hipMemsetAsync(e->pos, 0, 4, s));
-    GHIP_CHECK(hipMemsetAsync(e->key, 0, 8, s));
+    GHIP_CHECK(hipMemsetAsync(e->key, 0, (size_t)e->grid_big * 8, s));
     GHIP_CHECK(hipMemcpyAsync(e->nfix, &n_prompt, 4, hipMemcpyHostToDevice, s));
     GHIP_CHECK(hipStreamSynchronize(s));
     e->n_prompt = n_prompt;
@@ -537,6 +538,7 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
             return -1.0;
     }
     (void)act_q8;
+    if (const char *v = getenv("GHIP_ABLATE")) a.ablate = atoi(v);
     hipEvent_t t0, t1;
     GHIP_FATAL(hipEventCreate(&t0));
     GHIP_FATAL(hipEventCreate(&t1));
@@ -600,7 +602,7 @@ extern "C" int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float 
 // qkv [H*hd + 2*Hkv*hd] f32; kc [ctx][Hkv*hd], vc [Hkv*hd][ctx] f16 (updated in place at pos)
 extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos, int H, int Hkv, int hd,
                                       int ctx, float rope_base, float *out, float *dbg_w, uint16_t *dbg_p,
-                                      float *dbg_inv) {
+                                      float *dbg_inv, unsigned long long *dbg_t) {
     set_error("");
     const size_t qkv_n = (size_t)(H + 2 * Hkv) * hd, cache_n = (size_t)ctx * Hkv * hd;
     std::vector<uint16_t> et, gt;
@@ -611,6 +613,9 @@ extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *
     uint16_t *d_k, *d_v, *d_e;
     int *d_pos;
     float *d_dw = nullptr, *d_di = nullptr;
+    unsigned long long *d_dt = nullptr;
+    const size_t n_stamps = (size_t)H * ((hd + 63) / 64) * 8;
+    if (dbg_t) GHIP_CHECK(hipMalloc(&d_dt, n_stamps * 8));
     uint16_t *d_dp = nullptr;
     if (dbg_w) GHIP_CHECK(hipMalloc(&d_dw, (size_t)H * ctx * 4));
     if (dbg_p) GHIP_CHECK(hipMalloc(&d_dp, (size_t)H * ctx * 2));
@@ -633,8 +638,9 @@ extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *
     attn_args a;
     a.qkv = d_qkv; a.kc = d_k; a.vc = d_v; a.rope_cos = d_c; a.rope_sin = d_s; a.exp_tab = d_e; a.pos = d_pos;
     a.out = d_out; a.H = H; a.Hkv = Hkv; a.hd = hd; a.ctx = ctx; a.q_scale = 1.0f / sqrtf((float)hd);
-    a.dbg_w = d_dw; a.dbg_p = d_dp; a.dbg_inv = d_di;
-    const int r = launch_attn_decode(a, nullptr);
+    a.dbg_w = d_dw; a.dbg_p = d_dp; a.dbg_inv = d_di; a.dbg_t = d_dt;
+    int r = 0;
+    for (int rep = 0; rep < (dbg_t ? 3 : 1) && r == 0; ++rep) r = launch_attn_decode(a, nullptr);
     GHIP_CHECK(hipDeviceSynchronize());
     if (r == 0) {
         GHIP_CHECK(hipMemcpy(out, d_out, (size_t)H * hd * 4, hipMemcpyDeviceToHost));
@@ -643,8 +649,9 @@ extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *
         if (dbg_w) GHIP_CHECK(hipMemcpy(dbg_w, d_dw, (size_t)H * ctx * 4, hipMemcpyDeviceToHost));
         if (dbg_p) GHIP_CHECK(hipMemcpy(dbg_p, d_dp, (size_t)H * ctx * 2, hipMemcpyDeviceToHost));
         if (dbg_inv) GHIP_CHECK(hipMemcpy(dbg_inv, d_di, (size_t)H * 4, hipMemcpyDeviceToHost));
+        if (dbg_t) GHIP_CHECK(hipMemcpy(dbg_t, d_dt, n_stamps * 8, hipMemcpyDeviceToHost));
     }
-    void *bufs[] = {d_qkv, d_out, d_c, d_s, d_k, d_v, d_e, d_pos, d_dw, d_dp, d_di};
+    void *bufs[] = {d_qkv, d_out, d_c, d_s, d_k, d_v, d_e, d_pos, d_dw, d_dp, d_di, d_dt};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     return r;

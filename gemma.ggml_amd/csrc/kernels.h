@@ -40,8 +40,9 @@ struct mv_args {
     const float *resid = nullptr;
     const uint16_t *gelu_tab = nullptr;
     int gelu_clamp = 0;
-    unsigned long long *argmax_key = nullptr;
+    unsigned long long *argmax_key = nullptr;      // EPI_ARGMAX: one partial key per workgroup [grid]
     int ncols = 1;
+    int ablate = 0;  // timing-only ablations (bench): 1 = no prologue, 4 = no carry
 };
 
 // ks: waves that split one row tile's K range (ordered carry hand-off); 1 = one wave per tile.
@@ -69,12 +70,14 @@ struct attn_args {
     float *dbg_w = nullptr;      // optional debug taps: [H][ctx] scores, [H][ctx] fp16 P, [H] inv
     uint16_t *dbg_p = nullptr;
     float *dbg_inv = nullptr;
+    unsigned long long *dbg_t = nullptr;  // diagnostic phase stamps (s_memrealtime), [grid][8]
 };
 int launch_attn_decode(const attn_args &a, hipStream_t s);
 int launch_embed(const uint8_t *qs, const uint8_t *sc, int wtype, int64_t n_bt, const int *token, float scale,
                  float *out, int64_t E, hipStream_t s);
-int launch_advance(const unsigned long long *key, int *token, int *pos, int *hist, int hist_cap, const int *n_fixed,
-                   unsigned long long *key_reset, hipStream_t s);
+// reduces the n_parts per-workgroup argmax keys, appends the token, advances the position
+int launch_advance(const unsigned long long *keys, int n_parts, int *token, int *pos, int *hist, int hist_cap,
+                   const int *n_fixed, hipStream_t s);
 
 // ---- generic ggml-op kernels used by the C-ABI and the ggml-compatible executor ----------------
 int launch_mul_mat_f16(const uint16_t *src0, int64_t nb01_elems, int64_t ne01, const uint16_t *src1,

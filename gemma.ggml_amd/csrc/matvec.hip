@@ -12,8 +12,9 @@
 // butterfly — so results equal the ordered CPU restatement bit for bit.
 //
 // Memory: weights are read once, 16 B per thread per 8-block tile (1 KiB coalesced per wave;
-// DESIGN.md §HBM layout); the activation is quantized once per workgroup in the prologue
-// (optionally fused with RMSNorm and the embedding lookup) and staged in LDS.
+// DESIGN.md §HBM layout) through a U-deep register ring that is filled BEFORE the activation
+// prologue, so the first HBM round trip overlaps the (per-workgroup) RMSNorm + quantization of
+// the activation into LDS.  A wave streams its tiles continuously across row-tile boundaries.
 // K-split (KS > 1): the waves of a workgroup each take a contiguous K segment of the same 8 rows;
 // waves 1..KS-1 stash their exact (d, isum) terms in LDS and the fma chain is carried across the
 // segments in order (wave w continues wave w-1's accumulator), which keeps the AVX2 order.
@@ -28,30 +29,33 @@ __device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) {
 }
 
 // ---- LDS image --------------------------------------------------------------------------------
-// act: Q4_0 -> uint4 [n_bt*4 pairs][8 lanes] = {a_b, -8*sum(a_b), a_b+1, -8*sum(a_b+1)}
-//      Q8_0 -> uint4 [n_bt][8 lanes]        = {a_b0, a_b1, a_b2, a_b3}
-// da:  float [n_bt*BT] (fp32 of the fp16 activation scale)
+// act: uint4 [nb_pad/4][8 lanes] = {a_b, a_b+1, a_b+2, a_b+3} (4 int8 of lane l per block)
+// ns:  uint4 [nb_pad/4][8 lanes] = -8*sum(a) per (block, lane) (Q4_0 only, when NSA; otherwise
+//      recomputed with one more v_dot4 to save LDS)
+// da:  float [nb_pad] (fp32 of the fp16 activation scale)
+// stash (KS > 1): s float [KS-1][64 lanes][SBP], d float [KS-1][8 rows][SBP]  (SBP = seg + 4 pad)
+constexpr int STASH_PAD = 4;
 struct lds_map {
-    size_t act, da, stash_s, stash_d, xfer, red, total;
+    size_t act, ns, da, stash_s, stash_d, red, total;
+    int sbp;
 };
-template <int WT>
+template <int WT, bool NSA>
 __host__ __device__ inline lds_map make_lds_map(int ks, int64_t n_bt, int64_t seg_tiles) {
     constexpr int BT = wfmt<WT>::BT;
     lds_map m;
+    const size_t nb_pad = (size_t)n_bt * BT;
     m.act = 0;
-    const size_t act_bytes = WT == T_Q4_0 ? (size_t)n_bt * 4 * 8 * 16 : (size_t)n_bt * 8 * 16;
-    m.da = act_bytes;
-    size_t off = m.da + (size_t)n_bt * BT * 4;
+    size_t off = nb_pad / 4 * 8 * 16;
+    m.ns = off;
+    if (WT == T_Q4_0 && NSA) off += nb_pad / 4 * 8 * 16;
+    m.da = off;
+    off += nb_pad * 4;
     off = (off + 15) & ~(size_t)15;
-    const size_t seg_blocks = (size_t)seg_tiles * BT;
-    const size_t s_elem = WT == T_Q4_0 ? 2 : 4;
+    m.sbp = (int)(seg_tiles * BT) + STASH_PAD;
     m.stash_s = off;
-    off += (ks > 1 ? (size_t)(ks - 1) * seg_blocks * 64 * s_elem : 0);
-    off = (off + 15) & ~(size_t)15;
+    off += ks > 1 ? (size_t)(ks - 1) * 64 * m.sbp * 4 : 0;
     m.stash_d = off;
-    off += (ks > 1 ? (size_t)(ks - 1) * seg_blocks * 8 * 4 : 0);
-    m.xfer = off;
-    off += 2 * 64 * 4;
+    off += ks > 1 ? (size_t)(ks - 1) * 8 * m.sbp * 4 : 0;
     m.red = off;
     off += 64 * 8;
     m.total = off;
@@ -59,37 +63,36 @@ __host__ __device__ inline lds_map make_lds_map(int ks, int64_t n_bt, int64_t se
 }
 
 // ---- prologue: build the Q8_0 activation image in LDS (quantize_row_q8_0) ------
-// Writes block b (32 values v[0..31]) in the layout above.  amax, d = amax/127 (fp16 RNE),
-// id = amax ? 127/amax : 0, q = rint(v*id) — identical to oracle orc_quantize_row_q8_0.
-template <int WT>
-__device__ __forceinline__ void put_block(uint8_t *smem, const lds_map &m, int64_t b, const float *v) {
+// A quad of threads owns one block: thread q holds elements 8q..8q+7 (= AVX2 lanes 2q, 2q+1).
+// amax = max|v|; d = amax/127 (fp16 RNE); id = amax ? 127/amax : 0; q = rint(v*id) — identical
+// to oracle orc_quantize_row_q8_0.
+template <int WT, bool NSA>
+__device__ __forceinline__ void put_quad(uint8_t *smem, const lds_map &m, int64_t b, int q, const float v[8]) {
     float amax = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    amax = fmaxf(amax, __shfl_xor(amax, 1));
+    amax = fmaxf(amax, __shfl_xor(amax, 2));
     const float d = amax / 127.f;
     const uint32_t d16 = f2h(d);
     const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
     uint32_t *act = (uint32_t *)(smem + m.act);
 #pragma unroll
-    for (int l = 0; l < 8; ++l) {
-        int q[4];
+    for (int h = 0; h < 2; ++h) {
+        const int l = 2 * q + h;
+        int qi[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = (int)__builtin_rintf(v[4 * l + k] * id);
-        const uint32_t packed = (uint32_t)(q[0] & 0xFF) | ((uint32_t)(q[1] & 0xFF) << 8) |
-                                ((uint32_t)(q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
-        if (WT == T_Q4_0) {
-            const int nsa = -8 * (q[0] + q[1] + q[2] + q[3]);
-            const int64_t base = ((b >> 1) * 8 + l) * 4 + (b & 1) * 2;
-            act[base] = packed;
-            act[base + 1] = (uint32_t)nsa;
-        } else {
-            act[((b >> 2) * 8 + l) * 4 + (b & 3)] = packed;
-        }
+        for (int k = 0; k < 4; ++k) qi[k] = (int)__builtin_rintf(v[4 * h + k] * id);
+        const uint32_t packed = (uint32_t)(qi[0] & 0xFF) | ((uint32_t)(qi[1] & 0xFF) << 8) |
+                                ((uint32_t)(qi[2] & 0xFF) << 16) | ((uint32_t)(qi[3] & 0xFF) << 24);
+        const int64_t idx = ((b >> 2) * 8 + l) * 4 + (b & 3);
+        act[idx] = packed;
+        if (WT == T_Q4_0 && NSA) ((uint32_t *)(smem + m.ns))[idx] = (uint32_t)(-8 * (qi[0] + qi[1] + qi[2] + qi[3]));
     }
-    ((float *)(smem + m.da))[b] = h2f(d16);
+    if (q == 0) ((float *)(smem + m.da))[b] = h2f(d16);
 }
 
-template <int WT>
+template <int WT, bool NSA>
 __device__ __forceinline__ void put_block_q8(uint8_t *smem, const lds_map &m, int64_t b, const block_q8_0 *blk) {
     const uint8_t *p = (const uint8_t *)blk;
     const uint32_t d16 = (uint32_t)p[0] | ((uint32_t)p[1] << 8);
@@ -101,13 +104,9 @@ __device__ __forceinline__ void put_block_q8(uint8_t *smem, const lds_map &m, in
         for (int k = 0; k < 4; ++k) q[k] = (int)(int8_t)p[2 + 4 * l + k];
         const uint32_t packed = (uint32_t)(q[0] & 0xFF) | ((uint32_t)(q[1] & 0xFF) << 8) |
                                 ((uint32_t)(q[2] & 0xFF) << 16) | ((uint32_t)(q[3] & 0xFF) << 24);
-        if (WT == T_Q4_0) {
-            const int64_t base = ((b >> 1) * 8 + l) * 4 + (b & 1) * 2;
-            act[base] = packed;
-            act[base + 1] = (uint32_t)(-8 * (q[0] + q[1] + q[2] + q[3]));
-        } else {
-            act[((b >> 2) * 8 + l) * 4 + (b & 3)] = packed;
-        }
+        const int64_t idx = ((b >> 2) * 8 + l) * 4 + (b & 3);
+        act[idx] = packed;
+        if (WT == T_Q4_0 && NSA) ((uint32_t *)(smem + m.ns))[idx] = (uint32_t)(-8 * (q[0] + q[1] + q[2] + q[3]));
     }
     ((float *)(smem + m.da))[b] = h2f(d16);
 }
@@ -133,41 +132,94 @@ __device__ __forceinline__ float emb_value(const uint8_t *qs, const uint8_t *sc,
 }
 
 template <int WT, int PRO>
-__device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const lds_map &m) {
+__device__ __forceinline__ void load8(const mv_args &a, const float *x, int64_t tok, int64_t i0, float v[8]) {
+    if (PRO == PRO_EMBED) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t i = i0 + j;
+            // ggml_get_rows then ggml_scale (src/gemma_model.cpp:677-679)
+            v[j] = emb_value<WT>(a.emb_qs, a.emb_sc, a.emb_n_bt, tok, i >> 5, (int)(i & 31)) * a.emb_scale;
+        }
+    } else {
+        const float4 u = *(const float4 *)(x + i0), w = *(const float4 *)(x + i0 + 4);
+        v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
+    }
+}
+
+// Activation values for the first R blocks of each quad, loaded into registers BEFORE the weight
+// ring is filled (vmcnt retires in issue order: loads issued after the ring would wait for it).
+template <int R>
+struct act_regs {
+    float x[R][8];
+    float w[R][8];
+};
+
+template <int WT, int PRO, int R>
+__device__ __forceinline__ void prefetch_activation(const mv_args &a, int col, act_regs<R> &r) {
+    if (PRO != PRO_F32 && PRO != PRO_NORM) return;
+    const int tid = threadIdx.x, q = tid & 3, nquads = blockDim.x >> 2;
+    const float *x = (const float *)((const uint8_t *)a.x + (int64_t)col * a.x_col_stride);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int64_t b = (tid >> 2) + (int64_t)i * nquads;
+        const int64_t bb = b < a.nb ? b : 0;  // clamp instead of branching around the load
+        load8<WT, PRO_F32>(a, x, 0, bb * 32 + q * 8, r.x[i]);
+        if (PRO == PRO_NORM) {
+            const float4 w0 = *(const float4 *)(a.norm_w + bb * 32 + q * 8);
+            const float4 w1 = *(const float4 *)(a.norm_w + bb * 32 + q * 8 + 4);
+            r.w[i][0] = w0.x; r.w[i][1] = w0.y; r.w[i][2] = w0.z; r.w[i][3] = w0.w;
+            r.w[i][4] = w1.x; r.w[i][5] = w1.y; r.w[i][6] = w1.z; r.w[i][7] = w1.w;
+        }
+    }
+}
+
+template <int WT, int PRO, int R, bool NSA>
+__device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const lds_map &m, const act_regs<R> &r) {
     constexpr int BT = wfmt<WT>::BT;
+    constexpr bool CACHED = PRO == PRO_F32 || PRO == PRO_NORM;
     const int tid = threadIdx.x, nth = blockDim.x;
     const int64_t nb = a.nb, nb_pad = a.n_bt * BT;
-    // zero the padded tail blocks (their d = 0 makes every chain step an exact no-op)
-    for (int64_t b = nb + tid; b < nb_pad; b += nth) {
-        float z[32];
-#pragma unroll
-        for (int j = 0; j < 32; ++j) z[j] = 0.0f;
-        put_block<WT>(smem, m, b, z);
+    const int q = tid & 3;
+    const int nquads = nth >> 2;
+    // padded tail blocks: zero (d = 0 makes every chain step an exact no-op)
+    for (int64_t b = nb + (tid >> 2); b < nb_pad; b += nquads) {
+        float z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        put_quad<WT, NSA>(smem, m, b, q, z);
     }
     if (PRO == PRO_Q8) {
         const block_q8_0 *xb = (const block_q8_0 *)((const uint8_t *)a.x + (int64_t)col * a.x_col_stride);
-        for (int64_t b = tid; b < nb; b += nth) put_block_q8<WT>(smem, m, b, xb + b);
+        for (int64_t b = tid; b < nb; b += nth) put_block_q8<WT, NSA>(smem, m, b, xb + b);
         return;
     }
-    // f32 source (PRO_F32 / PRO_NORM) or dequantized embedding row (PRO_EMBED)
     const float *x = (const float *)((const uint8_t *)a.x + (int64_t)col * a.x_col_stride);
     int64_t tok = 0;
     if (PRO == PRO_EMBED) tok = ((const int *)a.x)[*a.tok_pos];
-    auto load = [&](int64_t i) -> float {
-        if (PRO == PRO_EMBED) {
-            const float v = emb_value<WT>(a.emb_qs, a.emb_sc, a.emb_n_bt, tok, i >> 5, (int)(i & 31));
-            return v * a.emb_scale;   // ggml_get_rows then ggml_scale (src/gemma_model.cpp:677-679)
+    // value of block (tid>>2) + i*nquads: from registers when cached, else loaded now
+    auto get = [&](int i, int64_t b, float v[8]) {
+        if (CACHED && i < R) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = r.x[i < R ? i : 0][j];
+        } else {
+            load8<WT, PRO>(a, x, tok, b * 32 + q * 8, v);
         }
-        return x[i];
     };
     float scale = 1.0f;
     if (PRO == PRO_NORM || PRO == PRO_EMBED) {
-        // rms_norm: double sum of fp32 squares, fixed-order tree
+        // rms_norm: double sum of fp32 squares; fixed-order tree
         double part = 0.0;
-        for (int64_t i = tid; i < nb * 32; i += nth) {
-            const float v = load(i);
-            const float sq = v * v;
-            part += (double)sq;
+        int i = 0;
+        for (int64_t b = tid >> 2; b < nb; b += nquads, ++i) {
+            float v[8];
+            get(i, b, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float sq = v[j] * v[j];
+                part += (double)sq;
+            }
+            if (PRO == PRO_EMBED && a.emb_out && blockIdx.x == 0 && col == 0) {
+                *(float4 *)(a.emb_out + b * 32 + q * 8) = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4 *)(a.emb_out + b * 32 + q * 8 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
         }
         double *red = (double *)(smem + m.red);
 #pragma unroll
@@ -178,74 +230,101 @@ __device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const
         for (int w = 0; w < nth / 64; ++w) sum += red[w];
         const float mean = (float)(sum / (double)(nb * 32));
         scale = 1.0f / sqrtf(mean + a.eps);
-        __syncthreads();
-        if (PRO == PRO_EMBED && a.emb_out && blockIdx.x == 0 && col == 0)
-            for (int64_t i = tid; i < nb * 32; i += nth) a.emb_out[i] = load(i);
     }
-    for (int64_t b = tid; b < nb; b += nth) {
-        float v[32];
+    int i = 0;
+    for (int64_t b = tid >> 2; b < nb; b += nquads, ++i) {
+        float v[8];
+        get(i, b, v);
+        if (PRO == PRO_NORM || PRO == PRO_EMBED) {
+            float wv[8];
+            if (PRO == PRO_NORM && i < R) {
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            float t = load(b * 32 + j);
-            if (PRO == PRO_NORM || PRO == PRO_EMBED) {
-                t = t * scale;            // rms_norm output
-                t = t * a.norm_w[b * 32 + j];  // ggml_mul by the norm weight
+                for (int j = 0; j < 8; ++j) wv[j] = r.w[i < R ? i : 0][j];
+            } else {
+                const float4 w0 = *(const float4 *)(a.norm_w + b * 32 + q * 8);
+                const float4 w1 = *(const float4 *)(a.norm_w + b * 32 + q * 8 + 4);
+                wv[0] = w0.x; wv[1] = w0.y; wv[2] = w0.z; wv[3] = w0.w;
+                wv[4] = w1.x; wv[5] = w1.y; wv[6] = w1.z; wv[7] = w1.w;
             }
-            v[j] = t;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float t = v[j] * scale;  // rms_norm output
+                v[j] = t * wv[j];              // ggml_mul by the norm weight
+            }
         }
-        put_block<WT>(smem, m, b, v);
+        put_quad<WT, NSA>(smem, m, b, q, v);
     }
 }
 
 // ---- one 8-row x BT-block tile for this thread's (row rr, lane l) ----------------------------
-// STASH: write the exact (d, isum) terms instead of accumulating (K-split waves 1..KS-1)
-template <int WT, bool STASH>
+// d = f32(dw) * da with the fp16 operand converted inside v_fma_mix_f32 (addend +0: the sign of a
+// zero d never reaches the result, since fmaf(+-0, s, acc) == acc for the accumulators here).
+__device__ __forceinline__ float mix_lo(uint32_t h2, float y) {
+    float d;
+    asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(h2), "v"(y));
+    return d;
+}
+__device__ __forceinline__ float mix_hi(uint32_t h2, float y) {
+    float d;
+    asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(h2), "v"(y));
+    return d;
+}
+
+// STASH: store the exact (d, (float)isum) terms for the carry instead of accumulating
+template <int WT, bool STASH, bool NSA>
 __device__ __forceinline__ float tile_dot(uint4 q, uint4 scv, const uint8_t *smem, const lds_map &m, int64_t bt, int l,
-                                          float acc, int16_t *st_s, int32_t *st_s32, float *st_d, int j0, int rr,
-                                          int lane) {
+                                          float acc, float *st_s, float *st_d, int j0) {
     const float *da = (const float *)(smem + m.da);
+    const uint4 *act = (const uint4 *)(smem + m.act);
     const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
     if (WT == T_Q4_0) {
-        const uint4 *act = (const uint4 *)(smem + m.act);
+        const uint4 A0 = act[(bt * 2) * 8 + l], A1 = act[(bt * 2 + 1) * 8 + l];
+        const uint32_t av[8] = {A0.x, A0.y, A0.z, A0.w, A1.x, A1.y, A1.z, A1.w};
+        uint32_t nv[8];
+        if (NSA) {
+            const uint4 *ns = (const uint4 *)(smem + m.ns);
+            const uint4 N0 = ns[(bt * 2) * 8 + l], N1 = ns[(bt * 2 + 1) * 8 + l];
+            nv[0] = N0.x; nv[1] = N0.y; nv[2] = N0.z; nv[3] = N0.w; nv[4] = N1.x; nv[5] = N1.y; nv[6] = N1.z; nv[7] = N1.w;
+        }
         const float4 DA0 = *(const float4 *)(da + bt * 8), DA1 = *(const float4 *)(da + bt * 8 + 4);
         const float dav[8] = {DA0.x, DA0.y, DA0.z, DA0.w, DA1.x, DA1.y, DA1.z, DA1.w};
         const uint32_t sv[4] = {scv.x, scv.y, scv.z, scv.w};
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const uint4 A = act[(bt * 4 + p) * 8 + l];
             const uint32_t lo = qv[p] & 0x0F0F0F0Fu, hi = (qv[p] >> 4) & 0x0F0F0F0Fu;
-            const int s0 = sdot4(lo, A.x, (int)A.y);
-            const int s1 = sdot4(hi, A.z, (int)A.w);
-            const float d0 = h2f(sv[p]) * dav[2 * p];
-            const float d1 = h2f(sv[p] >> 16) * dav[2 * p + 1];
+            // sum((nib - 8) * a) = sum(nib * a) - 8 * sum(a), exact in int32
+            const int n0 = NSA ? (int)nv[2 * p] : sdot4(av[2 * p], 0xF8F8F8F8u, 0);
+            const int n1 = NSA ? (int)nv[2 * p + 1] : sdot4(av[2 * p + 1], 0xF8F8F8F8u, 0);
+            const int s0 = sdot4(lo, av[2 * p], n0);
+            const int s1 = sdot4(hi, av[2 * p + 1], n1);
+            const float d0 = mix_lo(sv[p], dav[2 * p]);
+            const float d1 = mix_hi(sv[p], dav[2 * p + 1]);
             if (STASH) {
-                st_s[(j0 + 2 * p) * 64 + lane] = (int16_t)s0;
-                st_s[(j0 + 2 * p + 1) * 64 + lane] = (int16_t)s1;
-                if (l == 0) {
-                    st_d[(j0 + 2 * p) * 8 + rr] = d0;
-                    st_d[(j0 + 2 * p + 1) * 8 + rr] = d1;
-                }
+                *(float2 *)(st_s + j0 + 2 * p) = make_float2((float)s0, (float)s1);
+                if (l == 0) *(float2 *)(st_d + j0 + 2 * p) = make_float2(d0, d1);
             } else {
                 acc = __builtin_fmaf(d0, (float)s0, acc);
                 acc = __builtin_fmaf(d1, (float)s1, acc);
             }
         }
     } else {
-        const uint4 A = ((const uint4 *)(smem + m.act))[bt * 8 + l];
+        const uint4 A = act[bt * 8 + l];
         const uint32_t av[4] = {A.x, A.y, A.z, A.w};
         const float4 DA = *(const float4 *)(da + bt * 4);
         const float dav[4] = {DA.x, DA.y, DA.z, DA.w};
-        const uint32_t sv[4] = {scv.x & 0xFFFF, scv.x >> 16, scv.y & 0xFFFF, scv.y >> 16};
+        const uint32_t sv[2] = {scv.x, scv.y};
+        float dd[4], ss[4];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int s = sdot4(qv[p], av[p], 0);
-            const float d = h2f(sv[p]) * dav[p];
-            if (STASH) {
-                st_s32[(j0 + p) * 64 + lane] = s;
-                if (l == 0) st_d[(j0 + p) * 8 + rr] = d;
-            } else {
-                acc = __builtin_fmaf(d, (float)s, acc);
-            }
+            const float d = (p & 1) ? mix_hi(sv[p >> 1], dav[p]) : mix_lo(sv[p >> 1], dav[p]);
+            dd[p] = d;
+            ss[p] = (float)s;
+            if (!STASH) acc = __builtin_fmaf(d, (float)s, acc);
+        }
+        if (STASH) {
+            *(float4 *)(st_s + j0) = make_float4(ss[0], ss[1], ss[2], ss[3]);
+            if (l == 0) *(float4 *)(st_d + j0) = make_float4(dd[0], dd[1], dd[2], dd[3]);
         }
     }
     return acc;
@@ -256,41 +335,6 @@ __device__ __forceinline__ uint4 load_scale(const uint8_t *sc, int64_t tile, int
     if (WT == T_Q4_0) return ((const uint4 *)sc)[tile * 8 + rr];
     const uint2 v = ((const uint2 *)sc)[tile * 8 + rr];
     return make_uint4(v.x, v.y, 0, 0);
-}
-
-// chain over block tiles [bt0, bt1) of row tile rt, 4-deep register prefetch
-template <int WT, bool STASH>
-__device__ __forceinline__ float run_chain(const uint8_t *qs, const uint8_t *sc, int64_t n_bt, int64_t rt, int64_t bt0,
-                                           int64_t bt1, const uint8_t *smem, const lds_map &m, float acc, int lane,
-                                           int16_t *st_s, int32_t *st_s32, float *st_d) {
-    constexpr int BT = wfmt<WT>::BT;
-    constexpr int U = 4;
-    const int rr = lane >> 3, l = lane & 7;
-    const int64_t base = rt * n_bt + bt0;
-    const uint4 *q = (const uint4 *)qs + base * 64 + lane;
-    const int n = (int)(bt1 - bt0);
-    uint4 qb[U], sb[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-        if (u < n) {
-            qb[u] = q[(int64_t)u * 64];
-            sb[u] = load_scale<WT>(sc, base + u, rr);
-        }
-    for (int i = 0; i < n; i += U) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (i + u < n) {
-                const uint4 qc = qb[u], scc = sb[u];
-                if (i + u + U < n) {
-                    qb[u] = q[(int64_t)(i + u + U) * 64];
-                    sb[u] = load_scale<WT>(sc, base + i + u + U, rr);
-                }
-                acc = tile_dot<WT, STASH>(qc, scc, smem, m, bt0 + i + u, l, acc, st_s, st_s32, st_d, (i + u) * BT, rr,
-                                          lane);
-            }
-        }
-    }
-    return acc;
 }
 
 // ordered fold of the 8 lanes (hsum_float_8): xor 4, then 2, then 1
@@ -320,7 +364,7 @@ __device__ __forceinline__ void epilogue(const mv_args &a, int col, int64_t row,
     float *y = a.y + (int64_t)col * a.y_col_stride;
     if (EPI == EPI_STORE) y[row] = v;
     if (EPI == EPI_ADD) y[row] = v + a.resid[(int64_t)col * a.y_col_stride + row];
-    if (EPI == EPI_GELU_MUL) y[row] = gelu_tab(a, v) * vb;
+    if (EPI == EPI_GELU_MUL) y[row] = gelu_tab(a, v) * vb;  // gelu(gate) then ggml_mul by up
     if (EPI == EPI_ARGMAX) {
         y[row] = v;
         const unsigned long long k = argmax_key(v, row);
@@ -328,87 +372,174 @@ __device__ __forceinline__ void epilogue(const mv_args &a, int col, int64_t row,
     }
 }
 
-template <int WT, int KS, int PRO, int EPI>
+// ---- the tile stream: a wave's sequence of (matrix, row tile, block tile) items ----------------
+// item k -> row tile rt0 + (k / per_rt) * rstride; within it matrix (k % per_rt) / nbt and block
+// tile bt0 + (k % per_rt) % nbt.  Cursors advance incrementally (no divisions in the loop).
+struct cursor {
+    int64_t rt;
+    int m;
+    int bt;
+};
+
+template <int WT, int KS, int PRO, int EPI, int U, int R, bool NSA>
 __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int BT = wfmt<WT>::BT;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int BT = wfmt<WT>::BT, SB = wfmt<WT>::SCALE_BYTES;
+    constexpr int NM = EPI == EPI_GELU_MUL ? 2 : 1;  // matrices per row tile (gate, up)
+    // readfirstlane: makes the wave index (and every cursor derived from it) provably uniform, so
+    // the stream bookkeeping lives in SGPRs and its branches are scalar (cdna_hip_programming T20)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rr = lane >> 3, l = lane & 7;
     const int col = blockIdx.y;
     const int64_t seg_tiles = KS > 1 ? a.n_bt / KS : a.n_bt;
-    const lds_map m = make_lds_map<WT>(KS, a.n_bt, seg_tiles);
-    build_activation<WT, PRO>(a, col, smem, m);
-    __syncthreads();
-    unsigned long long best = 0;
-    const int rr = lane >> 3;
-
+    const lds_map m = make_lds_map<WT, NSA>(KS, a.n_bt, seg_tiles);
+    const int nbt = (int)seg_tiles;
+    const int bt0 = KS > 1 ? wave * nbt : 0;
+    // this wave's row tiles
+    int64_t rt0, rstride;
     if (KS == 1) {
         const int nw = blockDim.x >> 6;
-        for (int64_t rt = (int64_t)blockIdx.x * nw + wave; rt < a.n_rt; rt += (int64_t)gridDim.x * nw) {
-            float acc = run_chain<WT, false>(a.qs, a.sc, a.n_bt, rt, 0, a.n_bt, smem, m, 0.0f, lane, nullptr, nullptr,
-                                             nullptr);
-            const float v = fold8(acc);
-            float vb = 0.0f;
-            if (EPI == EPI_GELU_MUL) {
-                float accb = run_chain<WT, false>(a.qs2, a.sc2, a.n_bt, rt, 0, a.n_bt, smem, m, 0.0f, lane, nullptr,
-                                                  nullptr, nullptr);
-                vb = fold8(accb);
-            }
-            if ((lane & 7) == 0) epilogue<EPI>(a, col, rt * 8 + rr, v, vb, best);
-        }
+        rt0 = (int64_t)blockIdx.x * nw + wave;
+        rstride = (int64_t)gridDim.x * nw;
     } else {
-        float *xfer = (float *)(smem + m.xfer);
-        int16_t *st_s16 = (int16_t *)(smem + m.stash_s);
-        int32_t *st_s32 = (int32_t *)(smem + m.stash_s);
-        float *st_d = (float *)(smem + m.stash_d);
-        const int seg_blocks = (int)(seg_tiles * BT);
-        int16_t *my_s16 = st_s16 + (size_t)(wave > 0 ? wave - 1 : 0) * seg_blocks * 64;
-        int32_t *my_s32 = st_s32 + (size_t)(wave > 0 ? wave - 1 : 0) * seg_blocks * 64;
-        float *my_d = st_d + (size_t)(wave > 0 ? wave - 1 : 0) * seg_blocks * 8;
-        for (int64_t rt = blockIdx.x; rt < a.n_rt; rt += gridDim.x) {
-            const int64_t bt0 = wave * seg_tiles, bt1 = bt0 + seg_tiles;
-            float acc = 0.0f;
-            if (wave == 0)
-                acc = run_chain<WT, false>(a.qs, a.sc, a.n_bt, rt, bt0, bt1, smem, m, 0.0f, lane, nullptr, nullptr,
-                                           nullptr);
-            else
-                run_chain<WT, true>(a.qs, a.sc, a.n_bt, rt, bt0, bt1, smem, m, 0.0f, lane, my_s16, my_s32, my_d);
-            __syncthreads();
-            // ordered carry: wave w continues wave w-1's accumulator over its stashed terms
-            for (int w = 1; w < KS; ++w) {
-                if (wave == w - 1) xfer[(w & 1) * 64 + lane] = acc;
-                __syncthreads();
-                if (wave == w) {
-                    acc = xfer[(w & 1) * 64 + lane];
-#pragma unroll 8
-                    for (int j = 0; j < seg_blocks; ++j) {
-                        const float d = my_d[j * 8 + rr];
-                        const float s = WT == T_Q4_0 ? (float)my_s16[j * 64 + lane] : (float)my_s32[j * 64 + lane];
-                        acc = __builtin_fmaf(d, s, acc);
+        rt0 = blockIdx.x;
+        rstride = gridDim.x;
+    }
+    const int64_t n_my_rt = rt0 < a.n_rt ? (a.n_rt - rt0 + rstride - 1) / rstride : 0;
+    const int64_t n_items = n_my_rt * NM * nbt;
+
+    // 0) this thread's activation values (older than the weight loads -> waited for by count)
+    act_regs<R> ar;
+    prefetch_activation<WT, PRO, R>(a, col, ar);
+
+    // 1) fill the register ring: the HBM round trip overlaps the prologue below.  Loads are
+    //    never inside a runtime branch (hipcc would wait vmcnt(0) around them): past the last item
+    //    the cursor stays put and the same tile is re-read (L2 hit, at most U-1 per wave).  The
+    //    tile base is uniform (SGPR pair) and the lane offset 32-bit: global_load v, v_off, s[base].
+    uint4 qb[U], sb[U];
+    cursor ic{n_items ? rt0 : 0, 0, 0};
+    int64_t issued = 0;
+    const uint32_t q_off = (uint32_t)lane * 16u, s_off = (uint32_t)rr * SB;
+    auto issue = [&](uint4 &qd, uint4 &sd) {
+        const bool second = NM == 2 && ic.m;
+        const int64_t tile = ic.rt * a.n_bt + bt0 + ic.bt;
+        const uint8_t *qt = (second ? a.qs2 : a.qs) + tile * 1024;
+        const uint8_t *st = (second ? a.sc2 : a.sc) + tile * 8 * SB;
+        qd = *(const uint4 *)(qt + q_off);
+        if (WT == T_Q4_0) {
+            sd = *(const uint4 *)(st + s_off);
+        } else {
+            const uint2 v = *(const uint2 *)(st + s_off);
+            sd = make_uint4(v.x, v.y, 0, 0);
+        }
+        ++issued;
+        if (issued < n_items) {
+            if (++ic.bt == nbt) {
+                ic.bt = 0;
+                if (++ic.m == NM) {
+                    ic.m = 0;
+                    ic.rt += rstride;
+                }
+            }
+        }
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u) issue(qb[u], sb[u]);
+
+    // 2) activation image in LDS
+    if (!(a.ablate & 1)) build_activation<WT, PRO, R, NSA>(a, col, smem, m, ar);
+    __syncthreads();
+
+    // 3) stream
+    const int seg_blocks = nbt * BT;
+    float *st_s = (float *)(smem + m.stash_s), *st_d = (float *)(smem + m.stash_d);
+    float *my_s = st_s + ((size_t)(wave > 0 ? wave - 1 : 0) * 64 + lane) * m.sbp;
+    float *my_d = st_d + ((size_t)(wave > 0 ? wave - 1 : 0) * 8 + rr) * m.sbp;
+    unsigned long long best = 0;
+    cursor cc{rt0, 0, 0};
+    float acc = 0.0f, va = 0.0f;
+    const int64_t n_pad = (n_items + U - 1) / U * U;
+    for (int64_t k = 0; k < n_pad; k += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint4 qc = qb[u], scc = sb[u];
+            issue(qb[u], sb[u]);
+            if (k + u < n_items) {
+                const int64_t bt = bt0 + cc.bt;
+                if (KS == 1 || wave == 0)
+                    acc = tile_dot<WT, false, NSA>(qc, scc, smem, m, bt, l, acc, nullptr, nullptr, 0);
+                else
+                    tile_dot<WT, true, NSA>(qc, scc, smem, m, bt, l, 0.0f, my_s, my_d, cc.bt * BT);
+                if (cc.bt + 1 == nbt) {
+                    // end of this wave's part of a (matrix, row tile)
+                    if (KS == 1) {
+                        const float v = fold8(acc);
+                        acc = 0.0f;
+                        if (NM == 2 && cc.m == 0) {
+                            va = v;
+                        } else if ((lane & 7) == 0) {
+                            epilogue<EPI>(a, col, cc.rt * 8 + rr, NM == 2 ? va : v, v, best);
+                        }
+                    } else {
+                        // ordered carry: after ONE barrier, wave 0 continues its own accumulator
+                        // through the stashed terms of segments 1..KS-1, in block order
+                        __syncthreads();
+                        if (wave == 0) {
+                            if (!(a.ablate & 4)) {
+                                for (int w = 1; w < KS; ++w) {
+                                    const float *ss = st_s + ((size_t)(w - 1) * 64 + lane) * m.sbp;
+                                    const float *sd = st_d + ((size_t)(w - 1) * 8 + rr) * m.sbp;
+#pragma unroll 4
+                                    for (int j = 0; j < seg_blocks; j += 4) {
+                                        const float4 s4 = *(const float4 *)(ss + j), d4 = *(const float4 *)(sd + j);
+                                        acc = __builtin_fmaf(d4.x, s4.x, acc);
+                                        acc = __builtin_fmaf(d4.y, s4.y, acc);
+                                        acc = __builtin_fmaf(d4.z, s4.z, acc);
+                                        acc = __builtin_fmaf(d4.w, s4.w, acc);
+                                    }
+                                }
+                            }
+                            const float v = fold8(acc);
+                            if ((lane & 7) == 0) epilogue<EPI>(a, col, cc.rt * 8 + rr, v, 0.0f, best);
+                        }
+                        acc = 0.0f;
+                        __syncthreads();
+                    }
+                }
+                if (++cc.bt == nbt) {
+                    cc.bt = 0;
+                    if (++cc.m == NM) {
+                        cc.m = 0;
+                        cc.rt += rstride;
                     }
                 }
             }
-            if (wave == KS - 1) {
-                const float v = fold8(acc);
-                if ((lane & 7) == 0) epilogue<EPI>(a, col, rt * 8 + rr, v, 0.0f, best);
-            }
-            __syncthreads();
         }
     }
     if (EPI == EPI_ARGMAX) {
-        // wave-level max then one atomic per wave (first max wins via the index complement)
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             const unsigned long long o = __shfl_xor(best, off);
             best = o > best ? o : best;
         }
-        if (lane == 0 && best != 0) atomicMax(a.argmax_key, best);
+        // one plain store per workgroup into its own slot (a single-word atomic from every wave
+        // serialises at the memory side: MI355X_MICROARCH fan-in row); k_advance reduces the slots
+        unsigned long long *red = (unsigned long long *)(smem + m.red);
+        __syncthreads();
+        if (lane == 0) red[wave] = best;
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
+            a.argmax_key[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = best;
+        }
     }
 }
 
 template <int WT, int KS, int PRO, int EPI>
 int launch_t(const mv_args &a, int grid_x, hipStream_t s) {
+    constexpr bool NSA = KS != 8;  // 8-way split: recompute -8*sum(a) to leave LDS for the stash
     const int64_t seg = KS > 1 ? a.n_bt / KS : a.n_bt;
-    const lds_map m = make_lds_map<WT>(KS, a.n_bt, seg);
+    const lds_map m = make_lds_map<WT, NSA>(KS, a.n_bt, seg);
     const int threads = KS > 1 ? 64 * KS : 256;
     if (KS > 1 && a.n_bt % KS != 0) {
         set_error("matvec: n_bt not divisible by KS");
@@ -418,33 +549,28 @@ int launch_t(const mv_args &a, int grid_x, hipStream_t s) {
         set_error("matvec: LDS image too large");
         return -1;
     }
-    if (m.total > 64 * 1024)
-        GHIP_CHECK(hipFuncSetAttribute((const void *)k_matvec<WT, KS, PRO, EPI>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)m.total));
-    hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, a);
+    constexpr int U = 8;
+    constexpr int R = KS == 8 ? 4 : 1;  // activation blocks per quad held in registers
+    const void *fn = (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA>;
+    if (m.total > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m.total));
+    hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, a);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }
 
-template <int WT, int KS, int PRO>
-int dispatch_epi(int epi, const mv_args &a, int g, hipStream_t s) {
-    switch (epi) {
-        case EPI_STORE: return launch_t<WT, KS, PRO, EPI_STORE>(a, g, s);
-        case EPI_ADD: return launch_t<WT, KS, PRO, EPI_ADD>(a, g, s);
-        case EPI_GELU_MUL: return KS == 1 ? launch_t<WT, 1, PRO, EPI_GELU_MUL>(a, g, s) : -1;
-        case EPI_ARGMAX: return launch_t<WT, KS, PRO, EPI_ARGMAX>(a, g, s);
-    }
-    return -1;
-}
-
+// only the (prologue, epilogue) pairs the engine and the C-ABI use are instantiated
 template <int WT, int KS>
 int dispatch_pro(int pro, int epi, const mv_args &a, int g, hipStream_t s) {
-    switch (pro) {
-        case PRO_F32: return dispatch_epi<WT, KS, PRO_F32>(epi, a, g, s);
-        case PRO_NORM: return dispatch_epi<WT, KS, PRO_NORM>(epi, a, g, s);
-        case PRO_Q8: return dispatch_epi<WT, KS, PRO_Q8>(epi, a, g, s);
-        case PRO_EMBED: return dispatch_epi<WT, KS, PRO_EMBED>(epi, a, g, s);
-    }
+    if (pro == PRO_Q8 && epi == EPI_STORE) return launch_t<WT, KS, PRO_Q8, EPI_STORE>(a, g, s);       // C-ABI
+    if (pro == PRO_NORM && epi == EPI_STORE) return launch_t<WT, KS, PRO_NORM, EPI_STORE>(a, g, s);   // qkv
+    if (pro == PRO_EMBED && epi == EPI_STORE) return launch_t<WT, KS, PRO_EMBED, EPI_STORE>(a, g, s); // qkv, layer 0
+    if (pro == PRO_F32 && epi == EPI_ADD) return launch_t<WT, KS, PRO_F32, EPI_ADD>(a, g, s);         // wo, wdown
+    if (KS == 1 && pro == PRO_NORM && epi == EPI_GELU_MUL)
+        return launch_t<WT, 1, PRO_NORM, EPI_GELU_MUL>(a, g, s);                                      // gate/up
+    if (KS == 1 && pro == PRO_NORM && epi == EPI_ARGMAX)
+        return launch_t<WT, 1, PRO_NORM, EPI_ARGMAX>(a, g, s);                                        // logits
+    if (pro == PRO_F32 && epi == EPI_STORE) return launch_t<WT, KS, PRO_F32, EPI_STORE>(a, g, s);
+    set_error("matvec: (prologue, epilogue) combination not instantiated");
     return -1;
 }
 
@@ -463,13 +589,17 @@ int dispatch_ks(int ks, int pro, int epi, const mv_args &a, int g, hipStream_t s
 }  // namespace
 
 size_t matvec_lds_bytes(int wtype, int ks, int64_t n_bt, int64_t seg) {
-    return wtype == T_Q4_0 ? make_lds_map<T_Q4_0>(ks, n_bt, seg).total : make_lds_map<T_Q8_0>(ks, n_bt, seg).total;
+    return wtype == T_Q4_0 ? make_lds_map<T_Q4_0, true>(ks, n_bt, seg).total : make_lds_map<T_Q8_0, true>(ks, n_bt, seg).total;
 }
 
 int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int grid_x, hipStream_t s) {
     if (a.n_rt <= 0 || a.n_bt <= 0) return 0;
     if (grid_x <= 0) {
         set_error("matvec: grid_x <= 0");
+        return -1;
+    }
+    if (a.nb % 1 || (pro != PRO_Q8 && (a.nb * 32) % 8)) {
+        set_error("matvec: K must be a multiple of 32");
         return -1;
     }
     int r = -1;

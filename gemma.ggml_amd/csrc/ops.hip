@@ -230,24 +230,71 @@ __device__ __forceinline__ void f16_step(float acc[4][8], const uint4 *x4, const
     }
 }
 
-constexpr int ATT_THREADS = 256;
+constexpr int ATT_THREADS = 1024;
+constexpr int ATT_DCHUNK = 256;  // KQV outputs per workgroup: grid = (H, hd / 256): one pass of 256 quads
+constexpr int ATT_KPF = 8;      // K steps (of 32 elements) prefetched per thread: hd <= 256
+constexpr int ATT_VPF = 8;      // V steps (of 32 positions) prefetched per thread: n_kv <= 256
 
+// ggml_vec_dot_f16 with accumulator row j = t4 held by lane t4 of a quad: fold the
+// quad exactly as sum0+=sum2, sum1+=sum3, sum0+=sum1 (xor-2 then xor-1), then halves and hadds.
+__device__ __forceinline__ float quad_reduce_f16(const float acc[8], int t4) {
+    float x0[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const float u = acc[l] + __shfl_xor(acc[l], 2);
+        x0[l] = u + __shfl_xor(u, 1);
+    }
+    float t0[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t0[i] = x0[i] + x0[i + 4];
+    const float h0 = t0[0] + t0[1], h1 = t0[2] + t0[3];
+    (void)t4;
+    return h0 + h1;
+}
+
+__device__ __forceinline__ void f16_step8(float acc[8], uint4 xv, uint4 yv) {
+    const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w}, ys[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        acc[2 * w] = __builtin_fmaf(h2f(xs[w]), h2f(ys[w]), acc[2 * w]);
+        acc[2 * w + 1] = __builtin_fmaf(h2f(xs[w] >> 16), h2f(ys[w] >> 16), acc[2 * w + 1]);
+    }
+}
+
+// One token's attention for head h = blockIdx.x, KQV outputs [64*blockIdx.y, +64).  Every
+// workgroup recomputes the (cheap) RoPE, KQ and softmax of its head.  Quads of lanes own one KQ
+// position (or one KQV output): lane t4 runs accumulator row j = t4 of the AVX/F16C loop.  The
+// K rows and V rows of the first pass are requested at kernel entry, before RoPE.
 __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int hd = a.hd, half = hd / 2, tid = threadIdx.x;
-    const int h = blockIdx.x, grp = a.H / a.Hkv, kvh = h / grp;
+    const int hd = a.hd, half = hd / 2, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
+    const int h = blockIdx.x, ds = blockIdx.y, grp = a.H / a.Hkv, kvh = h / grp;
+    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     const int pos = *a.pos;
     const int n_total = pos + 1;
     int n_kv = 32 * (n_total / 32 + 1);                    // src/gemma_model.cpp:429
     if (n_kv > a.ctx) n_kv = a.ctx;
     const int kvw = a.Hkv * hd;
+    const int nq = blockDim.x >> 2;                      // quads per workgroup (64)
+    // ---- early loads: first KQ pass (position `quad`) and the first V steps of output d
+    const int d0 = ds * ATT_DCHUNK + quad;
+    const uint16_t *vrow = a.vc + ((int64_t)kvh * hd + (d0 < hd ? d0 : 0)) * a.ctx;
+    uint4 kpre[ATT_KPF], vpre[ATT_VPF];
+    {
+        const int j = quad < a.ctx ? quad : 0;           // no dependency on *pos: rows >= pos are masked
+        const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
+#pragma unroll
+        for (int s = 0; s < ATT_KPF; ++s) kpre[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
+#pragma unroll
+        for (int s = 0; s < ATT_VPF; ++s) vpre[s] = *(const uint4 *)(vrow + (s * 32 < a.ctx ? s * 32 : 0) + t4 * 8);
+    }
     uint16_t *q16 = (uint16_t *)smem;                    // hd
     uint16_t *k16 = q16 + hd;                            // hd (this token's k, post-rope)
     uint16_t *v16 = k16 + hd;                            // hd (this token's v)
     float *S = (float *)(smem + ((3 * hd * 2 + 15) & ~15));  // ctx
     uint16_t *P16 = (uint16_t *)(S + a.ctx);             // ctx
-    float *red = (float *)(P16 + a.ctx + 8);             // 8 floats / 8 u64 (aligned below)
-    unsigned long long *red64 = (unsigned long long *)(((uintptr_t)(red + 8) + 7) & ~(uintptr_t)7);
+    float *red = (float *)(P16 + a.ctx + 8);             // 16 floats, then 16 u64 (aligned below)
+    unsigned long long *red64 = (unsigned long long *)(((uintptr_t)(red + 16) + 7) & ~(uintptr_t)7);
 
     // RoPE NEOX on q (then * q_scale) and on k; f32 -> f16 (ggml_cpy / MUL_MAT INIT conversions)
     const float *cs = a.rope_cos + (int64_t)pos * half, *sn = a.rope_sin + (int64_t)pos * half;
@@ -272,33 +319,46 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     }
     for (int i = tid; i < hd; i += blockDim.x) v16[i] = f2h(vh[i]);
     __syncthreads();
+    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
     if (h % grp == 0) {  // one writer per kv head: K row `pos`, V column `pos` (src/gemma_model.cpp:506-517)
-        for (int i = tid; i < hd; i += blockDim.x) {
+        for (int i = ds * ATT_DCHUNK + tid; i < (ds + 1) * ATT_DCHUNK && i < hd; i += blockDim.x) {
             a.kc[(int64_t)pos * kvw + (int64_t)kvh * hd + i] = k16[i];
             a.vc[((int64_t)kvh * hd + i) * a.ctx + pos] = v16[i];
         }
     }
-    // KQ (vec_dot_f16 over hd per kv position) + mask (j > pos -> -inf), scale 1.0
-    for (int j = tid; j < n_kv; j += blockDim.x) {
-        float w;
-        if (j > pos) {
-            w = -INFINITY;
+    // ---- KQ (vec_dot_f16 over hd per kv position) + mask (j > pos -> -inf), scale 1.0
+    for (int j0 = 0; j0 < n_kv; j0 += nq) {
+        const int j = j0 + quad;
+        float acc[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+        if (j0 == 0) {
+#pragma unroll
+            for (int s = 0; s < ATT_KPF; ++s)
+                if (s * 32 < hd) {
+                    const uint4 kv = (j == pos) ? *(const uint4 *)(k16 + s * 32 + t4 * 8) : kpre[s];
+                    f16_step8(acc, kv, *(const uint4 *)(q16 + s * 32 + t4 * 8));
+                }
+            for (int s = ATT_KPF; s * 32 < hd; ++s) {
+                const uint16_t *krow = (j == pos) ? k16 : a.kc + (int64_t)j * kvw + (int64_t)kvh * hd;
+                f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
+            }
         } else {
-            float acc[4][8];
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 8; ++y) acc[x][y] = 0.0f;
-            const uint16_t *krow = (j == pos) ? k16 : a.kc + (int64_t)j * kvw + (int64_t)kvh * hd;
-            for (int st = 0; st < hd; st += 32) f16_step(acc, (const uint4 *)(krow + st), (const uint4 *)(q16 + st));
-            const float kq = reduce_f16_acc(acc);
-            w = kq * 1.0f + 0.0f;
+            const int jc = j < pos ? j : pos;
+            const uint16_t *krow = (jc == pos) ? k16 : a.kc + (int64_t)jc * kvw + (int64_t)kvh * hd;
+            for (int s = 0; s * 32 < hd; ++s)
+                f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
         }
-        S[j] = w;
-        if (a.dbg_w) a.dbg_w[(int64_t)h * a.ctx + j] = w;
+        const float kq = quad_reduce_f16(acc, t4);
+        if (t4 == 0 && j < n_kv) {
+            const float w = (j > pos) ? -INFINITY : kq * 1.0f + 0.0f;
+            S[j] = w;
+            if (a.dbg_w && ds == 0) a.dbg_w[(int64_t)h * a.ctx + j] = w;
+        }
     }
     __syncthreads();
-    // soft_max_ext: max; e = table_exp[f16(w - max)]; exact sum; y = e * (float)(1/sum)
+    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+    // ---- soft_max_ext: max; e = table_exp[f16(w - max)]; exact sum; e * (float)(1/sum)
     float mx = -INFINITY;
     for (int j = tid; j < n_kv; j += blockDim.x) mx = fmaxf(mx, S[j]);
 #pragma unroll
@@ -307,6 +367,7 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     __syncthreads();
     mx = red[0];
     for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmaxf(mx, red[w]);
+    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
     // e values are fp16 in [0,1]: exact multiples of 2^-24, so an integer sum is the exact sum
     // (ggml's double accumulation of them is exact too).
     unsigned long long isum = 0;
@@ -319,50 +380,72 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) isum += __shfl_xor(isum, off);
-    __syncthreads();
     if ((tid & 63) == 0) red64[tid >> 6] = isum;
     __syncthreads();
+    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 4] = __builtin_amdgcn_s_memrealtime();
     unsigned long long tot = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += red64[w];
     const double sum = (double)tot * (1.0 / 16777216.0);
     const float inv = (float)(1.0 / sum);
-    if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
+    if (a.dbg_inv && tid == 0 && ds == 0) a.dbg_inv[h] = inv;
     for (int j = tid; j < n_kv; j += blockDim.x) {
         P16[j] = f2h(S[j] * inv);
-        if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
+        if (a.dbg_p && ds == 0) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
     }
     __syncthreads();
-    // KQV: out[d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16)
-    for (int d = tid; d < hd; d += blockDim.x) {
-        float acc[4][8];
+    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+    // ---- KQV: out[d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16); lane t4 runs accumulator j = t4
+    for (int d = d0; d < (ds + 1) * ATT_DCHUNK && d < hd; d += nq) {
+        float acc[8];
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+        for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+        const uint16_t *vr = a.vc + ((int64_t)kvh * hd + d) * a.ctx;
+        for (int st = 0, s = 0; st < n_kv; st += 32, ++s) {
+            const int e0 = st + t4 * 8;
+            uint4 xv;
+            if (d == d0 && s < ATT_VPF) {
+                // statically-indexed pick from the early loads
+                xv = vpre[0];
 #pragma unroll
-            for (int y = 0; y < 8; ++y) acc[x][y] = 0.0f;
-        const uint16_t *vrow = a.vc + ((int64_t)kvh * hd + d) * a.ctx;
-        for (int st = 0; st < n_kv; st += 32) {
-            if (pos >= st && pos < st + 32) {
-                // this step contains the current token's V (only this WG's LDS copy is safe to read)
-                __attribute__((aligned(16))) uint16_t tmp[32];
-                for (int e = 0; e < 32; ++e) tmp[e] = (st + e == pos) ? v16[d] : vrow[st + e];
-                f16_step(acc, (const uint4 *)tmp, (const uint4 *)(P16 + st));
+                for (int k = 1; k < ATT_VPF; ++k)
+                    if (s == k) xv = vpre[k];
             } else {
-                f16_step(acc, (const uint4 *)(vrow + st), (const uint4 *)(P16 + st));
+                xv = *(const uint4 *)(vr + e0);
             }
+            if (pos >= e0 && pos < e0 + 8) {  // this token's V: only the LDS copy is safe to read
+                __attribute__((aligned(16))) uint16_t tmp[8];
+                *(uint4 *)tmp = xv;
+                tmp[pos - e0] = v16[d];
+                xv = *(const uint4 *)tmp;
+            }
+            f16_step8(acc, xv, *(const uint4 *)(P16 + e0));
         }
-        a.out[(int64_t)h * hd + d] = reduce_f16_acc(acc);
+        const float o = quad_reduce_f16(acc, t4);
+        if (t4 == 0) a.out[(int64_t)h * hd + d] = o;
     }
+    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 }
 
-__global__ void k_advance(const unsigned long long *key, int *token, int *pos, int *hist, int hist_cap,
-                          const int *n_fixed, unsigned long long *key_reset) {
-    const unsigned long long k = *key;
-    const int idx = (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull));
+__global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys, int n_parts, int *token, int *pos,
+                                                 int *hist, int hist_cap, const int *n_fixed) {
+    __shared__ unsigned long long red[4];
+    unsigned long long best = 0;
+    for (int i = threadIdx.x; i < n_parts; i += blockDim.x) best = keys[i] > best ? keys[i] : best;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
+    // strict '>' argmax, first max wins (src/gemma_model.cpp:538-543): the key's low word is ~index
+    const int idx = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
     const int p = *pos + 1;
     *token = idx;
     if (hist && p < hist_cap && p >= *n_fixed) hist[p] = idx;  // never overwrite the prompt
     *pos = p;
-    *key_reset = 0ull;
 }
 
 // C-ABI F16 mul_mat (KQ/KQV shapes): one thread per (row, col), vec_dot_f16 order
@@ -442,21 +525,21 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
         return -1;
     }
     const size_t lds = ((3 * (size_t)a.hd * 2 + 15) & ~(size_t)15) + (size_t)a.ctx * 4 + (size_t)a.ctx * 2 + 16 + 64 +
-                       64 + 64;
+                       64 + 8 + 128;  // red: 16 floats, align, 16 u64
     if (lds > 160 * 1024) {
         set_error("attn_decode: context too long for the LDS image");
         return -1;
     }
     if (lds > 64 * 1024)
         GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_attn_decode, dim3(a.H), dim3(ATT_THREADS), lds, s, a);
+    hipLaunchKernelGGL(k_attn_decode, dim3(a.H, (a.hd + ATT_DCHUNK - 1) / ATT_DCHUNK), dim3(ATT_THREADS), lds, s, a);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }
 
-int launch_advance(const unsigned long long *key, int *token, int *pos, int *hist, int hist_cap, const int *n_fixed,
-                   unsigned long long *key_reset, hipStream_t s) {
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, s, key, token, pos, hist, hist_cap, n_fixed, key_reset);
+int launch_advance(const unsigned long long *keys, int n_parts, int *token, int *pos, int *hist, int hist_cap,
+                   const int *n_fixed, hipStream_t s) {
+    hipLaunchKernelGGL(k_advance, dim3(1), dim3(256), 0, s, keys, n_parts, token, pos, hist, hist_cap, n_fixed);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

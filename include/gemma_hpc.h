@@ -79,7 +79,8 @@ int gemma_engine_sync(gemma_engine *e);
 int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
 /* per-op test entry: one decode-attention block on host buffers (caches updated in place) */
 int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos, int H, int Hkv, int hd, int ctx,
-                           float rope_base, float *out, float *dbg_w, uint16_t *dbg_p, float *dbg_inv);
+                           float rope_base, float *out, float *dbg_w, uint16_t *dbg_p, float *dbg_inv,
+                           unsigned long long *dbg_t);
 
 #ifdef __cplusplus
 }

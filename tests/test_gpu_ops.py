@@ -28,7 +28,7 @@ def test_attn_decode_bitexact(H, Hkv):
     import gemma_hip as G
     L = G.lib()
     L.gemma_test_attn_decode.restype = C.c_int
-    L.gemma_test_attn_decode.argtypes = [C.c_void_p] * 3 + [C.c_int] * 5 + [C.c_float] + [C.c_void_p] * 4
+    L.gemma_test_attn_decode.argtypes = [C.c_void_p] * 3 + [C.c_int] * 5 + [C.c_float] + [C.c_void_p] * 5
     OL = O.lib()
     OL.orc_attn_decode.argtypes = [C.c_void_p] * 3 + [C.c_int] * 5 + [C.c_float] + [C.c_void_p] * 4
     hd, ctx = 256, 512
@@ -45,7 +45,7 @@ def test_attn_decode_bitexact(H, Hkv):
             OL.orc_attn_decode(qkv.ctypes.data, k1.ctypes.data, v1.ctypes.data, pos, H, Hkv, hd, ctx, 10000.0,
                                ref.ctypes.data, w1.ctypes.data, p1.ctypes.data, None)
             r = L.gemma_test_attn_decode(qkv.ctypes.data, k2.ctypes.data, v2.ctypes.data, pos, H, Hkv, hd, ctx,
-                                         10000.0, got.ctypes.data, w2.ctypes.data, p2.ctypes.data, None)
+                                         10000.0, got.ctypes.data, w2.ctypes.data, p2.ctypes.data, None, None)
             assert r == 0, G.last_error()
             assert np.array_equal(k1, k2) and np.array_equal(v1, v2), f"cache update differs at pos {pos}"
             nd = int((got.view(np.uint32) != ref.view(np.uint32)).sum())
