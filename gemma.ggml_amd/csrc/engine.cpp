@@ -170,7 +170,14 @@ struct gemma_engine {
     void *pf_scratch = nullptr;
     size_t pf_bytes = 0;
     float *dbg = nullptr;  // per-layer taps [L][qkv_rows + qw + E] (debug steps only)
+    unsigned long long *stamp = nullptr;  // phase stamps of one layer's kernels (diagnostic steps only)
+    int stamp_layer = -1;
 };
+
+static constexpr size_t kStampRegion = 4096 * 16;  // u64 per kernel: <= 4096 workgroups x 16 stamps
+static unsigned long long *stamp_region(gemma_engine *e, int il, int k) {
+    return (e->stamp && il == e->stamp_layer) ? e->stamp + (size_t)k * kStampRegion : nullptr;
+}
 
 // largest power-of-two K split <= target that divides the block-tile count
 static int pick_ks(int64_t n_bt, int target) {
@@ -201,6 +208,7 @@ static int enqueue_step(gemma_engine *e) {
         } else {
             a.x = e->x;
         }
+        a.dbg_t = stamp_region(e, il, 0);
         if (launch_matvec(wt, pick_ks(L.qkv.n_bt, e->ks_small), pro, EPI_STORE, a, (int)L.qkv.n_rt, s)) return -1;
         // K2: rope + scale + kv store + KQ + softmax + KQV  (:698-718, :454-518)
         attn_args t;
@@ -211,6 +219,7 @@ static int enqueue_step(gemma_engine *e) {
         t.pos = e->pos; t.out = e->attn;
         t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
         t.q_scale = 1.0f / sqrtf((float)c.head_dim);
+        t.dbg_t = stamp_region(e, il, 1);
         if (launch_attn_decode(t, s)) return -1;
         const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
         if (e->dbg) GHIP_CHECK(hipMemcpyAsync(e->dbg + tap, e->qkv, (size_t)e->qkv_rows * 4, hipMemcpyDeviceToDevice, s));
@@ -220,6 +229,7 @@ static int enqueue_step(gemma_engine *e) {
         mv_args b;
         b.qs = L.o.qs; b.sc = L.o.sc; b.rows = L.o.rows; b.n_rt = L.o.n_rt; b.n_bt = L.o.n_bt; b.nb = L.o.nb;
         b.x = e->attn; b.y = e->sa; b.resid = e->x;
+        b.dbg_t = stamp_region(e, il, 2);
         if (launch_matvec(wt, pick_ks(L.o.n_bt, e->ks_small), PRO_F32, EPI_ADD, b, (int)L.o.n_rt, s)) return -1;
         // K4: rms_norm*ffn_norm + quantize -> gate & up -> gelu(gate)*up  (:724, :446-449)
         mv_args g;
@@ -227,6 +237,7 @@ static int enqueue_step(gemma_engine *e) {
         g.rows = L.gate.rows; g.n_rt = L.gate.n_rt; g.n_bt = L.gate.n_bt; g.nb = L.gate.nb;
         g.x = e->sa; g.norm_w = L.ffn_norm; g.eps = c.eps; g.y = e->h;
         g.gelu_tab = e->gelu_tab; g.gelu_clamp = c.gelu_clamp;
+        g.dbg_t = stamp_region(e, il, 3);
         if (launch_matvec(wt, 1, PRO_NORM, EPI_GELU_MUL, g, (int)std::min<int64_t>((L.gate.n_rt + 3) / 4, e->grid_big), s))
             return -1;
         // K5: quantize(h) -> Wdown, + sa  (:450, :731)
@@ -234,6 +245,7 @@ static int enqueue_step(gemma_engine *e) {
         d.qs = L.down.qs; d.sc = L.down.sc; d.rows = L.down.rows; d.n_rt = L.down.n_rt; d.n_bt = L.down.n_bt;
         d.nb = L.down.nb;
         d.x = e->h; d.y = e->x; d.resid = e->sa;
+        d.dbg_t = stamp_region(e, il, 4);
         if (launch_matvec(wt, pick_ks(L.down.n_bt, e->ks_down), PRO_F32, EPI_ADD, d, (int)L.down.n_rt, s)) return -1;
         if (e->dbg)
             GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows + e->qw, e->x, (size_t)E * 4, hipMemcpyDeviceToDevice, s));
@@ -244,6 +256,7 @@ static int enqueue_step(gemma_engine *e) {
     o.nb = e->embd.nb;
     o.x = e->x; o.norm_w = e->out_norm; o.eps = c.eps; o.y = e->logits; o.argmax_key = e->key;
     const int lg_grid = (int)std::min<int64_t>((e->embd.n_rt + 3) / 4, e->grid_big);
+    o.dbg_t = e->stamp ? e->stamp + 5 * kStampRegion : nullptr;
     if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, lg_grid, s)) return -1;
     // K7: token feedback (greedy_sample -> input.push_back, :282-285), position += 1
     // the prompt is never overwritten: hist writes only land at positions >= n_prompt
@@ -580,6 +593,28 @@ extern "C" int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *
 }
 
 // one eager step with per-layer taps copied to host: [L][qkv | attn | x_out]
+// Diagnostic: one eager decode step with s_memrealtime phase stamps (100 MHz) for the five kernels
+// of `layer` (regions 0..4: qkv, attention, o, gate/up, down) and the logits kernel (region 5).
+// out: 6 * 4096 * 16 u64; unused slots are 0.
+extern "C" int gemma_engine_stamp_step(gemma_engine *e, int layer, unsigned long long *out) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    const size_t n = 6 * kStampRegion;
+    GHIP_CHECK(hipMalloc(&e->stamp, n * 8));
+    GHIP_CHECK(hipMemsetAsync(e->stamp, 0, n * 8, e->stream));
+    e->stamp_layer = layer;
+    const int r = enqueue_step(e);
+    if (r == 0) {
+        GHIP_CHECK(hipStreamSynchronize(e->stream));
+        GHIP_CHECK(hipMemcpy(out, e->stamp, n * 8, hipMemcpyDeviceToHost));
+        e->host_pos += 1;
+    }
+    (void)hipFree(e->stamp);
+    e->stamp = nullptr;
+    e->stamp_layer = -1;
+    return r;
+}
+
 extern "C" int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits) {
     set_error("");
     (void)hipSetDevice(e->device);
@@ -614,8 +649,9 @@ extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *
     int *d_pos;
     float *d_dw = nullptr, *d_di = nullptr;
     unsigned long long *d_dt = nullptr;
-    const size_t n_stamps = (size_t)H * ((hd + 63) / 64) * 8;
+    const size_t n_stamps = (size_t)H * 8 * 8;  // >= workgroups x 8 stamps for any hd <= 512
     if (dbg_t) GHIP_CHECK(hipMalloc(&d_dt, n_stamps * 8));
+    if (dbg_t) GHIP_CHECK(hipMemset(d_dt, 0, n_stamps * 8));
     uint16_t *d_dp = nullptr;
     if (dbg_w) GHIP_CHECK(hipMalloc(&d_dw, (size_t)H * ctx * 4));
     if (dbg_p) GHIP_CHECK(hipMalloc(&d_dp, (size_t)H * ctx * 2));

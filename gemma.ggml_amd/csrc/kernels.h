@@ -43,6 +43,7 @@ struct mv_args {
     unsigned long long *argmax_key = nullptr;      // EPI_ARGMAX: one partial key per workgroup [grid]
     int ncols = 1;
     int ablate = 0;  // timing-only ablations (bench): 1 = no prologue, 4 = no carry
+    unsigned long long *dbg_t = nullptr;  // diagnostics: 8 s_memrealtime stamps per workgroup
 };
 
 // ks: waves that split one row tile's K range (ordered carry hand-off); 1 = one wave per tile.

@@ -33,7 +33,8 @@ __device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) {
 // ns:  uint4 [nb_pad/4][8 lanes] = -8*sum(a) per (block, lane) (Q4_0 only, when NSA; otherwise
 //      recomputed with one more v_dot4 to save LDS)
 // da:  float [nb_pad] (fp32 of the fp16 activation scale)
-// stash (KS > 1): s float [KS-1][64 lanes][SBP], d float [KS-1][8 rows][SBP]  (SBP = seg + 4 pad)
+// stash (KS > 1): s float [64 lanes][SBP], d float [8 rows][SBP]; a lane's (or row's) segments
+//      1..KS-1 are contiguous, so the carry chain reads one linear run (SBP = (KS-1)*seg + 4 pad)
 constexpr int STASH_PAD = 4;
 struct lds_map {
     size_t act, ns, da, stash_s, stash_d, red, total;
@@ -51,11 +52,11 @@ __host__ __device__ inline lds_map make_lds_map(int ks, int64_t n_bt, int64_t se
     m.da = off;
     off += nb_pad * 4;
     off = (off + 15) & ~(size_t)15;
-    m.sbp = (int)(seg_tiles * BT) + STASH_PAD;
+    m.sbp = ks > 1 ? (int)((ks - 1) * seg_tiles * BT) + STASH_PAD : 0;
     m.stash_s = off;
-    off += ks > 1 ? (size_t)(ks - 1) * 64 * m.sbp * 4 : 0;
+    off += (size_t)64 * m.sbp * 4;
     m.stash_d = off;
-    off += ks > 1 ? (size_t)(ks - 1) * 8 * m.sbp * 4 : 0;
+    off += (size_t)8 * m.sbp * 4;
     m.red = off;
     off += 64 * 8;
     m.total = off;
@@ -71,8 +72,8 @@ __device__ __forceinline__ void put_quad(uint8_t *smem, const lds_map &m, int64_
     float amax = 0.0f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
-    amax = fmaxf(amax, __shfl_xor(amax, 1));
-    amax = fmaxf(amax, __shfl_xor(amax, 2));
+    amax = fmaxf(amax, dpp_f<0xB1>(amax));  // quad xor 1
+    amax = fmaxf(amax, dpp_f<0x4E>(amax));  // quad xor 2
     const float d = amax / 127.f;
     const uint32_t d16 = f2h(d);
     const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
@@ -223,7 +224,7 @@ __device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const
         }
         double *red = (double *)(smem + m.red);
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+        for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);  // (once per launch)
         if ((tid & 63) == 0) red[tid >> 6] = part;
         __syncthreads();
         double sum = 0.0;
@@ -339,10 +340,7 @@ __device__ __forceinline__ uint4 load_scale(const uint8_t *sc, int64_t tile, int
 
 // ordered fold of the 8 lanes (hsum_float_8): xor 4, then 2, then 1
 __device__ __forceinline__ float fold8(float v) {
-    v = v + __shfl_xor(v, 4);
-    v = v + __shfl_xor(v, 2);
-    v = v + __shfl_xor(v, 1);
-    return v;
+    return fold8_dpp(v);
 }
 
 __device__ __forceinline__ unsigned long long argmax_key(float v, int64_t idx) {
@@ -381,7 +379,63 @@ struct cursor {
     int bt;
 };
 
-template <int WT, int KS, int PRO, int EPI, int U, int R, bool NSA>
+// Ordered carry (wave 0): acc continues through the stashed (d, isum) terms of segments 1..KS-1 in
+// block order — the exact fmaf chain of the sequential loop.  The run is linear in LDS (stash
+// layout above) and read AHEAD chunks of 4 blocks ahead of the FMAs, so the chain runs at FMA
+// latency, not LDS latency.  Reads are never inside a branch: past the end the index is clamped.
+template <int G, bool EXACT>
+__device__ __forceinline__ float carry_run(const float4 *ps, const float4 *pd, int total, float acc) {
+    float4 as[G], ad[G], bs[G], bd[G];
+    auto load = [&](float4 (&S)[G], float4 (&D)[G], int c0) {
+#pragma unroll
+        for (int r = 0; r < G; ++r) {
+            const int i = EXACT ? c0 + r : (c0 + r < total - 1 ? c0 + r : total - 1);
+            S[r] = ps[i];
+            D[r] = pd[i];
+        }
+    };
+    auto chain = [&](const float4 (&S)[G], const float4 (&D)[G], int c0) {
+#pragma unroll
+        for (int r = 0; r < G; ++r) {
+            if (EXACT || c0 + r < total) {
+                acc = __builtin_fmaf(D[r].x, S[r].x, acc);
+                acc = __builtin_fmaf(D[r].y, S[r].y, acc);
+                acc = __builtin_fmaf(D[r].z, S[r].z, acc);
+                acc = __builtin_fmaf(D[r].w, S[r].w, acc);
+            }
+        }
+    };
+    load(as, ad, 0);
+    load(bs, bd, G);
+    for (int c = 0; c < total; c += 2 * G) {
+        // the empty asm statements pin each set's reads one half-step ahead of their FMAs
+        asm volatile("" ::: "memory");
+        chain(as, ad, c);
+        asm volatile("" ::: "memory");
+        if (!EXACT || c + 2 * G < total) load(as, ad, c + 2 * G);
+        asm volatile("" ::: "memory");
+        chain(bs, bd, c + G);
+        asm volatile("" ::: "memory");
+        if (!EXACT || c + 3 * G < total) load(bs, bd, c + 3 * G);
+    }
+    return acc;
+}
+
+// gl = row * 8 + lane-of-row in the wave-0 numbering of the stash
+template <int KS>
+__device__ __forceinline__ float carry_chain(const float *st_s, const float *st_d, int sbp, int seg_blocks, int gl,
+                                             float acc) {
+    const float4 *ps = (const float4 *)(st_s + (size_t)gl * sbp);
+    const float4 *pd = (const float4 *)(st_d + (size_t)(gl >> 3) * sbp);
+    const int total = (KS - 1) * (seg_blocks >> 2);  // chunks of 4 blocks
+    // whole double-steps: no bounds test inside the dependent chain
+    if (total % 8 == 0) return carry_run<4, true>(ps, pd, total, acc);
+    if (total % 4 == 0) return carry_run<2, true>(ps, pd, total, acc);
+    return carry_run<2, false>(ps, pd, total, acc);
+}
+
+// ONE_SHOT: every wave's items fit the register ring (n_items <= U): no refills in the stream loop
+template <int WT, int KS, int PRO, int EPI, int U, int R, bool NSA, bool ONE_SHOT>
 __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int BT = wfmt<WT>::BT, SB = wfmt<WT>::SCALE_BYTES;
@@ -391,6 +445,7 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int rr = lane >> 3, l = lane & 7;
     const int col = blockIdx.y;
+    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 0] = __builtin_amdgcn_s_memrealtime();
     const int64_t seg_tiles = KS > 1 ? a.n_bt / KS : a.n_bt;
     const lds_map m = make_lds_map<WT, NSA>(KS, a.n_bt, seg_tiles);
     const int nbt = (int)seg_tiles;
@@ -445,25 +500,28 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     };
 #pragma unroll
     for (int u = 0; u < U; ++u) issue(qb[u], sb[u]);
+    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 1] = __builtin_amdgcn_s_memrealtime();
 
     // 2) activation image in LDS
     if (!(a.ablate & 1)) build_activation<WT, PRO, R, NSA>(a, col, smem, m, ar);
+    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 2] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
+    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 3] = __builtin_amdgcn_s_memrealtime();
 
     // 3) stream
     const int seg_blocks = nbt * BT;
     float *st_s = (float *)(smem + m.stash_s), *st_d = (float *)(smem + m.stash_d);
-    float *my_s = st_s + ((size_t)(wave > 0 ? wave - 1 : 0) * 64 + lane) * m.sbp;
-    float *my_d = st_d + ((size_t)(wave > 0 ? wave - 1 : 0) * 8 + rr) * m.sbp;
+    float *my_s = st_s + (size_t)lane * m.sbp + (size_t)(wave > 0 ? wave - 1 : 0) * nbt * BT;
+    float *my_d = st_d + (size_t)rr * m.sbp + (size_t)(wave > 0 ? wave - 1 : 0) * nbt * BT;
     unsigned long long best = 0;
     cursor cc{rt0, 0, 0};
     float acc = 0.0f, va = 0.0f;
-    const int64_t n_pad = (n_items + U - 1) / U * U;
+    const int64_t n_pad = ONE_SHOT ? U : (n_items + U - 1) / U * U;
     for (int64_t k = 0; k < n_pad; k += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint4 qc = qb[u], scc = sb[u];
-            issue(qb[u], sb[u]);
+            if (!ONE_SHOT) issue(qb[u], sb[u]);
             if (k + u < n_items) {
                 const int64_t bt = bt0 + cc.bt;
                 if (KS == 1 || wave == 0)
@@ -481,29 +539,33 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
                             epilogue<EPI>(a, col, cc.rt * 8 + rr, NM == 2 ? va : v, v, best);
                         }
                     } else {
-                        // ordered carry: after ONE barrier, wave 0 continues its own accumulator
-                        // through the stashed terms of segments 1..KS-1, in block order
+                        // ordered carry: wave 0 hands its accumulators over through LDS, then after ONE
+                        // barrier the carrier waves continue the chains of their rows through the
+                        // stashed terms of segments 1..KS-1, in block order.  The chain is bound by
+                        // the carrier's LDS read issue (2 x b128 per 4 steps), not by the FMA latency
+                        // (7.5 clk/step): tests/micro/carry_bench*.hip.
+                        float *hand = (float *)(smem + m.red);
+                        if (wave == 0) hand[lane] = acc;
+                        if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 6] = __builtin_amdgcn_s_memrealtime();
                         __syncthreads();
-                        if (wave == 0) {
-                            if (!(a.ablate & 4)) {
-                                for (int w = 1; w < KS; ++w) {
-                                    const float *ss = st_s + ((size_t)(w - 1) * 64 + lane) * m.sbp;
-                                    const float *sd = st_d + ((size_t)(w - 1) * 8 + rr) * m.sbp;
-#pragma unroll 4
-                                    for (int j = 0; j < seg_blocks; j += 4) {
-                                        const float4 s4 = *(const float4 *)(ss + j), d4 = *(const float4 *)(sd + j);
-                                        acc = __builtin_fmaf(d4.x, s4.x, acc);
-                                        acc = __builtin_fmaf(d4.y, s4.y, acc);
-                                        acc = __builtin_fmaf(d4.z, s4.z, acc);
-                                        acc = __builtin_fmaf(d4.w, s4.w, acc);
-                                    }
-                                }
+                        if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 7] = __builtin_amdgcn_s_memrealtime();
+                        {
+                            // one carrier wave: a wave pays ~16-21 clk per ds_read_b128 whatever its
+                            // active lanes, so more carriers only add LDS-array contention
+                            constexpr int NCAR = 1, RPW = 8 / NCAR;
+                            const int gl = wave * RPW * 8 + lane;
+                            if (wave < NCAR && lane < RPW * 8) {
+                                float c = hand[gl];
+                                if (!(a.ablate & 4)) c = carry_chain<KS>(st_s, st_d, m.sbp, seg_blocks, gl, c);
+                                if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 8] = __builtin_amdgcn_s_memrealtime();
+                                const float v = fold8(c);
+                                if ((lane & 7) == 0) epilogue<EPI>(a, col, cc.rt * 8 + (gl >> 3), v, 0.0f, best);
+                                if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 9] = __builtin_amdgcn_s_memrealtime();
                             }
-                            const float v = fold8(acc);
-                            if ((lane & 7) == 0) epilogue<EPI>(a, col, cc.rt * 8 + rr, v, 0.0f, best);
                         }
                         acc = 0.0f;
                         __syncthreads();
+                        if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 10] = __builtin_amdgcn_s_memrealtime();
                     }
                 }
                 if (++cc.bt == nbt) {
@@ -516,6 +578,7 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
             }
         }
     }
+    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 4] = __builtin_amdgcn_s_memrealtime();
     if (EPI == EPI_ARGMAX) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
@@ -533,6 +596,7 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
             a.argmax_key[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = best;
         }
     }
+    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 5] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <int WT, int KS, int PRO, int EPI>
@@ -549,11 +613,19 @@ int launch_t(const mv_args &a, int grid_x, hipStream_t s) {
         set_error("matvec: LDS image too large");
         return -1;
     }
+    // register ring depth (16 for gate/up measured slower: issue stalls at 32 loads per wave)
     constexpr int U = 8;
     constexpr int R = KS == 8 ? 4 : 1;  // activation blocks per quad held in registers
-    const void *fn = (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA>;
+    // one-shot when every wave owns at most one row tile of at most U items
+    const int64_t waves_x = (int64_t)grid_x * (KS > 1 ? 1 : threads / 64);
+    const bool one_shot = KS > 1 && seg <= U && waves_x >= a.n_rt;
+    const void *fn = one_shot ? (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1>
+                              : (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>;
     if (m.total > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m.total));
-    hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, a);
+    if (one_shot)
+        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, a);
+    else
+        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, a);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -240,10 +240,7 @@ constexpr int ATT_VPF = 8;      // V steps (of 32 positions) prefetched per thre
 __device__ __forceinline__ float quad_reduce_f16(const float acc[8], int t4) {
     float x0[8];
 #pragma unroll
-    for (int l = 0; l < 8; ++l) {
-        const float u = acc[l] + __shfl_xor(acc[l], 2);
-        x0[l] = u + __shfl_xor(u, 1);
-    }
+    for (int l = 0; l < 8; ++l) x0[l] = quad_fold_dpp(acc[l]);
     float t0[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) t0[i] = x0[i] + x0[i + 4];
@@ -293,8 +290,6 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     uint16_t *v16 = k16 + hd;                            // hd (this token's v)
     float *S = (float *)(smem + ((3 * hd * 2 + 15) & ~15));  // ctx
     uint16_t *P16 = (uint16_t *)(S + a.ctx);             // ctx
-    float *red = (float *)(P16 + a.ctx + 8);             // 16 floats, then 16 u64 (aligned below)
-    unsigned long long *red64 = (unsigned long long *)(((uintptr_t)(red + 16) + 7) & ~(uintptr_t)7);
 
     // RoPE NEOX on q (then * q_scale) and on k; f32 -> f16 (ggml_cpy / MUL_MAT INIT conversions)
     const float *cs = a.rope_cos + (int64_t)pos * half, *sn = a.rope_sin + (int64_t)pos * half;
@@ -359,37 +354,42 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     __syncthreads();
     if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
     // ---- soft_max_ext: max; e = table_exp[f16(w - max)]; exact sum; e * (float)(1/sum)
+    // Every wave reduces the whole row itself (DPP, no LDS round trip) and writes P16 for its own
+    // slice j = 64*wave + lane (+ blockDim.x*m): one barrier for the softmax instead of three.
+    const int lane = tid & 63, wave = tid >> 6;
     float mx = -INFINITY;
-    for (int j = tid; j < n_kv; j += blockDim.x) mx = fmaxf(mx, S[j]);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-    if ((tid & 63) == 0) red[tid >> 6] = mx;
-    __syncthreads();
-    mx = red[0];
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmaxf(mx, red[w]);
+    for (int j = lane; j < n_kv; j += 64) mx = fmaxf(mx, S[j]);
+    mx = wave_max(mx);
     if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
     // e values are fp16 in [0,1]: exact multiples of 2^-24, so an integer sum is the exact sum
     // (ggml's double accumulation of them is exact too).
     unsigned long long isum = 0;
-    for (int j = tid; j < n_kv; j += blockDim.x) {
+    float mine[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // e of this wave's own slice (n_kv <= 4 * blockDim.x)
+    for (int j = lane, k = 0; j < n_kv; j += 64, ++k) {
         const float w = S[j];
         float e = 0.0f;
         if (w != -INFINITY) e = h2f(a.exp_tab[f2h(w - mx)]);
-        S[j] = e;
         isum += (unsigned long long)(e * 16777216.0f);
+        const int r = k - wave;  // slot of j = 64*wave + lane + blockDim.x*m
+        if (r >= 0 && (r & ((int)(blockDim.x >> 6) - 1)) == 0) {
+            const int m = r / (int)(blockDim.x >> 6);
+            if (m == 0) mine[0] = e; else if (m == 1) mine[1] = e; else if (m == 2) mine[2] = e; else mine[3] = e;
+        }
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) isum += __shfl_xor(isum, off);
-    if ((tid & 63) == 0) red64[tid >> 6] = isum;
-    __syncthreads();
+    const unsigned long long tot = wave_sum_u64(isum);
     if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 4] = __builtin_amdgcn_s_memrealtime();
-    unsigned long long tot = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += red64[w];
     const double sum = (double)tot * (1.0 / 16777216.0);
     const float inv = (float)(1.0 / sum);
     if (a.dbg_inv && tid == 0 && ds == 0) a.dbg_inv[h] = inv;
-    for (int j = tid; j < n_kv; j += blockDim.x) {
-        P16[j] = f2h(S[j] * inv);
+    for (int j = tid, m = 0; j < n_kv; j += blockDim.x, ++m) {
+        float e;
+        if (m < 4) {
+            e = m == 0 ? mine[0] : m == 1 ? mine[1] : m == 2 ? mine[2] : mine[3];
+        } else {  // long rows: recompute (same table lookup, same value)
+            const float w = S[j];
+            e = w != -INFINITY ? h2f(a.exp_tab[f2h(w - mx)]) : 0.0f;
+        }
+        P16[j] = f2h(e * inv);
         if (a.dbg_p && ds == 0) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
     }
     __syncthreads();

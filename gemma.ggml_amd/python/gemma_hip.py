@@ -16,7 +16,7 @@ GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
 
 # exported symbols (checked against include/gemma_hpc.h by tests/test_capi_symbols.py)
 EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
-           "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
+           "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
            "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync"]
 
@@ -66,6 +66,8 @@ def lib():
     L.hpc_set_matvec_ks.argtypes = [C.c_int]
     L.gemma_engine_debug_step.restype = C.c_int
     L.gemma_engine_debug_step.argtypes = [vp, vp, vp]
+    L.gemma_engine_stamp_step.restype = C.c_int
+    L.gemma_engine_stamp_step.argtypes = [vp, C.c_int, vp]
     L.gemma_engine_create.restype = vp
     L.gemma_engine_create.argtypes = [C.POINTER(GemmaConfig), C.c_int]
     L.gemma_engine_free.argtypes = [vp]
@@ -175,6 +177,12 @@ class Engine:
         if n < 0:
             raise RuntimeError("tensor failed: " + last_error())
         return out[:n]
+
+    def stamp_step(self, layer):
+        """Diagnostics: one eager step; returns u64 stamps [6 regions][4096 workgroups][16 phases]."""
+        out = np.zeros(6 * 4096 * 16, dtype=np.uint64)
+        self._chk(self.L.gemma_engine_stamp_step(self.h, layer, _p(out)), "stamp_step")
+        return out.reshape(6, 4096, 16)
 
     def time_kernel(self, which, iters):
         b = C.c_double()

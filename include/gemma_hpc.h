@@ -77,6 +77,10 @@ double gemma_engine_time(gemma_engine *e, int which, int iters, double *algo_byt
 int gemma_engine_sync(gemma_engine *e);
 /* debugging: one eager step with per-layer taps [n_layer][qkv | attn_out | layer_out] */
 int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
+/* diagnostics: one eager step with s_memrealtime phase stamps (100 MHz) of layer `layer`'s five
+ * kernels (regions 0..4: qkv, attention, attn-out, gate/up, down) and the logits kernel (region 5);
+ * out = 6 * 4096 * 16 u64, slot [region][workgroup][phase], unused slots 0 */
+int gemma_engine_stamp_step(gemma_engine *e, int layer, unsigned long long *out);
 /* per-op test entry: one decode-attention block on host buffers (caches updated in place) */
 int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos, int H, int Hkv, int hd, int ctx,
                            float rope_base, float *out, float *dbg_w, uint16_t *dbg_p, float *dbg_inv,

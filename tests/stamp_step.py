@@ -1,0 +1,41 @@
+"""Diagnostic: in-step phase timeline of one layer's kernels (s_memrealtime stamps, 10 ns ticks).
+
+Prints, per kernel, the workgroup start spread and the median / max time of each phase end
+relative to the kernel's first workgroup start, and the gap from the previous kernel's last
+workgroup end to this kernel's first start."""
+import sys
+
+import numpy as np
+
+sys.path.insert(0, "gemma.ggml_amd/python")
+sys.path.insert(0, ".")
+import gemma_hip as G
+from bench import GEMMA_2B, make_prompt
+
+layer = int(sys.argv[1]) if len(sys.argv) > 1 else 9
+e = G.Engine(GEMMA_2B, n_ctx=512, device=0)
+e.begin(make_prompt(128, GEMMA_2B["n_vocab"]))
+e.step(140, use_graph=True)
+names = ["qkv", "attention", "attn-out", "gate/up", "down", "logits"]
+phases = {0: ["issue", "prologue", "sync", "stream", "end", "own", "carry0", "fma", "store", "sync2"], 1: ["rope", "KQ", "max", "sum", "P16", "KQV"]}
+for rep in range(2):
+    st = e.stamp_step(layer).astype(np.int64)
+prev_end = None
+for k, nm in enumerate(names):
+    r = st[k].reshape(-1, 8) if k == 1 else st[k]  # attention writes 8 stamps per workgroup
+    r = r[r[:, 0] != 0]
+    if len(r) == 0:
+        continue
+    t0 = r[:, 0].min()
+    ph = phases[1] if k == 1 else phases[0]
+    n = len(ph) + 1
+    rel = (r[:, :n] - t0) * 10
+    rel[r[:, :n] == 0] = -1
+    end = r[:, 6 if k == 1 else 5].max()
+    gap = (t0 - prev_end) * 10 if prev_end is not None else None
+    print(f"{nm:10s} WGs={len(r):5d} start spread {int((r[:, 0].max() - t0) * 10):6d} ns  gap {gap} ns  "
+          f"span {int((end - t0) * 10)} ns")
+    print("   median " + " ".join(f"{p}={int(v)}" for p, v in zip(["start"] + ph, np.median(rel, axis=0))))
+    print("   max    " + " ".join(f"{p}={int(v)}" for p, v in zip(["start"] + ph, rel.max(axis=0))))
+    prev_end = end
+e.close()
