@@ -153,8 +153,12 @@ struct gemma_engine {
     float *out_norm = nullptr;
     std::vector<layer_dev> layers;
     uint16_t *kc = nullptr, *vc = nullptr;  // [L][ctx][kvw], [L][kvw][ctx]
+    int att_mode = ATTN_PER_HEAD;
+    attn_geom ag;                           // split-attention geometry and its scratch
+    float *att_sbuf = nullptr;
+    int *att_sync = nullptr;                // hand-off counters [Hkv][2] + sticky error word
     uint16_t *exp_tab = nullptr, *gelu_tab = nullptr;
-    float *rope_cos = nullptr, *rope_sin = nullptr;
+    float *rope_cos = nullptr, *rope_sin = nullptr, *rope_cur = nullptr;
     // activations
     float *x = nullptr, *qkv = nullptr, *attn = nullptr, *sa = nullptr, *h = nullptr, *logits = nullptr;
     unsigned long long *key = nullptr;
@@ -215,10 +219,12 @@ static int enqueue_step(gemma_engine *e) {
         t.qkv = e->qkv;
         t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
         t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
-        t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.exp_tab = e->exp_tab;
+        t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.rope_cur = e->rope_cur; t.exp_tab = e->exp_tab;
         t.pos = e->pos; t.out = e->attn;
         t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
         t.q_scale = 1.0f / sqrtf((float)c.head_dim);
+        t.mode = e->att_mode;
+        t.nwg = e->ag.nwg; t.sbuf = e->att_sbuf; t.sync = e->att_sync; t.err = e->att_sync + e->ag.sync_ints;
         t.dbg_t = stamp_region(e, il, 1);
         if (launch_attn_decode(t, s)) return -1;
         const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
@@ -260,7 +266,9 @@ static int enqueue_step(gemma_engine *e) {
     if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, lg_grid, s)) return -1;
     // K7: token feedback (greedy_sample -> input.push_back, :282-285), position += 1
     // the prompt is never overwritten: hist writes only land at positions >= n_prompt
-    return launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, s);
+    rope_row rr;
+    rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+    return launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
 }
 
 extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int device) {
@@ -325,10 +333,23 @@ extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int de
     build_f16_tables(et, gt);
     std::vector<float> rc, rs;
     build_rope(c.n_ctx, c.head_dim, c.rope_base, rc, rs);
+    // attention form: one workgroup per head up to 2048 positions, the position-split form beyond
+    e->att_mode = (c.head_dim <= 256 && c.n_ctx <= 2048) ? ATTN_PER_HEAD : ATTN_SPLIT;
+    if (const char *v = getenv("GHIP_ATTN")) e->att_mode = strcmp(v, "split") == 0 ? ATTN_SPLIT : ATTN_PER_HEAD;
+    e->ag = attn_geometry(c.n_head, c.n_head_kv, c.head_dim, c.n_ctx);
+    if (e->att_mode == ATTN_SPLIT && !e->ag.nwg) {
+        set_error("gemma_engine_create: unsupported attention geometry");
+        gemma_engine_free(e);
+        return nullptr;
+    }
+    GHIP_FATAL(hipMalloc(&e->att_sbuf, std::max<size_t>(e->ag.sbuf_floats, 1) * 4));
+    GHIP_FATAL(hipMalloc(&e->att_sync, (e->ag.sync_ints + 1) * 4));
+    GHIP_FATAL(hipMemsetAsync(e->att_sync, 0, (e->ag.sync_ints + 1) * 4, s));
     GHIP_FATAL(hipMalloc(&e->exp_tab, 65536 * 2));
     GHIP_FATAL(hipMalloc(&e->gelu_tab, 65536 * 2));
     GHIP_FATAL(hipMalloc(&e->rope_cos, rc.size() * 4));
     GHIP_FATAL(hipMalloc(&e->rope_sin, rs.size() * 4));
+    GHIP_FATAL(hipMalloc(&e->rope_cur, (size_t)(c.head_dim + 4) * 4));  // [cos | sin | (int)pos]
     GHIP_FATAL(hipMemcpy(e->exp_tab, et.data(), 65536 * 2, hipMemcpyHostToDevice));
     GHIP_FATAL(hipMemcpy(e->gelu_tab, gt.data(), 65536 * 2, hipMemcpyHostToDevice));
     GHIP_FATAL(hipMemcpy(e->rope_cos, rc.data(), rc.size() * 4, hipMemcpyHostToDevice));
@@ -365,7 +386,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
         free_tiled(L.qkv); free_tiled(L.o); free_tiled(L.gate); free_tiled(L.up); free_tiled(L.down);
         (void)hipFree(L.attn_norm); (void)hipFree(L.ffn_norm);
     }
-    void *bufs[] = {e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
+    void *bufs[] = {e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
                     e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf_scratch};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
@@ -388,6 +409,10 @@ extern "C" int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_
     GHIP_CHECK(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
     GHIP_CHECK(hipMemcpyAsync(e->hist, prompt, (size_t)n_prompt * 4, hipMemcpyHostToDevice, s));
     GHIP_CHECK(hipMemsetAsync(e->pos, 0, 4, s));
+    const size_t half = (size_t)c.head_dim / 2;  // RoPE row of position 0
+    GHIP_CHECK(hipMemcpyAsync(e->rope_cur, e->rope_cos, half * 4, hipMemcpyDeviceToDevice, s));
+    GHIP_CHECK(hipMemcpyAsync(e->rope_cur + half, e->rope_sin, half * 4, hipMemcpyDeviceToDevice, s));
+    GHIP_CHECK(hipMemsetAsync(e->rope_cur + 2 * half, 0, 4, s));
     GHIP_CHECK(hipMemsetAsync(e->key, 0, (size_t)e->grid_big * 8, s));
     GHIP_CHECK(hipMemcpyAsync(e->nfix, &n_prompt, 4, hipMemcpyHostToDevice, s));
     GHIP_CHECK(hipStreamSynchronize(s));
@@ -637,7 +662,7 @@ extern "C" int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float 
 // qkv [H*hd + 2*Hkv*hd] f32; kc [ctx][Hkv*hd], vc [Hkv*hd][ctx] f16 (updated in place at pos)
 extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos, int H, int Hkv, int hd,
                                       int ctx, float rope_base, float *out, float *dbg_w, uint16_t *dbg_p,
-                                      float *dbg_inv, unsigned long long *dbg_t) {
+                                      float *dbg_inv, unsigned long long *dbg_t, int mode) {
     set_error("");
     const size_t qkv_n = (size_t)(H + 2 * Hkv) * hd, cache_n = (size_t)ctx * Hkv * hd;
     std::vector<uint16_t> et, gt;
@@ -671,8 +696,24 @@ extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *
     GHIP_CHECK(hipMemcpy(d_v, vc, cache_n * 2, hipMemcpyHostToDevice));
     GHIP_CHECK(hipMemcpy(d_e, et.data(), 65536 * 2, hipMemcpyHostToDevice));
     GHIP_CHECK(hipMemcpy(d_pos, &pos, 4, hipMemcpyHostToDevice));
+    const attn_geom g = attn_geometry(H, Hkv, hd, ctx);
+    float *d_sb = nullptr;
+    int *d_sy = nullptr;
+    if (g.nwg) {
+        GHIP_CHECK(hipMalloc(&d_sb, g.sbuf_floats * 4));
+        GHIP_CHECK(hipMalloc(&d_sy, (g.sync_ints + 1) * 4));
+        GHIP_CHECK(hipMemset(d_sy, 0, (g.sync_ints + 1) * 4));
+    }
     attn_args a;
     a.qkv = d_qkv; a.kc = d_k; a.vc = d_v; a.rope_cos = d_c; a.rope_sin = d_s; a.exp_tab = d_e; a.pos = d_pos;
+    a.nwg = g.nwg; a.sbuf = d_sb; a.sync = d_sy; a.err = d_sy ? d_sy + g.sync_ints : nullptr;
+    float *d_rc = nullptr;
+    GHIP_CHECK(hipMalloc(&d_rc, (size_t)(hd + 4) * 4));
+    GHIP_CHECK(hipMemcpy(d_rc, rc.data() + (size_t)pos * (hd / 2), (size_t)(hd / 2) * 4, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_rc + hd / 2, rs.data() + (size_t)pos * (hd / 2), (size_t)(hd / 2) * 4, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_rc + hd, &pos, 4, hipMemcpyHostToDevice));
+    a.rope_cur = d_rc;
+    a.mode = mode;
     a.out = d_out; a.H = H; a.Hkv = Hkv; a.hd = hd; a.ctx = ctx; a.q_scale = 1.0f / sqrtf((float)hd);
     a.dbg_w = d_dw; a.dbg_p = d_dp; a.dbg_inv = d_di; a.dbg_t = d_dt;
     int r = 0;
@@ -687,7 +728,15 @@ extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *
         if (dbg_inv) GHIP_CHECK(hipMemcpy(dbg_inv, d_di, (size_t)H * 4, hipMemcpyDeviceToHost));
         if (dbg_t) GHIP_CHECK(hipMemcpy(dbg_t, d_dt, n_stamps * 8, hipMemcpyDeviceToHost));
     }
-    void *bufs[] = {d_qkv, d_out, d_c, d_s, d_k, d_v, d_e, d_pos, d_dw, d_dp, d_di, d_dt};
+    if (r == 0 && d_sy) {
+        int err = 0;
+        GHIP_CHECK(hipMemcpy(&err, d_sy + g.sync_ints, 4, hipMemcpyDeviceToHost));
+        if (err) {
+            set_error("attn_decode: hand-off spin timed out");
+            r = -1;
+        }
+    }
+    void *bufs[] = {d_qkv, d_out, d_c, d_s, d_k, d_v, d_e, d_pos, d_dw, d_dp, d_di, d_dt, d_sb, d_sy, d_rc};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     return r;

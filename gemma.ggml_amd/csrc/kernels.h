@@ -59,10 +59,12 @@ int launch_synth_norm(float *dst, int64_t n, uint64_t key, float scale, hipStrea
 int launch_untile(const tiled_mat &m, uint8_t *dst_rowmajor, hipStream_t s);
 
 // ---- small decode ops (ops.hip) -----------------------------------------------------------------
+enum attn_mode { ATTN_PER_HEAD = 0, ATTN_SPLIT = 1 };
 struct attn_args {
     const float *qkv;       // [q(H*hd) | k(Hkv*hd) | v(Hkv*hd)] for one token
     uint16_t *kc, *vc;      // layer caches: K [ctx][Hkv*hd], V [Hkv*hd][ctx] (f16 bits)
     const float *rope_cos, *rope_sin;  // [ctx][hd/2]
+    const float *rope_cur = nullptr;   // [cos | sin | (int)pos] of *pos (k_advance keeps it current)
     const uint16_t *exp_tab;
     const int *pos;         // device scalar (position of this token)
     float *out;             // [H*hd]
@@ -72,13 +74,30 @@ struct attn_args {
     uint16_t *dbg_p = nullptr;
     float *dbg_inv = nullptr;
     unsigned long long *dbg_t = nullptr;  // diagnostic phase stamps (s_memrealtime), [grid][8]
+    int mode = 0;  // ATTN_PER_HEAD (one workgroup per head) or ATTN_SPLIT (long contexts)
+    // split form: workgroups per kv head, scores scratch [Hkv][ctx][G], hand-off counters [Hkv][2]
+    // (zero before the first launch; each launch leaves them zero), sticky error word
+    int nwg = 0;
+    float *sbuf = nullptr;
+    int *sync = nullptr;
+    int *err = nullptr;
 };
+struct attn_geom {
+    int nwg = 0, grid = 0;
+    size_t lds = 0, sbuf_floats = 0, sync_ints = 0;
+};
+attn_geom attn_geometry(int H, int Hkv, int hd, int ctx);
 int launch_attn_decode(const attn_args &a, hipStream_t s);
 int launch_embed(const uint8_t *qs, const uint8_t *sc, int wtype, int64_t n_bt, const int *token, float scale,
                  float *out, int64_t E, hipStream_t s);
 // reduces the n_parts per-workgroup argmax keys, appends the token, advances the position
+struct rope_row {  // k_advance also publishes the new position's RoPE row: cur = [cos | sin | (int)pos]
+    const float *cos = nullptr, *sin = nullptr;
+    float *cur = nullptr;
+    int half = 0, ctx = 0;
+};
 int launch_advance(const unsigned long long *keys, int n_parts, int *token, int *pos, int *hist, int hist_cap,
-                   const int *n_fixed, hipStream_t s);
+                   const int *n_fixed, const rope_row &r, hipStream_t s);
 
 // ---- generic ggml-op kernels used by the C-ABI and the ggml-compatible executor ----------------
 int launch_mul_mat_f16(const uint16_t *src0, int64_t nb01_elems, int64_t ne01, const uint16_t *src1,

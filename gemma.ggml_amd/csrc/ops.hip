@@ -5,8 +5,11 @@
 //    oracle/gemma_cpu.cpp; DESIGN.md §Synthetic weights), writing straight into the tiled layout.
 //  * k_attn_decode: RoPE-NEOX (src/gemma_model.cpp:698-716) + q scale (:708) + KV store (:499-518)
 //    + KQ (:474) + soft_max_ext (:476) + KQV (:485) + permute/cont (:487-489) for one token, with
-//    ggml's AVX/F16C vec_dot_f16 order and the fp16 exp table (A.6).
+//    ggml's AVX/F16C vec_dot_f16 order and the fp16 exp table (A.6); split over the
+//    workgroups of each kv group with one in-kernel sc1 hand-off of the scores.
 //  * k_embed, k_advance (greedy token feedback), k_mul_mat_f16 (C-ABI F16 path).
+#include <algorithm>
+
 #include "device_util.h"
 #include "kernels.h"
 
@@ -230,14 +233,15 @@ __device__ __forceinline__ void f16_step(float acc[4][8], const uint4 *x4, const
     }
 }
 
-constexpr int ATT_THREADS = 1024;
-constexpr int ATT_DCHUNK = 256;  // KQV outputs per workgroup: grid = (H, hd / 256): one pass of 256 quads
-constexpr int ATT_KPF = 8;      // K steps (of 32 elements) prefetched per thread: hd <= 256
-constexpr int ATT_VPF = 8;      // V steps (of 32 positions) prefetched per thread: n_kv <= 256
+constexpr int ATT_THREADS = 256;
+constexpr int ATT_QUADS = ATT_THREADS / 4;  // 64 quads: one KQ (position, head) or KQV (dim, head) each
+constexpr int ATT_VW = 256;                 // V positions staged in LDS per dimension row (n_kv <= 256)
+constexpr int ATT_STG = 2;                  // staging uint4 per thread for each of K and V
+constexpr int ATT_MAXWG = 256;              // co-resident workgroups (in-kernel hand-off)
 
 // ggml_vec_dot_f16 with accumulator row j = t4 held by lane t4 of a quad: fold the
 // quad exactly as sum0+=sum2, sum1+=sum3, sum0+=sum1 (xor-2 then xor-1), then halves and hadds.
-__device__ __forceinline__ float quad_reduce_f16(const float acc[8], int t4) {
+__device__ __forceinline__ float quad_reduce_f16(const float acc[8]) {
     float x0[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) x0[l] = quad_fold_dpp(acc[l]);
@@ -245,143 +249,478 @@ __device__ __forceinline__ float quad_reduce_f16(const float acc[8], int t4) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) t0[i] = x0[i] + x0[i + 4];
     const float h0 = t0[0] + t0[1], h1 = t0[2] + t0[3];
-    (void)t4;
     return h0 + h1;
 }
 
+// acc = fmaf((float)x16, (float)y16, acc) in ONE instruction: v_fma_mix_f32 converts its f16
+// operands exactly and rounds the fused result once — the F16C/FMA step of ggml_vec_dot_f16.
+__device__ __forceinline__ float fma_mix_lo(uint32_t x, uint32_t y, float acc) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(r) : "v"(x), "v"(y), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ float fma_mix_hi(uint32_t x, uint32_t y, float acc) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "=v"(r) : "v"(x), "v"(y), "v"(acc));
+    return r;
+}
 __device__ __forceinline__ void f16_step8(float acc[8], uint4 xv, uint4 yv) {
     const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w}, ys[4] = {yv.x, yv.y, yv.z, yv.w};
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        acc[2 * w] = __builtin_fmaf(h2f(xs[w]), h2f(ys[w]), acc[2 * w]);
-        acc[2 * w + 1] = __builtin_fmaf(h2f(xs[w] >> 16), h2f(ys[w] >> 16), acc[2 * w + 1]);
+        acc[2 * w] = fma_mix_lo(xs[w], ys[w], acc[2 * w]);
+        acc[2 * w + 1] = fma_mix_hi(xs[w], ys[w], acc[2 * w + 1]);
     }
 }
 
-// One token's attention for head h = blockIdx.x, KQV outputs [64*blockIdx.y, +64).  Every
-// workgroup recomputes the (cheap) RoPE, KQ and softmax of its head.  Quads of lanes own one KQ
-// position (or one KQV output): lane t4 runs accumulator row j = t4 of the AVX/F16C loop.  The
-// K rows and V rows of the first pass are requested at kernel entry, before RoPE.
+// positions per KQ block (PS) and dims per KQV workgroup (DS): quads = PS*G and DS*G <= 64, and
+// the staged K rows (PS*hd halfs) and V rows (DS*ATT_VW halfs) fit ATT_STG uint4 per thread
+struct attn_split {
+    int ps, ds;
+};
+__host__ __device__ inline attn_split attn_split_of(int G, int hd) {
+    int ps = ATT_QUADS / G, ds = ATT_QUADS / G;
+    const int cap = ATT_STG * ATT_THREADS * 8;  // halfs
+    if (ps * hd > cap) ps = cap / hd;
+    if (ds * ATT_VW > cap) ds = cap / ATT_VW;
+    return {ps, ds};
+}
+
+// Cross-workgroup hand-off (MI355X_MICROARCH §inter-workgroup visibility, row 1 of the sc1 table):
+// every byte handed off is stored and loaded with global sc1 accesses; each storing wave drains
+// vmcnt before the workgroup barrier, then one lane adds to the counter; the consumer polls the
+// counter with an sc1 load and joins a barrier before any of its sc1 loads.
+typedef __attribute__((address_space(1))) float gfloat_t;
+typedef __attribute__((address_space(1))) int gint_t;
+__device__ __forceinline__ void st_sc1(float *p, float v) {
+    __hip_atomic_store((gfloat_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float *p) {
+    return __hip_atomic_load((const gfloat_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_sc1_i(const int *p) {
+    return __hip_atomic_load((const gint_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+#define ATT_STAMP(i)                                                                                        \
+    do {                                                                                                    \
+        if (a.dbg_t && tid == 0) a.dbg_t[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+// One token's attention for the G = H/Hkv query heads of kv head kvh = blockIdx.x / nwg, split over
+// the group's nwg workgroups (wg = blockIdx.x % nwg) in two phases joined by an in-kernel hand-off:
+//  A) KQ: position blocks of PS positions, block b -> workgroup b % nwg.  Quad q scores (position
+//     q / G, head q % G) from the block's K rows staged once in LDS.  Scores (masked j > pos ->
+//     -inf) go to sbuf[kvh][j][h].
+//  B) softmax + KQV: every workgroup re-derives each head's exact softmax from all scores (the
+//     reduction is exact, so redundancy is free of order effects), then workgroup wg < nb computes
+//     out[h][d] for d in [wg*DS, +DS): quad q owns (dim q / G, head q % G).
+// The per-position / per-output arithmetic is exactly that of a single-workgroup form: RoPE, f16
+// conversions, vec_dot_f16 order, exp table, integer-exact sum, (float)(1/sum).
 __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int hd = a.hd, half = hd / 2, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
-    const int h = blockIdx.x, ds = blockIdx.y, grp = a.H / a.Hkv, kvh = h / grp;
-    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-    const int pos = *a.pos;
-    const int n_total = pos + 1;
-    int n_kv = 32 * (n_total / 32 + 1);                    // src/gemma_model.cpp:429
-    if (n_kv > a.ctx) n_kv = a.ctx;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int G = a.H / a.Hkv, nwg = a.nwg, kvh = blockIdx.x / nwg, wg = blockIdx.x % nwg;
+    const attn_split sp = attn_split_of(G, hd);
+    const int PS = sp.ps, DS = sp.ds;
+    const int nb = (hd + DS - 1) / DS;  // workgroups with KQV work
     const int kvw = a.Hkv * hd;
-    const int nq = blockDim.x >> 2;                      // quads per workgroup (64)
-    // ---- early loads: first KQ pass (position `quad`) and the first V steps of output d
-    const int d0 = ds * ATT_DCHUNK + quad;
-    const uint16_t *vrow = a.vc + ((int64_t)kvh * hd + (d0 < hd ? d0 : 0)) * a.ctx;
-    uint4 kpre[ATT_KPF], vpre[ATT_VPF];
-    {
-        const int j = quad < a.ctx ? quad : 0;           // no dependency on *pos: rows >= pos are masked
-        const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
+    ATT_STAMP(0);
+    // ---- early loads (issue order = wait order): RoPE inputs, then the K and V rows to stage
+    const float *qg = a.qkv + (int64_t)kvh * G * hd;
+    const float *kh = a.qkv + (int64_t)a.H * hd + (int64_t)kvh * hd;
+    const float *vh = a.qkv + (int64_t)a.H * hd + kvw + (int64_t)kvh * hd;
+    const float *cs = a.rope_cur, *sn = a.rope_cur + half;  // row of *pos (k_advance keeps it)
+    // q: thread t takes 4 consecutive pairs (h, e..e+3) of the G*half pairs (npair % 4 == 0)
+    const int npair = G * half, nq4 = npair / 4;
+    float4 qa[2], qb[2], ca[2], sa[2];
 #pragma unroll
-        for (int s = 0; s < ATT_KPF; ++s) kpre[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
-#pragma unroll
-        for (int s = 0; s < ATT_VPF; ++s) vpre[s] = *(const uint4 *)(vrow + (s * 32 < a.ctx ? s * 32 : 0) + t4 * 8);
+    for (int r = 0; r < 2; ++r) {
+        const int i4 = tid + r * ATT_THREADS;
+        const int i = (i4 < nq4 ? i4 : 0) * 4;
+        const int h = i / half, e = i % half;
+        qa[r] = *(const float4 *)(qg + h * hd + e);
+        qb[r] = *(const float4 *)(qg + h * hd + e + half);
+        ca[r] = *(const float4 *)(cs + e);
+        sa[r] = *(const float4 *)(sn + e);
     }
-    uint16_t *q16 = (uint16_t *)smem;                    // hd
-    uint16_t *k16 = q16 + hd;                            // hd (this token's k, post-rope)
-    uint16_t *v16 = k16 + hd;                            // hd (this token's v)
-    float *S = (float *)(smem + ((3 * hd * 2 + 15) & ~15));  // ctx
-    uint16_t *P16 = (uint16_t *)(S + a.ctx);             // ctx
+    const int kq4 = half / 4;  // k: 4 pairs per thread for tid < half/4
+    const int ik = (tid < kq4 ? tid : 0) * 4;
+    const float4 ka = *(const float4 *)(kh + ik), kb = *(const float4 *)(kh + ik + half);
+    const float4 kc4 = *(const float4 *)(cs + ik), ks4 = *(const float4 *)(sn + ik);
+    // phase A, first position block of this workgroup: its PS K rows, one coalesced uint4 each
+    const int kcw = hd / 8;  // uint4 per K row
+    uint4 kst[ATT_STG];
+#pragma unroll
+    for (int r = 0; r < ATT_STG; ++r) {
+        const int idx = tid + r * ATT_THREADS;
+        const int row = idx / kcw, c = idx % kcw;
+        int j = wg * PS + row;
+        j = (idx < PS * kcw && j < a.ctx) ? j : 0;  // rows >= pos are masked; no dependency on pos
+        kst[r] = *(const uint4 *)(a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + c * 8);
+    }
+    // phase B: V rows d of [wg*DS, +DS), positions [0, ATT_VW), one coalesced uint4 each
+    constexpr int vcw = ATT_VW / 8;
+    uint4 vst[ATT_STG];
+    float vsx[ATT_STG];
+#pragma unroll
+    for (int r = 0; r < ATT_STG; ++r) {
+        const int idx = tid + r * ATT_THREADS;
+        const int dd = idx / vcw, c = idx % vcw;
+        int d = wg * DS + dd;
+        d = (idx < DS * vcw && d < hd && wg < nb) ? d : 0;
+        vst[r] = *(const uint4 *)(a.vc + ((int64_t)kvh * hd + d) * a.ctx + (c * 8 < a.ctx ? c * 8 : 0));
+        vsx[r] = vh[d];  // this token's v of the row (patched into the staged copy)
+    }
+    const int pa = quad / G < PS ? quad / G : 0, ha = quad % G;
+    const bool has_a = quad / G < PS;
+    const int db = wg * DS + quad / G, hb = quad % G;
+    const bool has_b = wg < nb && quad / G < DS && db < hd;
+    const uint16_t *vrow = a.vc + ((int64_t)kvh * hd + (has_b ? db : 0)) * a.ctx;
+    const float vx = has_b ? vh[db] : 0.0f;
+    ATT_STAMP(6);
+    // pos is published with the RoPE row (k_advance / begin): no dependent load
+    const int pos = __builtin_amdgcn_readfirstlane(((const int *)a.rope_cur)[hd]);
+    const int n_total = pos + 1;
+    int n_kv = 32 * (n_total / 32 + 1);  // src/gemma_model.cpp:429
+    if (n_kv > a.ctx) n_kv = a.ctx;
+    ATT_STAMP(7);
+
+    // LDS: q16 [G][hd], k16 [hd], Ks [PS][hd], Vs [DS][ATT_VW], P16 [G][ctx]
+    uint16_t *q16 = (uint16_t *)smem;
+    uint16_t *k16 = q16 + (size_t)G * hd;
+    uint16_t *Ks = k16 + hd;
+    uint16_t *Vs = Ks + (size_t)PS * hd;
+    uint16_t *P16 = Vs + (size_t)DS * ATT_VW;
 
     // RoPE NEOX on q (then * q_scale) and on k; f32 -> f16 (ggml_cpy / MUL_MAT INIT conversions)
-    const float *cs = a.rope_cos + (int64_t)pos * half, *sn = a.rope_sin + (int64_t)pos * half;
+    auto rope4 = [&](float4 x0v, float4 x1v, float4 cv, float4 sv, float scale, bool scaled, uint16_t *lo,
+                     uint16_t *hi) {
+        const float x0s[4] = {x0v.x, x0v.y, x0v.z, x0v.w}, x1s[4] = {x1v.x, x1v.y, x1v.z, x1v.w};
+        const float cs4[4] = {cv.x, cv.y, cv.z, cv.w}, sn4[4] = {sv.x, sv.y, sv.z, sv.w};
+        uint32_t l2[2] = {0, 0}, h2[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float x0 = x0s[k], x1 = x1s[k], c = cs4[k], s = sn4[k];
+            const float p0 = x0 * c, p1 = x1 * s, p2 = x0 * s, p3 = x1 * c;
+            const float r0 = p0 - p1, r1 = p2 + p3;
+            const uint32_t a0 = scaled ? f2h(r0 * scale) : f2h(r0), a1 = scaled ? f2h(r1 * scale) : f2h(r1);
+            l2[k >> 1] |= a0 << (16 * (k & 1));
+            h2[k >> 1] |= a1 << (16 * (k & 1));
+        }
+        *(uint2 *)lo = make_uint2(l2[0], l2[1]);
+        *(uint2 *)hi = make_uint2(h2[0], h2[1]);
+    };
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int i4 = tid + r * ATT_THREADS;
+        if (i4 < nq4) {
+            const int i = i4 * 4, h = i / half, e = i % half;
+            rope4(qa[r], qb[r], ca[r], sa[r], a.q_scale, true, q16 + h * hd + e, q16 + h * hd + e + half);
+        }
+    }
+    for (int i4 = tid + 2 * ATT_THREADS; i4 < nq4; i4 += ATT_THREADS) {  // G * hd > 4096 (rare)
+        const int i = i4 * 4, h = i / half, e = i % half;
+        rope4(*(const float4 *)(qg + h * hd + e), *(const float4 *)(qg + h * hd + e + half), *(const float4 *)(cs + e),
+              *(const float4 *)(sn + e), a.q_scale, true, q16 + h * hd + e, q16 + h * hd + e + half);
+    }
+    if (tid < kq4) rope4(ka, kb, kc4, ks4, 1.0f, false, k16 + ik, k16 + ik + half);
+    // stage K and V rows (V patched at `pos`: this token's cache write is not visible in-launch)
+#pragma unroll
+    for (int r = 0; r < ATT_STG; ++r) {
+        const int idx = tid + r * ATT_THREADS;
+        if (idx < PS * kcw) *(uint4 *)(Ks + (size_t)idx * 8) = kst[r];
+        if (idx < DS * vcw) {
+            const int c = idx % vcw;
+            uint4 v = vst[r];
+            if (pos >= c * 8 && pos < c * 8 + 8) {
+                const uint32_t h = f2h(vsx[r]), sh = 16 * ((pos - c * 8) & 1);
+                const uint32_t m = ~(0xFFFFu << sh);
+                switch ((pos - c * 8) >> 1) {
+                    case 0: v.x = (v.x & m) | (h << sh); break;
+                    case 1: v.y = (v.y & m) | (h << sh); break;
+                    case 2: v.z = (v.z & m) | (h << sh); break;
+                    default: v.w = (v.w & m) | (h << sh); break;
+                }
+            }
+            *(uint4 *)(Vs + (size_t)idx * 8) = v;
+        }
+    }
+    __syncthreads();
+    ATT_STAMP(1);
+    // this token's cache entries (src/gemma_model.cpp:506-517): K row by workgroup 0, V column
+    // `pos` by the KQV workgroup owning each dimension
+    if (wg == 0)
+        for (int i = tid; i < hd; i += ATT_THREADS) a.kc[(int64_t)pos * kvw + (int64_t)kvh * hd + i] = k16[i];
+    if (has_b && hb == 0 && t4 == 0) a.vc[((int64_t)kvh * hd + db) * a.ctx + pos] = f2h(vx);
+
+    // ---- phase A: KQ (vec_dot_f16 over hd per kv position) + mask (j > pos -> -inf), scale 1.0
+    float *sk_out = a.sbuf + (int64_t)kvh * a.ctx * G;  // [ctx][G]
+    for (int blk = wg, pass = 0; blk * PS < n_kv; blk += nwg, ++pass) {
+        const int j = blk * PS + pa;
+        float acc[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+        const uint16_t *qh16 = q16 + (size_t)ha * hd + t4 * 8;
+        if (pass == 0) {  // staged rows (LDS); row `pos` from this token's k16
+            const uint16_t *krow = ((j == pos) ? k16 : Ks + (size_t)pa * hd) + t4 * 8;
+            for (int s = 0; s * 32 < hd; ++s)
+                f16_step8(acc, *(const uint4 *)(krow + s * 32), *(const uint4 *)(qh16 + s * 32));
+        } else {
+            const int jc = j < pos ? j : pos;
+            if (jc == pos) {
+                for (int s = 0; s * 32 < hd; ++s)
+                    f16_step8(acc, *(const uint4 *)(k16 + s * 32 + t4 * 8), *(const uint4 *)(qh16 + s * 32));
+            } else {
+                const uint16_t *krow = a.kc + (int64_t)jc * kvw + (int64_t)kvh * hd + t4 * 8;
+                for (int s = 0; s * 32 < hd; ++s)
+                    f16_step8(acc, *(const uint4 *)(krow + s * 32), *(const uint4 *)(qh16 + s * 32));
+            }
+        }
+        const float kq = quad_reduce_f16(acc);
+        if (t4 == 0 && has_a && j < n_kv) {
+            const float w = (j > pos) ? -INFINITY : kq * 1.0f + 0.0f;
+            st_sc1(sk_out + (int64_t)j * G + ha, w);
+            if (a.dbg_w) a.dbg_w[(int64_t)(kvh * G + ha) * a.ctx + j] = w;
+        }
+    }
+    // publish: every storing wave drains its stores, then one lane arrives
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ATT_STAMP(2);
+    int *cnt = a.sync + kvh * 2;
+    if (tid == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wg >= nb) return;  // no KQV work for this workgroup
+
+    // ---- hand-off: wait for all nwg workgroups of this kv head (bounded spin)
+    if (tid == 0) {
+        int spins = 0;
+        while (ld_sc1_i(cnt) < nwg) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1 << 26)) {  // never on a healthy device: flag and fall through
+                if (a.err) *a.err = 1;
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    ATT_STAMP(3);
+
+    // ---- soft_max_ext per head h: one wave reduces a head's scores (DPP, exact)
+    for (int h = wave; h < G; h += ATT_THREADS / 64) {
+        float mx = -INFINITY;
+        float sv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = lane + 64 * k;
+            sv[k] = j < n_kv ? ld_sc1(sk_out + (int64_t)j * G + h) : -INFINITY;
+            mx = fmaxf(mx, sv[k]);
+        }
+        for (int j = lane + 256; j < n_kv; j += 64) mx = fmaxf(mx, ld_sc1(sk_out + (int64_t)j * G + h));
+        mx = wave_max(mx);
+        // e values are fp16 in [0,1]: exact multiples of 2^-24, so an integer sum is the exact sum
+        // (ggml's double accumulation of them is exact too).  e is parked as f16 in P16.
+        unsigned long long isum = 0;
+        uint16_t *prow = P16 + (size_t)h * a.ctx;
+        for (int j = lane, k = 0; j < n_kv; j += 64, ++k) {
+            const float w = k < 4 ? (k == 0 ? sv[0] : k == 1 ? sv[1] : k == 2 ? sv[2] : sv[3])
+                                  : ld_sc1(sk_out + (int64_t)j * G + h);
+            uint16_t e16 = 0;
+            if (w != -INFINITY) e16 = a.exp_tab[f2h(w - mx)];
+            prow[j] = e16;
+            isum += (unsigned long long)(h2f(e16) * 16777216.0f);
+        }
+        const unsigned long long tot = wave_sum_u64(isum);
+        const double sum = (double)tot * (1.0 / 16777216.0);
+        const float inv = (float)(1.0 / sum);
+        if (a.dbg_inv && lane == 0 && wg == 0) a.dbg_inv[kvh * G + h] = inv;
+        for (int j = lane; j < n_kv; j += 64) {
+            const uint16_t p = f2h(h2f(prow[j]) * inv);
+            prow[j] = p;
+            if (a.dbg_p && wg == 0) a.dbg_p[(int64_t)(kvh * G + h) * a.ctx + j] = p;
+        }
+    }
+    __syncthreads();
+    ATT_STAMP(4);
+    // hand-off bookkeeping: the last KQV workgroup to get here resets the counters for the next
+    // launch (every other workgroup of this kv head has already passed its poll)
+    if (tid == 0) {
+        const int done = __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == nb - 1) {
+            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+
+    // ---- KQV: out[h][d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16[h]); lane t4 = accumulator j
+    if (has_b) {
+        float acc[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+        const uint16_t *prow = P16 + (size_t)hb * a.ctx;
+        const uint16_t *vs = Vs + (size_t)(db - wg * DS) * ATT_VW;
+        for (int st = 0; st < n_kv; st += 32) {
+            const int e0 = st + t4 * 8;
+            uint4 xv;
+            if (st < ATT_VW) {  // staged (and already patched at `pos`)
+                xv = *(const uint4 *)(vs + e0);
+            } else {
+                xv = *(const uint4 *)(vrow + e0);
+                if (pos >= e0 && pos < e0 + 8) {  // this token's V: its cache write may not be visible
+                    __attribute__((aligned(16))) uint16_t tmp[8];
+                    *(uint4 *)tmp = xv;
+                    tmp[pos - e0] = f2h(vx);
+                    xv = *(const uint4 *)tmp;
+                }
+            }
+            f16_step8(acc, xv, *(const uint4 *)(prow + e0));
+        }
+        const float o = quad_reduce_f16(acc);
+        if (t4 == 0) a.out[(int64_t)(kvh * G + hb) * hd + db] = o;
+    }
+    ATT_STAMP(5);
+}
+
+constexpr int AH_THREADS = 1024;  // per-head form: 256 quads = 256 KQ positions / KQV dims per pass
+constexpr int AH_KPF = 8;         // K steps (of 32 elements) prefetched per lane: hd <= 256
+constexpr int AH_VPF = 8;         // V steps (of 32 positions) prefetched per lane: n_kv <= 256
+
+#define AH_STAMP(i)                                                                                         \
+    do {                                                                                                    \
+        if (a.dbg_t && tid == 0) a.dbg_t[(int64_t)(blockIdx.x >> 3) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+// One token's attention for query head h, one 1024-thread workgroup per head (SURVEY A.4/A.6 order,
+// same arithmetic as the split form).  The grid is 8*H workgroups and only blockIdx % 8 == kvh % 8
+// works: blocks b and b+8 share an XCD (MI355X_MICROARCH §dispatch; speed only, never correctness),
+// so the G heads reading one kv head's K/V rows meet in one L2 and the rows leave HBM once.
+__global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int hd = a.hd, half = hd / 2, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
+    const int lane = tid & 63, wave = tid >> 6, nwave = AH_THREADS / 64;
+    const int G = a.H / a.Hkv, h = blockIdx.x >> 3, kvh = h / G;
+    if ((int)(blockIdx.x & 7) != (kvh & 7)) return;
+    AH_STAMP(0);
+    const int kvw = a.Hkv * hd;
     const float *qh = a.qkv + (int64_t)h * hd;
     const float *kh = a.qkv + (int64_t)a.H * hd + (int64_t)kvh * hd;
     const float *vh = a.qkv + (int64_t)a.H * hd + kvw + (int64_t)kvh * hd;
-    for (int i = tid; i < half; i += blockDim.x) {
-        const float c = cs[i], s = sn[i];
-        {
-            const float x0 = qh[i], x1 = qh[i + half];
+    const float *cs = a.rope_cur, *sn = a.rope_cur + half;
+    // ---- early loads (issue order = wait order): RoPE inputs + pos, then K rows, then V rows
+    const int n4 = half / 4, i4 = (tid < n4 ? tid : 0) * 4;
+    const float4 qa = *(const float4 *)(qh + i4), qb = *(const float4 *)(qh + i4 + half);
+    const float4 ka = *(const float4 *)(kh + i4), kb = *(const float4 *)(kh + i4 + half);
+    const float4 ca = *(const float4 *)(cs + i4), sa = *(const float4 *)(sn + i4);
+    const int pos_v = ((const int *)a.rope_cur)[hd];  // published with the row (k_advance / begin)
+    uint4 kpre[AH_KPF];
+    {
+        const int j = quad < a.ctx ? quad : 0;  // no dependency on pos: rows >= pos are masked
+        const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
+#pragma unroll
+        for (int s = 0; s < AH_KPF; ++s) kpre[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
+    }
+    const int d0 = quad < hd ? quad : 0;
+    const uint16_t *vrow0 = a.vc + ((int64_t)kvh * hd + d0) * a.ctx;
+    uint4 vpre[AH_VPF];
+#pragma unroll
+    for (int s = 0; s < AH_VPF; ++s) vpre[s] = *(const uint4 *)(vrow0 + (s * 32 < a.ctx ? s * 32 : 0) + t4 * 8);
+    const float vx0 = vh[d0];
+    const int pos = __builtin_amdgcn_readfirstlane(pos_v);
+    const int n_total = pos + 1;
+    int n_kv = 32 * (n_total / 32 + 1);  // src/gemma_model.cpp:429
+    if (n_kv > a.ctx) n_kv = a.ctx;
+
+    uint16_t *q16 = (uint16_t *)smem;  // hd
+    uint16_t *k16 = q16 + hd;          // hd (this token's k, post-rope)
+    float *S = (float *)(smem + ((2 * hd * 2 + 15) & ~15));  // ctx
+    uint16_t *P16 = (uint16_t *)(S + a.ctx);                 // ctx
+
+    // RoPE NEOX on q (then * q_scale) and on k; f32 -> f16 (ggml_cpy / MUL_MAT INIT conversions)
+    auto rope4 = [&](float4 x0v, float4 x1v, float scale, bool scaled, uint16_t *lo, uint16_t *hi) {
+        const float x0s[4] = {x0v.x, x0v.y, x0v.z, x0v.w}, x1s[4] = {x1v.x, x1v.y, x1v.z, x1v.w};
+        const float cs4[4] = {ca.x, ca.y, ca.z, ca.w}, sn4[4] = {sa.x, sa.y, sa.z, sa.w};
+        uint32_t l2[2] = {0, 0}, h2[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float x0 = x0s[k], x1 = x1s[k], c = cs4[k], s = sn4[k];
             const float p0 = x0 * c, p1 = x1 * s, p2 = x0 * s, p3 = x1 * c;
             const float r0 = p0 - p1, r1 = p2 + p3;
-            q16[i] = f2h(r0 * a.q_scale);
-            q16[i + half] = f2h(r1 * a.q_scale);
+            const uint32_t a0 = scaled ? f2h(r0 * scale) : f2h(r0), a1 = scaled ? f2h(r1 * scale) : f2h(r1);
+            l2[k >> 1] |= a0 << (16 * (k & 1));
+            h2[k >> 1] |= a1 << (16 * (k & 1));
         }
-        {
-            const float x0 = kh[i], x1 = kh[i + half];
-            const float p0 = x0 * c, p1 = x1 * s, p2 = x0 * s, p3 = x1 * c;
-            k16[i] = f2h(p0 - p1);
-            k16[i + half] = f2h(p2 + p3);
-        }
+        *(uint2 *)lo = make_uint2(l2[0], l2[1]);
+        *(uint2 *)hi = make_uint2(h2[0], h2[1]);
+    };
+    if (tid < n4) {
+        rope4(qa, qb, a.q_scale, true, q16 + i4, q16 + i4 + half);
+        rope4(ka, kb, 1.0f, false, k16 + i4, k16 + i4 + half);
     }
-    for (int i = tid; i < hd; i += blockDim.x) v16[i] = f2h(vh[i]);
     __syncthreads();
-    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
-    if (h % grp == 0) {  // one writer per kv head: K row `pos`, V column `pos` (src/gemma_model.cpp:506-517)
-        for (int i = ds * ATT_DCHUNK + tid; i < (ds + 1) * ATT_DCHUNK && i < hd; i += blockDim.x) {
-            a.kc[(int64_t)pos * kvw + (int64_t)kvh * hd + i] = k16[i];
-            a.vc[((int64_t)kvh * hd + i) * a.ctx + pos] = v16[i];
-        }
+    AH_STAMP(1);
+    // this token's cache entries (src/gemma_model.cpp:506-517), by the group's first head; readers
+    // in this launch use k16 / the v values instead
+    if (h % G == 0) {
+        for (int i = tid; i < hd; i += AH_THREADS) a.kc[(int64_t)pos * kvw + (int64_t)kvh * hd + i] = k16[i];
+        for (int d = quad; d < hd; d += AH_THREADS / 4)
+            if (t4 == 0) a.vc[((int64_t)kvh * hd + d) * a.ctx + pos] = f2h(d == d0 ? vx0 : vh[d]);
     }
     // ---- KQ (vec_dot_f16 over hd per kv position) + mask (j > pos -> -inf), scale 1.0
-    for (int j0 = 0; j0 < n_kv; j0 += nq) {
+    for (int j0 = 0; j0 < n_kv; j0 += AH_THREADS / 4) {
         const int j = j0 + quad;
         float acc[8];
 #pragma unroll
         for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
-        if (j0 == 0) {
+        if (j == pos) {
+            for (int s = 0; s * 32 < hd; ++s)
+                f16_step8(acc, *(const uint4 *)(k16 + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
+        } else if (j0 == 0) {
 #pragma unroll
-            for (int s = 0; s < ATT_KPF; ++s)
-                if (s * 32 < hd) {
-                    const uint4 kv = (j == pos) ? *(const uint4 *)(k16 + s * 32 + t4 * 8) : kpre[s];
-                    f16_step8(acc, kv, *(const uint4 *)(q16 + s * 32 + t4 * 8));
-                }
-            for (int s = ATT_KPF; s * 32 < hd; ++s) {
-                const uint16_t *krow = (j == pos) ? k16 : a.kc + (int64_t)j * kvw + (int64_t)kvh * hd;
+            for (int s = 0; s < AH_KPF; ++s)
+                if (s * 32 < hd) f16_step8(acc, kpre[s], *(const uint4 *)(q16 + s * 32 + t4 * 8));
+            const uint16_t *krow = a.kc + (int64_t)(j < a.ctx ? j : 0) * kvw + (int64_t)kvh * hd;
+            for (int s = AH_KPF; s * 32 < hd; ++s)
                 f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
-            }
         } else {
-            const int jc = j < pos ? j : pos;
-            const uint16_t *krow = (jc == pos) ? k16 : a.kc + (int64_t)jc * kvw + (int64_t)kvh * hd;
+            const int jc = j < pos ? j : 0;  // j > pos is masked below
+            const uint16_t *krow = a.kc + (int64_t)jc * kvw + (int64_t)kvh * hd;
             for (int s = 0; s * 32 < hd; ++s)
                 f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
         }
-        const float kq = quad_reduce_f16(acc, t4);
+        const float kq = quad_reduce_f16(acc);
         if (t4 == 0 && j < n_kv) {
             const float w = (j > pos) ? -INFINITY : kq * 1.0f + 0.0f;
             S[j] = w;
-            if (a.dbg_w && ds == 0) a.dbg_w[(int64_t)h * a.ctx + j] = w;
+            if (a.dbg_w) a.dbg_w[(int64_t)h * a.ctx + j] = w;
         }
     }
     __syncthreads();
-    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-    // ---- soft_max_ext: max; e = table_exp[f16(w - max)]; exact sum; e * (float)(1/sum)
-    // Every wave reduces the whole row itself (DPP, no LDS round trip) and writes P16 for its own
-    // slice j = 64*wave + lane (+ blockDim.x*m): one barrier for the softmax instead of three.
-    const int lane = tid & 63, wave = tid >> 6;
+    AH_STAMP(2);
+    // ---- soft_max_ext: every wave reduces the whole row (DPP) and writes P16 for its
+    // own slice j = 64*wave + lane + AH_THREADS*m: one barrier for the whole softmax
     float mx = -INFINITY;
     for (int j = lane; j < n_kv; j += 64) mx = fmaxf(mx, S[j]);
     mx = wave_max(mx);
-    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
-    // e values are fp16 in [0,1]: exact multiples of 2^-24, so an integer sum is the exact sum
-    // (ggml's double accumulation of them is exact too).
     unsigned long long isum = 0;
-    float mine[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // e of this wave's own slice (n_kv <= 4 * blockDim.x)
+    float mine[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int j = lane, k = 0; j < n_kv; j += 64, ++k) {
         const float w = S[j];
         float e = 0.0f;
         if (w != -INFINITY) e = h2f(a.exp_tab[f2h(w - mx)]);
+        // e is fp16 in [0,1]: an exact multiple of 2^-24, so the integer sum is the exact sum
         isum += (unsigned long long)(e * 16777216.0f);
-        const int r = k - wave;  // slot of j = 64*wave + lane + blockDim.x*m
-        if (r >= 0 && (r & ((int)(blockDim.x >> 6) - 1)) == 0) {
-            const int m = r / (int)(blockDim.x >> 6);
-            if (m == 0) mine[0] = e; else if (m == 1) mine[1] = e; else if (m == 2) mine[2] = e; else mine[3] = e;
+        const int r = k - wave;
+        if (r >= 0 && r % nwave == 0) {
+            const int m = r / nwave;
+            if (m == 0) mine[0] = e; else if (m == 1) mine[1] = e; else if (m == 2) mine[2] = e; else if (m == 3) mine[3] = e;
         }
     }
     const unsigned long long tot = wave_sum_u64(isum);
-    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 4] = __builtin_amdgcn_s_memrealtime();
     const double sum = (double)tot * (1.0 / 16777216.0);
     const float inv = (float)(1.0 / sum);
-    if (a.dbg_inv && tid == 0 && ds == 0) a.dbg_inv[h] = inv;
-    for (int j = tid, m = 0; j < n_kv; j += blockDim.x, ++m) {
+    if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
+    for (int j = tid, m = 0; j < n_kv; j += AH_THREADS, ++m) {
         float e;
         if (m < 4) {
             e = m == 0 ? mine[0] : m == 1 ? mine[1] : m == 2 ? mine[2] : mine[3];
@@ -390,45 +729,50 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
             e = w != -INFINITY ? h2f(a.exp_tab[f2h(w - mx)]) : 0.0f;
         }
         P16[j] = f2h(e * inv);
-        if (a.dbg_p && ds == 0) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
+        if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
     }
     __syncthreads();
-    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+    AH_STAMP(3);
     // ---- KQV: out[d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16); lane t4 runs accumulator j = t4
-    for (int d = d0; d < (ds + 1) * ATT_DCHUNK && d < hd; d += nq) {
+    for (int d = quad; d < hd; d += AH_THREADS / 4) {
         float acc[8];
 #pragma unroll
         for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
         const uint16_t *vr = a.vc + ((int64_t)kvh * hd + d) * a.ctx;
+        const float vx = d == d0 ? vx0 : vh[d];
         for (int st = 0, s = 0; st < n_kv; st += 32, ++s) {
             const int e0 = st + t4 * 8;
             uint4 xv;
-            if (d == d0 && s < ATT_VPF) {
-                // statically-indexed pick from the early loads
-                xv = vpre[0];
+            if (d == d0 && s < AH_VPF) {
+                xv = vpre[0];  // statically-indexed pick from the early loads
 #pragma unroll
-                for (int k = 1; k < ATT_VPF; ++k)
+                for (int k = 1; k < AH_VPF; ++k)
                     if (s == k) xv = vpre[k];
             } else {
                 xv = *(const uint4 *)(vr + e0);
             }
-            if (pos >= e0 && pos < e0 + 8) {  // this token's V: only the LDS copy is safe to read
-                __attribute__((aligned(16))) uint16_t tmp[8];
-                *(uint4 *)tmp = xv;
-                tmp[pos - e0] = v16[d];
-                xv = *(const uint4 *)tmp;
+            if (pos >= e0 && pos < e0 + 8) {  // this token's V: its cache write may not be visible
+                const uint32_t hv = f2h(vx), sh = 16 * ((pos - e0) & 1);
+                const uint32_t msk = ~(0xFFFFu << sh);
+                switch ((pos - e0) >> 1) {
+                    case 0: xv.x = (xv.x & msk) | (hv << sh); break;
+                    case 1: xv.y = (xv.y & msk) | (hv << sh); break;
+                    case 2: xv.z = (xv.z & msk) | (hv << sh); break;
+                    default: xv.w = (xv.w & msk) | (hv << sh); break;
+                }
             }
             f16_step8(acc, xv, *(const uint4 *)(P16 + e0));
         }
-        const float o = quad_reduce_f16(acc, t4);
+        const float o = quad_reduce_f16(acc);
         if (t4 == 0) a.out[(int64_t)h * hd + d] = o;
     }
-    if (a.dbg_t && tid == 0) a.dbg_t[(blockIdx.x * gridDim.y + blockIdx.y) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+    AH_STAMP(4);
 }
 
 __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys, int n_parts, int *token, int *pos,
-                                                 int *hist, int hist_cap, const int *n_fixed) {
+                                                 int *hist, int hist_cap, const int *n_fixed, rope_row r) {
     __shared__ unsigned long long red[4];
+    __shared__ int sp;
     unsigned long long best = 0;
     for (int i = threadIdx.x; i < n_parts; i += blockDim.x) best = keys[i] > best ? keys[i] : best;
 #pragma unroll
@@ -438,14 +782,25 @@ __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys,
     }
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
-    // strict '>' argmax, first max wins (src/gemma_model.cpp:538-543): the key's low word is ~index
-    const int idx = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
-    const int p = *pos + 1;
-    *token = idx;
-    if (hist && p < hist_cap && p >= *n_fixed) hist[p] = idx;  // never overwrite the prompt
-    *pos = p;
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
+        // strict '>' argmax, first max wins (src/gemma_model.cpp:538-543): the key's low word is ~index
+        const int idx = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+        const int p = *pos + 1;
+        *token = idx;
+        if (hist && p < hist_cap && p >= *n_fixed) hist[p] = idx;  // never overwrite the prompt
+        *pos = p;
+        sp = p;
+    }
+    __syncthreads();
+    // the RoPE row of the next position, at a fixed address (attention loads it without *pos)
+    if (r.cur && sp < r.ctx) {
+        for (int i = threadIdx.x; i < r.half; i += blockDim.x) {
+            r.cur[i] = r.cos[(int64_t)sp * r.half + i];
+            r.cur[r.half + i] = r.sin[(int64_t)sp * r.half + i];
+        }
+        if (threadIdx.x == 0) ((int *)r.cur)[2 * r.half] = sp;
+    }
 }
 
 // C-ABI F16 mul_mat (KQ/KQV shapes): one thread per (row, col), vec_dot_f16 order
@@ -519,27 +874,66 @@ int launch_embed(const uint8_t *qs, const uint8_t *sc, int wtype, int64_t n_bt, 
     return 0;
 }
 
+attn_geom attn_geometry(int H, int Hkv, int hd, int ctx) {
+    attn_geom g{};
+    if (Hkv <= 0 || H % Hkv) return g;
+    const int G = H / Hkv;
+    if (G > ATT_QUADS || ATT_QUADS % G || hd % 8 || (G * hd / 2) % 4 || (hd / 2) / 4 > ATT_THREADS) return g;
+    const attn_split sp = attn_split_of(G, hd);
+    const int PS = sp.ps, DS = sp.ds;
+    if (PS < 1 || DS < 1) return g;
+    const int nb = (hd + DS - 1) / DS;
+    if (nb * Hkv > ATT_MAXWG) return g;
+    const int na = (ctx + PS - 1) / PS;
+    g.nwg = std::max(nb, std::min(na, std::min(32, ATT_MAXWG / Hkv)));
+    g.grid = g.nwg * Hkv;
+    g.lds = (size_t)G * hd * 2 + (size_t)hd * 2 + (size_t)PS * hd * 2 + (size_t)DS * ATT_VW * 2 + (size_t)G * ctx * 2;
+    g.sbuf_floats = (size_t)Hkv * ctx * G;
+    g.sync_ints = (size_t)Hkv * 2;
+    return g;
+}
+
 int launch_attn_decode(const attn_args &a, hipStream_t s) {
-    if (a.hd % 32 != 0 || a.hd > 512 || a.ctx % 32 != 0 || a.H % a.Hkv != 0) {
-        set_error("attn_decode: unsupported shape");
+    if (a.mode == ATTN_PER_HEAD) {
+        if (a.hd % 32 != 0 || a.hd > 256 || a.ctx % 32 != 0 || a.H % a.Hkv != 0 || !a.rope_cur) {
+            set_error("attn_decode: unsupported shape for the per-head form");
+            return -1;
+        }
+        const size_t lds = ((2 * (size_t)a.hd * 2 + 15) & ~(size_t)15) + (size_t)a.ctx * 4 + (size_t)a.ctx * 2 + 16;
+        if (lds > 160 * 1024) {
+            set_error("attn_decode: context too long for the LDS image");
+            return -1;
+        }
+        if (lds > 64 * 1024)
+            GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_head, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(k_attn_head, dim3(8 * a.H), dim3(AH_THREADS), lds, s, a);
+        GHIP_CHECK(hipGetLastError());
+        return 0;
+    }
+    const attn_geom g = attn_geometry(a.H, a.Hkv, a.hd, a.ctx);
+    if (a.hd % 32 != 0 || a.hd > 512 || a.ctx % 32 != 0 || g.nwg == 0 || a.nwg != g.nwg || !a.sbuf || !a.sync) {
+        set_error("attn_decode: unsupported shape or missing scratch");
         return -1;
     }
-    const size_t lds = ((3 * (size_t)a.hd * 2 + 15) & ~(size_t)15) + (size_t)a.ctx * 4 + (size_t)a.ctx * 2 + 16 + 64 +
-                       64 + 8 + 128;  // red: 16 floats, align, 16 u64
-    if (lds > 160 * 1024) {
+    // every workgroup of a kv group must be resident at once (in-kernel hand-off)
+    if (g.grid > ATT_MAXWG) {
+        set_error("attn_decode: too many workgroups for the in-kernel hand-off");
+        return -1;
+    }
+    if (g.lds > 160 * 1024) {
         set_error("attn_decode: context too long for the LDS image");
         return -1;
     }
-    if (lds > 64 * 1024)
-        GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_attn_decode, dim3(a.H, (a.hd + ATT_DCHUNK - 1) / ATT_DCHUNK), dim3(ATT_THREADS), lds, s, a);
+    if (g.lds > 64 * 1024)
+        GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
+    hipLaunchKernelGGL(k_attn_decode, dim3(g.grid), dim3(ATT_THREADS), g.lds, s, a);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }
 
 int launch_advance(const unsigned long long *keys, int n_parts, int *token, int *pos, int *hist, int hist_cap,
-                   const int *n_fixed, hipStream_t s) {
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(256), 0, s, keys, n_parts, token, pos, hist, hist_cap, n_fixed);
+                   const int *n_fixed, const rope_row &r, hipStream_t s) {
+    hipLaunchKernelGGL(k_advance, dim3(1), dim3(256), 0, s, keys, n_parts, token, pos, hist, hist_cap, n_fixed, r);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -81,10 +81,11 @@ int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
  * kernels (regions 0..4: qkv, attention, attn-out, gate/up, down) and the logits kernel (region 5);
  * out = 6 * 4096 * 16 u64, slot [region][workgroup][phase], unused slots 0 */
 int gemma_engine_stamp_step(gemma_engine *e, int layer, unsigned long long *out);
-/* per-op test entry: one decode-attention block on host buffers (caches updated in place) */
+/* per-op test entry: one decode-attention block on host buffers (caches updated in place);
+ * mode 0 = one workgroup per head, 1 = position-split form with the in-kernel hand-off */
 int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos, int H, int Hkv, int hd, int ctx,
                            float rope_base, float *out, float *dbg_w, uint16_t *dbg_p, float *dbg_inv,
-                           unsigned long long *dbg_t);
+                           unsigned long long *dbg_t, int mode);
 
 #ifdef __cplusplus
 }

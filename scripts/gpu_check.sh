@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 for w in $WHAT; do
   case $w in
     tests) timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; } ; tail -2 $OUT/pytest_gpu.log ;;
-    stamp) timeout -k 10 120 python tests/stamp_attn.py > $OUT/stamp.log 2>&1 || { cat $OUT/stamp.log; exit 1; } ; cat $OUT/stamp.log ;;
+    stamp) timeout -k 10 120 python tests/stamp_attn.py 0 > $OUT/stamp.log 2>&1 && timeout -k 10 120 python tests/stamp_attn.py 1 >> $OUT/stamp.log 2>&1 || { cat $OUT/stamp.log; exit 1; } ; cat $OUT/stamp.log ;;
     steps) timeout -k 10 180 python tests/stamp_step.py 9 > $OUT/stamp_step.log 2>&1 && timeout -k 10 180 python tests/stamp_step.py 17 >> $OUT/stamp_step.log 2>&1 || { cat $OUT/stamp_step.log; exit 1; } ; cat $OUT/stamp_step.log ;;
     bench) timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --no-cpu --steps 32 > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; } ;

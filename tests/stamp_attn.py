@@ -9,7 +9,8 @@ import gemma_hip as G
 
 L = G.lib()
 L.gemma_test_attn_decode.restype = C.c_int
-L.gemma_test_attn_decode.argtypes = [C.c_void_p] * 3 + [C.c_int] * 5 + [C.c_float] + [C.c_void_p] * 5
+L.gemma_test_attn_decode.argtypes = [C.c_void_p] * 3 + [C.c_int] * 5 + [C.c_float] + [C.c_void_p] * 5 + [C.c_int]
+mode = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 H, Hkv, hd, ctx, pos = 8, 1, 256, 512, 200
 rng = np.random.default_rng(0)
 qkv = rng.standard_normal((H + 2 * Hkv) * hd).astype(np.float32)
@@ -18,12 +19,12 @@ vc = rng.standard_normal(ctx * Hkv * hd).astype(np.float16).view(np.uint16)
 out = np.zeros(H * hd, np.float32)
 st = np.zeros(H * 8 * 8, np.uint64)
 r = L.gemma_test_attn_decode(qkv.ctypes.data, kc.ctypes.data, vc.ctypes.data, pos, H, Hkv, hd, ctx, 10000.0,
-                             out.ctypes.data, None, None, None, st.ctypes.data)
+                             out.ctypes.data, None, None, None, st.ctypes.data, mode)
 assert r == 0, G.last_error()
 st = st.reshape(H * 8, 8).astype(np.int64)
 st = st[st[:, 0] != 0]  # launched workgroups only
-rel = (st[:, :7] - st[:, :1]) * 10
-print("phase end times (ns) per WG [start, rope, KQ, max, sum, P16, KQV]:")
+rel = (st[:, :8] - st[:, :1]) * 10
+print("phase end times (ns) per WG [start, p1..p7] (mode %d; AH_STAMP / ATT_STAMP order)" % mode)
 print("median", np.median(rel, axis=0).astype(int).tolist())
 print("max   ", rel.max(axis=0).tolist())
 print("WG start spread (ns)", int((st[:, 0].max() - st[:, 0].min()) * 10))

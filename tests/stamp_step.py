@@ -17,7 +17,7 @@ e = G.Engine(GEMMA_2B, n_ctx=512, device=0)
 e.begin(make_prompt(128, GEMMA_2B["n_vocab"]))
 e.step(140, use_graph=True)
 names = ["qkv", "attention", "attn-out", "gate/up", "down", "logits"]
-phases = {0: ["issue", "prologue", "sync", "stream", "end", "own", "carry0", "fma", "store", "sync2"], 1: ["rope", "KQ", "max", "sum", "P16", "KQV"]}
+phases = {0: ["issue", "prologue", "sync", "stream", "end", "own", "carry0", "fma", "store", "sync2"], 1: ["p1", "p2", "p3", "p4", "p5", "p6", "p7"]}  # attention: see AH_STAMP / ATT_STAMP
 for rep in range(2):
     st = e.stamp_step(layer).astype(np.int64)
 prev_end = None
@@ -31,7 +31,7 @@ for k, nm in enumerate(names):
     n = len(ph) + 1
     rel = (r[:, :n] - t0) * 10
     rel[r[:, :n] == 0] = -1
-    end = r[:, 6 if k == 1 else 5].max()
+    end = r[:, :n].max() if k == 1 else r[:, 5].max()
     gap = (t0 - prev_end) * 10 if prev_end is not None else None
     print(f"{nm:10s} WGs={len(r):5d} start spread {int((r[:, 0].max() - t0) * 10):6d} ns  gap {gap} ns  "
           f"span {int((end - t0) * 10)} ns")

@@ -23,12 +23,13 @@ def _attn_case(rng, pos, H, Hkv, hd, ctx, scale_q=1.0):
 
 
 @gpu
+@pytest.mark.parametrize("mode", [0, 1], ids=["per_head", "split"])
 @pytest.mark.parametrize("H,Hkv", [(8, 1), (2, 1), (4, 2), (16, 16)])
-def test_attn_decode_bitexact(H, Hkv):
+def test_attn_decode_bitexact(H, Hkv, mode):
     import gemma_hip as G
     L = G.lib()
     L.gemma_test_attn_decode.restype = C.c_int
-    L.gemma_test_attn_decode.argtypes = [C.c_void_p] * 3 + [C.c_int] * 5 + [C.c_float] + [C.c_void_p] * 5
+    L.gemma_test_attn_decode.argtypes = [C.c_void_p] * 3 + [C.c_int] * 5 + [C.c_float] + [C.c_void_p] * 5 + [C.c_int]
     OL = O.lib()
     OL.orc_attn_decode.argtypes = [C.c_void_p] * 3 + [C.c_int] * 5 + [C.c_float] + [C.c_void_p] * 4
     hd, ctx = 256, 512
@@ -45,7 +46,7 @@ def test_attn_decode_bitexact(H, Hkv):
             OL.orc_attn_decode(qkv.ctypes.data, k1.ctypes.data, v1.ctypes.data, pos, H, Hkv, hd, ctx, 10000.0,
                                ref.ctypes.data, w1.ctypes.data, p1.ctypes.data, None)
             r = L.gemma_test_attn_decode(qkv.ctypes.data, k2.ctypes.data, v2.ctypes.data, pos, H, Hkv, hd, ctx,
-                                         10000.0, got.ctypes.data, w2.ctypes.data, p2.ctypes.data, None, None)
+                                         10000.0, got.ctypes.data, w2.ctypes.data, p2.ctypes.data, None, None, mode)
             assert r == 0, G.last_error()
             assert np.array_equal(k1, k2) and np.array_equal(v1, v2), f"cache update differs at pos {pos}"
             nd = int((got.view(np.uint32) != ref.view(np.uint32)).sum())
