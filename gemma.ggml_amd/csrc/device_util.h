@@ -88,4 +88,13 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
     return s;
 }
 
+// ggml's exp table entry table_exp_f16[x16] = fp16(expf(fp32(x16))) (ggml_init), computed instead of
+// gathered (the gather is a dependent global round trip in the softmax).  The f16 rounding absorbs
+// the f32 error of the hardware exp: for every non-positive f16 input (the only ones the softmax
+// forms) __expf, expf and exp(double) all give the glibc-expf table entry (tests/micro/exp_variants;
+// the GPU test test_exp_f16_matches_table re-checks this very function on all inputs).
+__device__ __forceinline__ uint32_t exp_f16_of(uint32_t x16) {
+    return f2h(__expf(h2f(x16)));
+}
+
 }  // namespace ghip

@@ -741,3 +741,13 @@ extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *
         if (p) (void)hipFree(p);
     return r;
 }
+
+extern "C" int gemma_test_exp_f16(uint16_t *out) {
+    set_error("");
+    uint16_t *d = nullptr;
+    GHIP_CHECK(hipMalloc(&d, 65536 * 2));
+    int r = launch_exp_f16_all(d, nullptr);
+    if (r == 0) GHIP_CHECK(hipMemcpy(out, d, 65536 * 2, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return r;
+}

@@ -527,7 +527,7 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
             const float w = k < 4 ? (k == 0 ? sv[0] : k == 1 ? sv[1] : k == 2 ? sv[2] : sv[3])
                                   : ld_sc1(sk_out + (int64_t)j * G + h);
             uint16_t e16 = 0;
-            if (w != -INFINITY) e16 = a.exp_tab[f2h(w - mx)];
+            if (w != -INFINITY) e16 = (uint16_t)exp_f16_of(f2h(w - mx));
             prow[j] = e16;
             isum += (unsigned long long)(h2f(e16) * 16777216.0f);
         }
@@ -707,7 +707,7 @@ __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
     for (int j = lane, k = 0; j < n_kv; j += 64, ++k) {
         const float w = S[j];
         float e = 0.0f;
-        if (w != -INFINITY) e = h2f(a.exp_tab[f2h(w - mx)]);
+        if (w != -INFINITY) e = h2f(exp_f16_of(f2h(w - mx)));
         // e is fp16 in [0,1]: an exact multiple of 2^-24, so the integer sum is the exact sum
         isum += (unsigned long long)(e * 16777216.0f);
         const int r = k - wave;
@@ -726,7 +726,7 @@ __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
             e = m == 0 ? mine[0] : m == 1 ? mine[1] : m == 2 ? mine[2] : mine[3];
         } else {  // long rows: recompute (same table lookup, same value)
             const float w = S[j];
-            e = w != -INFINITY ? h2f(a.exp_tab[f2h(w - mx)]) : 0.0f;
+            e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
         }
         P16[j] = f2h(e * inv);
         if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
@@ -767,6 +767,11 @@ __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
         if (t4 == 0) a.out[(int64_t)h * hd + d] = o;
     }
     AH_STAMP(4);
+}
+
+__global__ void k_exp_f16_all(uint16_t *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 65536) out[i] = (uint16_t)exp_f16_of((uint32_t)i);
 }
 
 __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys, int n_parts, int *token, int *pos,
@@ -927,6 +932,12 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
     if (g.lds > 64 * 1024)
         GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
     hipLaunchKernelGGL(k_attn_decode, dim3(g.grid), dim3(ATT_THREADS), g.lds, s, a);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_exp_f16_all(uint16_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_exp_f16_all, dim3(256), dim3(256), 0, s, out);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

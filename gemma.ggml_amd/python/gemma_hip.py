@@ -10,7 +10,8 @@ import subprocess
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libgemma_hip.so")
+# GHIP_LIB: an alternative build of the same library (A/B timing of two builds on one box)
+LIB_PATH = os.environ.get("GHIP_LIB") or os.path.join(PKG_DIR, "lib", "libgemma_hip.so")
 
 GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
 

@@ -63,3 +63,24 @@ def test_attn_decode_bitexact(H, Hkv, mode):
                                       float(w1[h].max()), float(w2[h].max()))
                 fails.append((pos, scale_q, nd, float(np.abs(got - ref).max()), info))
     assert not fails, fails[:10]
+
+
+@gpu
+def test_exp_f16_matches_table():
+    """The attention softmax computes ggml's table_exp_f16 entry (fp16(expf(x)), ggml_init) as
+    fp16(f32(exp(double x))); it must equal the glibc-expf table for every input it can see
+    (x = f16(w - max) <= 0) — checked here for all non-positive codes, on the device."""
+    import gemma_hip as G
+    L = G.lib()
+    L.gemma_test_exp_f16.restype = C.c_int
+    L.gemma_test_exp_f16.argtypes = [C.c_void_p]
+    got = np.zeros(65536, np.uint16)
+    assert L.gemma_test_exp_f16(got.ctypes.data) == 0, G.last_error()
+    libm = C.CDLL("libm.so.6")
+    libm.expf.restype = C.c_float
+    libm.expf.argtypes = [C.c_float]
+    x = np.arange(65536, dtype=np.uint16).view(np.float16).astype(np.float32)
+    sel = np.flatnonzero((x <= 0) & np.isfinite(x))
+    ref = np.array([libm.expf(float(x[i])) for i in sel], np.float32).astype(np.float16).view(np.uint16)
+    bad = sel[got[sel] != ref]
+    assert len(bad) == 0, [(int(i), int(got[i])) for i in bad[:8]]
