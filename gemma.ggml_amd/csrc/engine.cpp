@@ -527,14 +527,17 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
     (void)hipSetDevice(e->device);
     const gemma_hip_config &c = e->cfg;
     const int wt = c.wtype;
-    layer_dev &L = e->layers[0];
     const double act_q8 = 34.0 / 32.0;  // bytes per activation element after quantization
+    // launches rotate over the layers' matrices, as in a decode step: each launch reads its weights
+    // cold (18 x the FFN matrices exceed the 256 MB Infinity Cache)
+    int layer = 0;
     mv_args a;
     int ks = 1, pro = PRO_F32, epi = EPI_STORE, grid = 1;
     double bytes = 0;
     auto set_mat = [&](const tiled_mat &m) {
         a.qs = m.qs; a.sc = m.sc; a.rows = m.rows; a.n_rt = m.n_rt; a.n_bt = m.n_bt; a.nb = m.nb;
     };
+    auto setup = [&](layer_dev &L) {
     switch (which) {
         case 0:
             set_mat(L.gate);
@@ -569,12 +572,15 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
             grid = (int)std::min<int64_t>((e->embd.n_rt + 3) / 4, e->grid_big);
             bytes = (double)e->embd.algo_bytes() + c.n_embd * 8.0 + c.n_vocab * 4.0;
             break;
-        case 5:
-            break;
         default:
-            set_error("gemma_engine_time: bad kernel id");
-            return -1.0;
+            break;
     }
+    };
+    if (which < 0 || which > 5) {
+        set_error("gemma_engine_time: bad kernel id");
+        return -1.0;
+    }
+    setup(e->layers[0]);
     (void)act_q8;
     if (const char *v = getenv("GHIP_ABLATE")) a.ablate = atoi(v);
     hipEvent_t t0, t1;
@@ -585,6 +591,10 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
             if (ensure_graph(e)) return -1;
             GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
             return 0;
+        }
+        if (which < 4) {
+            setup(e->layers[layer]);
+            layer = (layer + 1) % c.n_layer;
         }
         return launch_matvec(wt, ks, pro, epi, a, grid, e->stream);
     };
@@ -750,4 +760,39 @@ extern "C" int gemma_test_exp_f16(uint16_t *out) {
     if (r == 0) GHIP_CHECK(hipMemcpy(out, d, 65536 * 2, hipMemcpyDeviceToHost));
     (void)hipFree(d);
     return r;
+}
+
+// Measured HBM read roofline: a streaming read of `bytes` (>= 4 GB defeats the
+// Infinity Cache), `iters` passes timed with hipEvents; returns GB/s (negative on error).
+extern "C" double gemma_hbm_read_gbs(int device, size_t bytes, int iters) {
+    set_error("");
+    if (hipSetDevice(device) != hipSuccess) return -1.0;
+    void *buf = nullptr;
+    unsigned *sink = nullptr;
+    if (hipMalloc(&buf, bytes) != hipSuccess || hipMalloc(&sink, 4) != hipSuccess) {
+        set_error("gemma_hbm_read_gbs: allocation failed");
+        return -1.0;
+    }
+    (void)hipMemset(buf, 1, bytes);
+    hipStream_t s;
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    hipEvent_t t0, t1;
+    (void)hipEventCreate(&t0);
+    (void)hipEventCreate(&t1);
+    double gbs = -1.0;
+    if (launch_stream_read(buf, bytes, sink, s) == 0) {
+        (void)hipEventRecord(t0, s);
+        for (int i = 0; i < iters; ++i) (void)launch_stream_read(buf, bytes, sink, s);
+        (void)hipEventRecord(t1, s);
+        (void)hipEventSynchronize(t1);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, t0, t1);
+        gbs = (double)bytes * iters / (ms * 1e-3) / 1e9;
+    }
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    (void)hipStreamDestroy(s);
+    (void)hipFree(buf);
+    (void)hipFree(sink);
+    return gbs;
 }

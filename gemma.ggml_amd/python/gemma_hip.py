@@ -19,7 +19,7 @@ GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
 EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
            "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
            "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
-           "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync"]
+           "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_hbm_read_gbs"]
 
 
 def build():
@@ -86,6 +86,8 @@ def lib():
     L.gemma_engine_tensor.argtypes = [vp, C.c_int, vp, i64]
     L.gemma_engine_time.restype = C.c_double
     L.gemma_engine_time.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    L.gemma_hbm_read_gbs.restype = C.c_double
+    L.gemma_hbm_read_gbs.argtypes = [C.c_int, C.c_size_t, C.c_int]
     L.gemma_engine_sync.restype = C.c_int
     L.gemma_engine_sync.argtypes = [vp]
     _lib = L

@@ -87,6 +87,8 @@ int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos
                            float rope_base, float *out, float *dbg_w, uint16_t *dbg_p, float *dbg_inv,
                            unsigned long long *dbg_t, int mode);
 
+/* measured HBM read roofline: streaming read of `bytes` on `device`, `iters` passes; GB/s */
+double gemma_hbm_read_gbs(int device, size_t bytes, int iters);
 /* per-op test entry: the softmax's exp(f16) for all 65536 codes (compared with ggml's table) */
 int gemma_test_exp_f16(uint16_t *out);
 
