@@ -173,3 +173,23 @@ def test_prefill_equals_tokenwise_decode():
     for i in range(2, len(p) + 1):
         _, last, _ = m.inference(p[:i], 1)
     assert np.array_equal(last, last_prefill)
+
+
+def test_graph_wiring_matches_transformers_gemma_golden():
+    """Oracle forward (ggml semantics, Q8_0 weights and activations) vs the float forward of a
+    locally built transformers GemmaForCausalLM on the same (dequantized) weights — fixture made by
+    tests/golden/make_hf_wiring_golden.py.  Pins the graph wiring of src/gemma_model.cpp:665-747
+    (embedding scale, '+1' RMSNorm weights, RoPE-NEOX pairs, MQA, q scale, GeGLU, residuals, tied
+    output); the tolerance covers Q8_0 activation quantization only (measured: corr >= 0.9998,
+    max |diff| 0.066 at logit std 0.99)."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "hf_wiring_tiny.npz"))
+    keys = ("n_layer", "n_embd", "n_head", "n_head_kv", "head_dim", "n_ff", "n_vocab")
+    shape = dict(zip(keys, (int(v) for v in g["shape"])))
+    m = O.Model(O.make_config(shape, n_ctx=64, wtype=O.Q8_0, seed=int(g["seed"][0])))
+    _, _, ours = m.inference(g["prompt"], 0, want_all=True)
+    ref = g["logits"]
+    corr = min(np.corrcoef(ours[i], ref[i])[0, 1] for i in range(len(ref)))
+    assert corr > 0.999, corr
+    assert np.abs(ours - ref).max() < 0.15 * ref.std()
+    assert (ours.argmax(1) == ref.argmax(1)).mean() >= 0.9
