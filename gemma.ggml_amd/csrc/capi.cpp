@@ -226,3 +226,50 @@ extern "C" void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, 
     for (int64_t c = 0; c < col_num; ++c)
         memcpy(d + (c % ne1) * nb1 + (c / ne1) * nb2, res + c * ne01, (size_t)ne01 * 4);
 }
+
+// ---- per-op test entry for the prefill GEMM (tests/test_gpu_prefill.py) -------------------------
+// W: ggml row-major blocks [rows][K/32] of `type`; X: [T][K] f32.  Quantizes X like ggml's INIT
+// (Q8_0, AVX2 semantics) and runs the int8 MFMA GEMM: Y[T][rows].  xq/da (optional) return the
+// activation image for a bit-exact check of the quantizer.
+extern "C" int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X, float *Y,
+                               int8_t *xq_out, float *da_out) {
+    set_error("");
+    if ((type != T_Q4_0 && type != T_Q8_0) || K % 32 || rows <= 0 || T <= 0) {
+        set_error("gemma_test_gemm: bad arguments");
+        return -1;
+    }
+    const int bb = type == T_Q4_0 ? 18 : 34;
+    const int64_t row_bytes = K / 32 * bb, ldq = (K + 255) / 256 * 256, ldd = ldq / 32;
+    uint8_t *d_rows = nullptr;
+    float *d_x = nullptr, *d_y = nullptr, *d_da = nullptr;
+    int8_t *d_q = nullptr;
+    GHIP_CHECK(hipMalloc(&d_rows, (size_t)(row_bytes * rows)));
+    GHIP_CHECK(hipMalloc(&d_x, (size_t)(T * K * 4)));
+    GHIP_CHECK(hipMalloc(&d_y, (size_t)(T * rows * 4)));
+    GHIP_CHECK(hipMalloc(&d_q, (size_t)(T * ldq)));
+    GHIP_CHECK(hipMalloc(&d_da, (size_t)(T * ldd * 4)));
+    GHIP_CHECK(hipMemcpy(d_rows, W, (size_t)(row_bytes * rows), hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(d_x, X, (size_t)(T * K * 4), hipMemcpyHostToDevice));
+    tiled_mat m = alloc_tiled(type, rows, K, nullptr);
+    int r = launch_repack(m, d_rows, row_bytes, nullptr);
+    qrow_args qa;
+    qa.x = d_x; qa.ldx = K; qa.K = K; qa.q = d_q; qa.ldq = ldq; qa.da = d_da; qa.ldd = ldd;
+    if (r == 0) r = launch_quant_rows(QR_F32, qa, (int)T, nullptr);
+    gemm_args g;
+    g.qs = m.qs; g.sc = m.sc; g.rows = rows; g.n_rt = m.n_rt; g.n_bt = m.n_bt; g.nb = m.nb;
+    g.xq = d_q; g.ldq = ldq; g.da = d_da; g.ldd = ldd; g.T = T; g.y = d_y; g.ldy = rows;
+    if (r == 0) r = launch_gemm_q(type, EPI_STORE, g, nullptr);
+    if (r == 0) GHIP_CHECK(hipDeviceSynchronize());
+    if (r == 0) {
+        GHIP_CHECK(hipMemcpy(Y, d_y, (size_t)(T * rows * 4), hipMemcpyDeviceToHost));
+        if (xq_out)
+            GHIP_CHECK(hipMemcpy2D(xq_out, (size_t)K, d_q, (size_t)ldq, (size_t)K, (size_t)T, hipMemcpyDeviceToHost));
+        if (da_out)
+            GHIP_CHECK(hipMemcpy2D(da_out, (size_t)(K / 32 * 4), d_da, (size_t)(ldd * 4), (size_t)(K / 32 * 4), (size_t)T,
+                                   hipMemcpyDeviceToHost));
+    }
+    free_tiled(m);
+    void *bufs[] = {d_rows, d_x, d_y, d_q, d_da};
+    for (void *p : bufs) (void)hipFree(p);
+    return r;
+}

@@ -171,8 +171,16 @@ struct gemma_engine {
     int ks_small = 4, ks_down = 8;
     int grid_big = 2048;
     // prefill scratch (lazily allocated)
-    void *pf_scratch = nullptr;
-    size_t pf_bytes = 0;
+    // prefill buffers (lazily sized for the prompt length)
+    struct {
+        int T = 0;
+        int64_t ldq = 0, ldd = 0;
+        float *X = nullptr, *SA = nullptr, *QKV = nullptr, *ATT = nullptr, *G = nullptr, *U = nullptr, *LG = nullptr;
+        float *DA = nullptr;
+        uint16_t *Q16 = nullptr;
+        int8_t *XQ = nullptr;
+        void *keys = nullptr;
+    } pf;
     float *dbg = nullptr;  // per-layer taps [L][qkv_rows + qw + E] (debug steps only)
     unsigned long long *stamp = nullptr;  // phase stamps of one layer's kernels (diagnostic steps only)
     int stamp_layer = -1;
@@ -387,7 +395,8 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
         (void)hipFree(L.attn_norm); (void)hipFree(L.ffn_norm);
     }
     void *bufs[] = {e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
-                    e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf_scratch};
+                    e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf.X, e->pf.SA, e->pf.QKV, e->pf.ATT, e->pf.G, e->pf.U,
+                    e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.keys};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     (void)hipStreamDestroy(e->stream);
@@ -621,10 +630,115 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
     return (double)ms * 1000.0 / iters;
 }
 
+static int prefill_alloc(gemma_engine *e, int T) {
+    auto &p = e->pf;
+    if (p.T >= T) return 0;
+    void *bufs[] = {p.X, p.SA, p.QKV, p.ATT, p.G, p.U, p.LG, p.DA, p.Q16, p.XQ, p.keys};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    const gemma_hip_config &c = e->cfg;
+    const int64_t E = c.n_embd, F = c.n_ff;
+    p.ldq = (std::max(std::max(E, F), (int64_t)e->qw) + 255) / 256 * 256;
+    p.ldd = p.ldq / 32;
+    GHIP_CHECK(hipMalloc(&p.X, (size_t)T * E * 4));
+    GHIP_CHECK(hipMalloc(&p.SA, (size_t)T * E * 4));
+    GHIP_CHECK(hipMalloc(&p.QKV, (size_t)T * e->qkv_rows * 4));
+    GHIP_CHECK(hipMalloc(&p.ATT, (size_t)T * e->qw * 4));
+    GHIP_CHECK(hipMalloc(&p.G, (size_t)T * F * 4));
+    GHIP_CHECK(hipMalloc(&p.U, (size_t)T * F * 4));
+    GHIP_CHECK(hipMalloc(&p.LG, (size_t)T * c.n_vocab * 4));  // all rows, as the reference computes them
+    GHIP_CHECK(hipMalloc(&p.DA, (size_t)T * p.ldd * 4));
+    GHIP_CHECK(hipMalloc(&p.Q16, (size_t)T * e->qw * 2));
+    GHIP_CHECK(hipMalloc(&p.XQ, (size_t)T * p.ldq));
+    GHIP_CHECK(hipMalloc(&p.keys, 256 * 8));
+    p.T = T;
+    return 0;
+}
+
+static int enqueue_prefill(gemma_engine *e, int T, float *taps = nullptr) {
+    const gemma_hip_config &c = e->cfg;
+    hipStream_t s = e->stream;
+    auto &p = e->pf;
+    const int wt = c.wtype;
+    const int64_t E = c.n_embd, F = c.n_ff;
+    auto gemm = [&](const tiled_mat &m, int epi, const float *resid, float *y, int64_t ldy) {
+        gemm_args g;
+        g.qs = m.qs; g.sc = m.sc; g.rows = m.rows; g.n_rt = m.n_rt; g.n_bt = m.n_bt; g.nb = m.nb;
+        g.xq = p.XQ; g.ldq = p.ldq; g.da = p.DA; g.ldd = p.ldd; g.T = T; g.y = y; g.resid = resid; g.ldy = ldy;
+        return launch_gemm_q(wt, epi, g, s);
+    };
+    auto quant = [&](int mode, const float *x, const float *x2, int64_t K, const float *norm_w) {
+        qrow_args a;
+        a.x = x; a.x2 = x2; a.ldx = K; a.K = K; a.norm_w = norm_w; a.eps = c.eps;
+        a.q = p.XQ; a.ldq = p.ldq; a.da = p.DA; a.ldd = p.ldd;
+        a.gelu_tab = e->gelu_tab; a.gelu_clamp = c.gelu_clamp;
+        if (mode == QR_EMBED_NORM) {
+            a.tokens = e->hist; a.emb_qs = e->embd.qs; a.emb_sc = e->embd.sc; a.emb_type = wt;
+            a.emb_n_bt = e->embd.n_bt; a.emb_scale = sqrtf((float)E); a.emb_out = p.X; a.ldx = E;
+        }
+        return launch_quant_rows(mode, a, T, s);
+    };
+    int n_kv = 32 * (T / 32 + 1);  // src/gemma_model.cpp:429 with n_total = T
+    if (n_kv > c.n_ctx) n_kv = c.n_ctx;
+    for (int il = 0; il < c.n_layer; ++il) {
+        layer_dev &L = e->layers[il];
+        if (quant(il == 0 ? QR_EMBED_NORM : QR_NORM, p.X, nullptr, E, L.attn_norm)) return -1;
+        if (gemm(L.qkv, EPI_STORE, nullptr, p.QKV, e->qkv_rows)) return -1;
+        ropekv_args r;
+        r.qkv = p.QKV; r.ldqkv = e->qkv_rows; r.rope_cos = e->rope_cos; r.rope_sin = e->rope_sin; r.q16 = p.Q16;
+        r.kc = e->kc + (size_t)il * c.n_ctx * e->kvw; r.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
+        r.H = c.n_head; r.Hkv = c.n_head_kv; r.hd = c.head_dim; r.ctx = c.n_ctx; r.p0 = 0;
+        r.q_scale = 1.0f / sqrtf((float)c.head_dim);
+        if (launch_rope_kv_prefill(r, T, s)) return -1;
+        attnp_args at;
+        at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
+        at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
+        if (launch_attn_prefill(at, s)) return -1;
+        if (quant(QR_F32, p.ATT, nullptr, e->qw, nullptr)) return -1;
+        if (gemm(L.o, EPI_ADD, p.X, p.SA, E)) return -1;
+        if (quant(QR_NORM, p.SA, nullptr, E, L.ffn_norm)) return -1;
+        if (gemm(L.gate, EPI_STORE, nullptr, p.G, F)) return -1;
+        if (gemm(L.up, EPI_STORE, nullptr, p.U, F)) return -1;
+        if (quant(QR_GELU, p.G, p.U, F, nullptr)) return -1;
+        if (gemm(L.down, EPI_ADD, p.SA, p.X, E)) return -1;
+        if (taps) GHIP_CHECK(hipMemcpyAsync(taps + (size_t)il * T * E, p.X, (size_t)T * E * 4, hipMemcpyDeviceToDevice, s));
+    }
+    if (quant(QR_NORM, p.X, nullptr, E, e->out_norm)) return -1;
+    if (gemm(e->embd, EPI_STORE, nullptr, p.LG, c.n_vocab)) return -1;
+    // greedy token from the last row; position T-1 -> T, token appended at hist[T]
+    if (launch_row_argmax(p.LG + (size_t)(T - 1) * c.n_vocab, c.n_vocab, (unsigned long long *)p.keys, 256, s)) return -1;
+    const int last = T - 1;
+    GHIP_CHECK(hipMemcpyAsync(e->pos, &last, 4, hipMemcpyHostToDevice, s));
+    rope_row rr;
+    rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+    return launch_advance((const unsigned long long *)p.keys, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
+}
+
+// MFMA prefill of the prompt given to gemma_engine_begin: all prompt
+// positions in one pass (int8 MFMA GEMMs, f16 MFMA causal attention), KV cache filled, logits for
+// every row as the reference computes them (src/gemma_model.cpp:740); returns the greedy token
+// and leaves the engine at position T, ready for gemma_engine_step.  Logits match the CPU path
+// within fp32 reordering; the token-by-token path remains the bit-exact one.
 extern "C" int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *logits_all) {
-    (void)e; (void)logits_last; (void)logits_all;
-    set_error("gemma_engine_prefill: MFMA prefill not built yet");
-    return -1;
+    set_error("");
+    (void)hipSetDevice(e->device);
+    const gemma_hip_config &c = e->cfg;
+    const int T = e->n_prompt;
+    if (T <= 0 || e->host_pos != 0) {
+        set_error("gemma_engine_prefill: call right after gemma_engine_begin");
+        return -1;
+    }
+    if (prefill_alloc(e, T)) return -1;
+    if (enqueue_prefill(e, T)) return -1;
+    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    if (logits_last)
+        GHIP_CHECK(hipMemcpy(logits_last, e->pf.LG + (size_t)(T - 1) * c.n_vocab, (size_t)c.n_vocab * 4,
+                             hipMemcpyDeviceToHost));
+    if (logits_all) GHIP_CHECK(hipMemcpy(logits_all, e->pf.LG, (size_t)T * c.n_vocab * 4, hipMemcpyDeviceToHost));
+    int tok = -1;
+    GHIP_CHECK(hipMemcpy(&tok, e->token, 4, hipMemcpyDeviceToHost));
+    e->host_pos = T;
+    return tok;
 }
 
 // one eager step with per-layer taps copied to host: [L][qkv | attn | x_out]
@@ -795,4 +909,27 @@ extern "C" double gemma_hbm_read_gbs(int device, size_t bytes, int iters) {
     (void)hipFree(buf);
     (void)hipFree(sink);
     return gbs;
+}
+
+// diagnostics: the MFMA prefill with the residual stream after every layer copied to host_taps
+// [n_layer][T][n_embd] (compare with the oracle's per-layer hidden states)
+extern "C" int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    const gemma_hip_config &c = e->cfg;
+    const int T = e->n_prompt;
+    if (T <= 0 || e->host_pos != 0) {
+        set_error("gemma_engine_prefill_taps: call right after gemma_engine_begin");
+        return -1;
+    }
+    if (prefill_alloc(e, T)) return -1;
+    float *d = nullptr;
+    const size_t n = (size_t)c.n_layer * T * c.n_embd;
+    GHIP_CHECK(hipMalloc(&d, n * 4));
+    int r = enqueue_prefill(e, T, d);
+    if (r == 0) GHIP_CHECK(hipStreamSynchronize(e->stream));
+    if (r == 0) GHIP_CHECK(hipMemcpy(host_taps, d, n * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    if (r == 0) e->host_pos = T;
+    return r;
 }

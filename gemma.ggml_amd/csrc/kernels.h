@@ -50,6 +50,61 @@ struct mv_args {
 int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int grid_x, hipStream_t s);
 size_t matvec_lds_bytes(int wtype, int ks, int64_t n_bt, int64_t segment_tiles);
 
+// ---- prefill (prefill.hip) ----------------------------------------------------------------------
+enum qrow_mode { QR_F32 = 0, QR_NORM = 1, QR_EMBED_NORM = 2, QR_GELU = 3 };
+struct qrow_args {  // T rows of K floats -> Q8_0 image q [T][ldq] int8 + da [T][ldd] (f32 of fp16 d)
+    const float *x = nullptr, *x2 = nullptr;  // rows (stride ldx); x2 = `up` for QR_GELU (x = gate)
+    int64_t ldx = 0, K = 0;
+    const float *norm_w = nullptr;
+    float eps = 0.f;
+    const int *tokens = nullptr;              // QR_EMBED_NORM: token ids; embedding table (tiled)
+    const uint8_t *emb_qs = nullptr, *emb_sc = nullptr;
+    int emb_type = 0;
+    int64_t emb_n_bt = 0;
+    float emb_scale = 1.f;
+    float *emb_out = nullptr;                 // scaled embedding rows (the residual stream), stride ldx
+    const uint16_t *gelu_tab = nullptr;
+    int gelu_clamp = 0;
+    int8_t *q = nullptr;
+    int64_t ldq = 0;                          // multiple of 256 (zero padded)
+    float *da = nullptr;
+    int64_t ldd = 0;                          // >= ldq / 32
+};
+int launch_quant_rows(int mode, const qrow_args &a, int T, hipStream_t s);
+struct gemm_args {  // Y[t][r] (stride ldy) = W (tiled) x Xq[t] (+ resid), t < T, r < rows
+    const uint8_t *qs = nullptr, *sc = nullptr;
+    int64_t rows = 0, n_rt = 0, n_bt = 0, nb = 0;
+    const int8_t *xq = nullptr;
+    int64_t ldq = 0;
+    const float *da = nullptr;
+    int64_t ldd = 0;
+    int64_t T = 0;
+    float *y = nullptr;
+    const float *resid = nullptr;
+    int64_t ldy = 0;
+};
+int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s);
+
+struct ropekv_args {  // RoPE q (-> f16, x q_scale) and k, store k/v of positions p0.. in the layer caches
+    const float *qkv = nullptr;  // [T][ldqkv] = q | k | v
+    int64_t ldqkv = 0;
+    const float *rope_cos = nullptr, *rope_sin = nullptr;
+    uint16_t *q16 = nullptr;     // [T][H][hd]
+    uint16_t *kc = nullptr, *vc = nullptr;
+    int H = 0, Hkv = 0, hd = 0, ctx = 0, p0 = 0;
+    float q_scale = 1.f;
+};
+int launch_rope_kv_prefill(const ropekv_args &a, int T, hipStream_t s);
+struct attnp_args {  // causal attention of T prompt tokens against the layer caches
+    const uint16_t *q16 = nullptr;
+    const uint16_t *kc = nullptr, *vc = nullptr;
+    float *out = nullptr;        // [T][ldo], head h at h*hd
+    int64_t ldo = 0;
+    int T = 0, H = 0, Hkv = 0, hd = 0, ctx = 0, n_kv = 0;
+};
+int launch_attn_prefill(const attnp_args &a, hipStream_t s);
+int launch_row_argmax(const float *row, int64_t n, unsigned long long *keys, int parts, hipStream_t s);
+
 // ---- weights (ops.hip) ------------------------------------------------------------------------
 // ggml row-major blocks (host layout) already on device -> tiled layout
 int launch_repack(const tiled_mat &m, const uint8_t *src_rowmajor, int64_t row_bytes, hipStream_t s);

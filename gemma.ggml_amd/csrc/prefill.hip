@@ -1,0 +1,528 @@
+// prefill.hip — the batched-prompt (prefill) path for gfx950: every MUL_MAT of the Gemma graph
+// with col_num = T tokens becomes an int8 MFMA GEMM.
+//
+// Numerics: activations are quantized to Q8_0 exactly as ggml's INIT does
+// (AVX2 quantize_row_q8_0, SURVEY A.2, bit-identical to the decode prologue), and the int32 dot of
+// every 32-element block is exact (v_mfma_i32_16x16x32_i8 = one block).  Only the fp32 accumulation
+// across blocks differs from ggml's AVX2 lane order (one chain acc = fmaf(d_w*d_a, isum, acc) in
+// block order instead of 8 lane chains + fold), so prefill logits match the CPU path to ~1e-6
+// relative (tests: 1e-3), while the per-token decode path stays bit-exact.
+#include <type_traits>
+
+#include "device_util.h"
+#include "kernels.h"
+
+namespace ghip {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// ---- rows -> Q8_0 (int8 image + f32 of the fp16 block scale) --------------------------------
+// One 256-thread workgroup per token row; a quad of threads owns a block (8 elements each).
+template <int MODE>
+__global__ void __launch_bounds__(256) k_quant_rows(qrow_args a) {
+    const int t = blockIdx.x, tid = threadIdx.x, q = tid & 3;
+    const int64_t K = a.K, nb = K / 32;
+    const float *x = a.x + (int64_t)t * a.ldx;
+    const float *x2 = a.x2 ? a.x2 + (int64_t)t * a.ldx : nullptr;
+    int64_t tok = 0;
+    if (MODE == QR_EMBED_NORM) tok = a.tokens[t];
+    auto load = [&](int64_t i0, float v[8]) {
+        if (MODE == QR_EMBED_NORM) {
+            // ggml_get_rows (dequantize_row_*) then ggml_scale by sqrt(E) (src/gemma_model.cpp:677-679)
+            const int64_t rt = tok >> 3, rr = tok & 7;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t i = i0 + j, b = i >> 5;
+                const int e = (int)(i & 31), l = e >> 2, k = e & 3;
+                float w;
+                if (a.emb_type == T_Q4_0) {
+                    const int64_t tile = rt * a.emb_n_bt + (b >> 3), bi = b & 7;
+                    const uint16_t d16 = ((const uint16_t *)(a.emb_sc + (tile * 8 + rr) * 16))[bi];
+                    const uint8_t byte = a.emb_qs[tile * 1024 + (rr * 8 + l) * 16 + (bi >> 1) * 4 + k];
+                    const int qv = (int)((bi & 1) ? (byte >> 4) : (byte & 15)) - 8;
+                    w = (float)qv * pin(h2f(d16));
+                } else {
+                    const int64_t tile = rt * a.emb_n_bt + (b >> 2), bi = b & 3;
+                    const uint16_t d16 = ((const uint16_t *)(a.emb_sc + (tile * 8 + rr) * 8))[bi];
+                    const int qv = (int)(int8_t)a.emb_qs[tile * 1024 + (rr * 8 + l) * 16 + bi * 4 + k];
+                    w = (float)qv * pin(h2f(d16));
+                }
+                v[j] = w * a.emb_scale;
+            }
+        } else {
+            const float4 u = *(const float4 *)(x + i0), w4 = *(const float4 *)(x + i0 + 4);
+            v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w4.x; v[5] = w4.y; v[6] = w4.z; v[7] = w4.w;
+            if (MODE == QR_GELU) {  // gelu(gate) (fp16 table) then ggml_mul by up
+                const float4 g0 = *(const float4 *)(x2 + i0), g1 = *(const float4 *)(x2 + i0 + 4);
+                const float up[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float g;
+                    if (a.gelu_clamp && v[j] <= -10.0f) g = 0.0f;
+                    else if (a.gelu_clamp && v[j] >= 10.0f) g = v[j];
+                    else g = h2f(a.gelu_tab[f2h(v[j])]);
+                    v[j] = g * up[j];
+                }
+            }
+        }
+    };
+    float scale = 1.0f;
+    if (MODE == QR_NORM || MODE == QR_EMBED_NORM) {
+        double part = 0.0;
+        for (int64_t b = tid >> 2; b < nb; b += 64) {
+            float v[8];
+            load(b * 32 + q * 8, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) part += (double)(v[j] * v[j]);
+            if (MODE == QR_EMBED_NORM) {
+                float *eo = a.emb_out + (int64_t)t * a.ldx + b * 32 + q * 8;
+                *(float4 *)eo = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4 *)(eo + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        }
+        __shared__ double red[4];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+        if ((tid & 63) == 0) red[tid >> 6] = part;
+        __syncthreads();
+        const double sum = red[0] + red[1] + red[2] + red[3];
+        const float mean = (float)(sum / (double)K);
+        scale = 1.0f / sqrtf(mean + a.eps);
+    }
+    int8_t *qo = a.q + (int64_t)t * a.ldq;
+    float *dout = a.da + (int64_t)t * a.ldd;
+    for (int64_t b = tid >> 2; b < nb; b += 64) {
+        float v[8];
+        load(b * 32 + q * 8, v);
+        if (MODE == QR_NORM || MODE == QR_EMBED_NORM) {
+            const float4 w0 = *(const float4 *)(a.norm_w + b * 32 + q * 8);
+            const float4 w1 = *(const float4 *)(a.norm_w + b * 32 + q * 8 + 4);
+            const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (v[j] * scale) * wv[j];  // rms_norm, then ggml_mul
+        }
+        // quantize_row_q8_0 (AVX2): amax, d = amax/127 (fp16 RNE), id = 127/amax, rint
+        float amax = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+        amax = fmaxf(amax, dpp_f<0xB1>(amax));
+        amax = fmaxf(amax, dpp_f<0x4E>(amax));
+        const uint32_t d16 = f2h(amax / 127.f);
+        const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+        uint32_t pk[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int qi[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) qi[k] = (int)__builtin_rintf(v[4 * h + k] * id);
+            pk[h] = (uint32_t)(qi[0] & 0xFF) | ((uint32_t)(qi[1] & 0xFF) << 8) | ((uint32_t)(qi[2] & 0xFF) << 16) |
+                    ((uint32_t)(qi[3] & 0xFF) << 24);
+        }
+        *(uint2 *)(qo + b * 32 + q * 8) = make_uint2(pk[0], pk[1]);
+        if (q == 0) dout[b] = h2f(d16);
+    }
+    // zero the K padding of the int8 image (the GEMM stages whole 256-element chunks)
+    for (int64_t i = K + tid * 4; i < a.ldq; i += 256 * 4) *(uint32_t *)(qo + i) = 0;
+    for (int64_t b = nb + tid; b < a.ldd; b += 256) dout[b] = 0.0f;
+}
+
+// ---- int8 MFMA GEMM: Y[t][r] = sum_b (d_w[r][b] * d_a[t][b]) * isum_b(W[r], Xq[t]) ------------
+// Workgroup tile 64 weight rows x 64 tokens, 4 waves of 32 x 32 (2 x 2 MFMA 16x16x32 tiles).  K is
+// staged 8 blocks (256 int8) at a time: weight tiles of the decode layout are unpacked to plain int8
+// rows in LDS (row stride 272 B: conflict-free ds_read_b64 of the MFMA operands), the token rows are
+// copied as they are.  One MFMA = one block's exact int32 dot for 16 x 16 (row, token) pairs.
+constexpr int GM = 64, GN = 64, GKB = 8, GS = 272;
+
+template <int WT, int EPI>
+__global__ void __launch_bounds__(256) k_gemm_q(gemm_args g) {
+    __shared__ __attribute__((aligned(16))) int8_t As[GM * GS];
+    __shared__ __attribute__((aligned(16))) int8_t Bs[GN * GS];
+    __shared__ float dws[GM][GKB + 1];
+    __shared__ float das[GN][GKB + 1];
+    constexpr int BT = wfmt<WT>::BT, SB = wfmt<WT>::SCALE_BYTES;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r0 = blockIdx.x * GM, t0 = blockIdx.y * GN;
+    const int wr = (wave & 1) * 32, wt = (wave >> 1) * 32;
+    const int l16 = lane & 15, kg = lane >> 4;
+    float acc[2][2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[i][j][v] = 0.0f;
+
+    const int64_t n_rt = g.n_rt, n_bt = g.n_bt;
+    for (int64_t kb0 = 0; kb0 < g.nb; kb0 += GKB) {
+        // stage weights: 8 row tiles x (8 / BT) block tiles, 64 lane records of 16 B each
+        constexpr int TPR = GKB / BT;  // block tiles per row tile in one stage
+        for (int rec = tid; rec < 8 * TPR * 64; rec += 256) {
+            const int tile_i = rec >> 6, ln = rec & 63, rr = ln >> 3, l = ln & 7;
+            const int rti = tile_i / TPR, bti = tile_i % TPR;
+            int64_t rt = r0 / 8 + rti, bt = kb0 / BT + bti;
+            const bool ok = rt < n_rt && bt < n_bt;
+            rt = ok ? rt : 0;
+            bt = ok ? bt : 0;
+            const uint4 qv = *(const uint4 *)(g.qs + (rt * n_bt + bt) * 1024 + ln * 16);
+            const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+            int8_t *arow = As + (rti * 8 + rr) * GS + bti * BT * 32 + l * 4;
+            if (WT == T_Q4_0) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    // byte k of dword p: low nibble = block 2p elem 4l+k, high = block 2p+1
+                    const uint32_t lo = qd[p] & 0x0F0F0F0Fu, hi = (qd[p] >> 4) & 0x0F0F0F0Fu;
+                    // nibble n -> int8 n - 8 per byte, no cross-byte borrow: v = n ^ 8 is n - 8 as a
+                    // 4-bit two's complement; sign-extend it (bit 3 set -> high nibble 0xF)
+                    const uint32_t vlo = lo ^ 0x08080808u, vhi = hi ^ 0x08080808u;
+                    const uint32_t slo = vlo | ((vlo & 0x08080808u) * 0x1Eu);
+                    const uint32_t shi = vhi | ((vhi & 0x08080808u) * 0x1Eu);
+                    *(uint32_t *)(arow + (2 * p) * 32) = ok ? slo : 0u;
+                    *(uint32_t *)(arow + (2 * p + 1) * 32) = ok ? shi : 0u;
+                }
+            } else {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) *(uint32_t *)(arow + p * 32) = ok ? qd[p] : 0u;
+            }
+            if (l == 0) {
+                const uint16_t *sp = (const uint16_t *)(g.sc + ((rt * n_bt + bt) * 8 + rr) * SB);
+#pragma unroll
+                for (int b = 0; b < BT; ++b) dws[rti * 8 + rr][bti * BT + b] = ok ? h2f(sp[b]) : 0.0f;
+            }
+        }
+        // stage tokens: 64 rows x 256 int8 + their block scales
+        for (int c = tid; c < GN * 16; c += 256) {
+            const int row = c >> 4, seg = c & 15;
+            const int64_t t = t0 + row < g.T ? t0 + row : 0;
+            const uint4 v = *(const uint4 *)(g.xq + t * g.ldq + kb0 * 32 + seg * 16);
+            *(uint4 *)(Bs + row * GS + seg * 16) = v;
+        }
+        for (int c = tid; c < GN * GKB; c += 256) {
+            const int row = c >> 3, b = c & 7;
+            const int64_t t = t0 + row < g.T ? t0 + row : 0;
+            das[row][b] = (kb0 + b < g.nb) ? g.da[t * g.ldd + kb0 + b] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int b = 0; b < GKB; ++b) {
+            long av[2], bv[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) av[i] = *(const long *)(As + (wr + i * 16 + l16) * GS + b * 32 + kg * 8);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bv[j] = *(const long *)(Bs + (wt + j * 16 + l16) * GS + b * 32 + kg * 8);
+            float dw[2][4], dt[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) dw[i][v] = dws[wr + i * 16 + kg * 4 + v][b];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) dt[j] = das[wt + j * 16 + l16][b];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const v4i z = {0, 0, 0, 0};
+                    const v4i c = __builtin_amdgcn_mfma_i32_16x16x32_i8(av[i], bv[j], z, 0, 0, 0);
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc[i][j][v] = __builtin_fmaf(dw[i][v] * dt[j], (float)c[v], acc[i][j][v]);
+                }
+        }
+        __syncthreads();
+    }
+    // epilogue: lane holds rows r0+wr+i*16+kg*4+v (4 consecutive) of token t0+wt+j*16+l16
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int64_t t = t0 + wt + j * 16 + l16;
+        if (t >= g.T) continue;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int64_t r = r0 + wr + i * 16 + kg * 4;
+            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            float *y = g.y + t * g.ldy + r;
+            if (EPI == EPI_ADD) {
+                const float *rs = g.resid + t * g.ldy + r;
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    if (r + v < g.rows) o[v] = o[v] + rs[v];
+            }
+            if (r + 3 < g.rows && (g.ldy & 3) == 0) {
+                *(float4 *)y = make_float4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    if (r + v < g.rows) y[v] = o[v];
+            }
+        }
+    }
+}
+
+// ---- RoPE + q scale + KV store for T prompt tokens (positions p0 .. p0+T-1) --------------------
+// Same per-element arithmetic as the decode attention (src/gemma_model.cpp:698-718, 499-518).
+__global__ void __launch_bounds__(256) k_rope_kv_prefill(ropekv_args a) {
+    const int t = blockIdx.x, tid = threadIdx.x, half = a.hd / 2, p = a.p0 + t;
+    const float *row = a.qkv + (int64_t)t * a.ldqkv;
+    const float *cs = a.rope_cos + (int64_t)p * half, *sn = a.rope_sin + (int64_t)p * half;
+    const int kvw = a.Hkv * a.hd;
+    for (int i = tid; i < a.H * half; i += 256) {
+        const int h = i / half, e = i % half;
+        const float x0 = row[h * a.hd + e], x1 = row[h * a.hd + e + half], c = cs[e], s = sn[e];
+        const float p0 = x0 * c, p1 = x1 * s, p2 = x0 * s, p3 = x1 * c;
+        const float r0 = p0 - p1, r1 = p2 + p3;
+        uint16_t *qo = a.q16 + ((int64_t)t * a.H + h) * a.hd;
+        qo[e] = (uint16_t)f2h(r0 * a.q_scale);
+        qo[e + half] = (uint16_t)f2h(r1 * a.q_scale);
+    }
+    const float *kr = row + (int64_t)a.H * a.hd, *vr = kr + kvw;
+    for (int i = tid; i < a.Hkv * half; i += 256) {
+        const int kh = i / half, e = i % half;
+        const float x0 = kr[kh * a.hd + e], x1 = kr[kh * a.hd + e + half], c = cs[e], s = sn[e];
+        const float p0 = x0 * c, p1 = x1 * s, p2 = x0 * s, p3 = x1 * c;
+        a.kc[(int64_t)p * kvw + kh * a.hd + e] = (uint16_t)f2h(p0 - p1);
+        a.kc[(int64_t)p * kvw + kh * a.hd + e + half] = (uint16_t)f2h(p2 + p3);
+    }
+    for (int d = tid; d < kvw; d += 256) a.vc[(int64_t)d * a.ctx + p] = (uint16_t)f2h(vr[d]);
+}
+
+// ---- causal prefill attention on f16 MFMA ---------------------------------------------------------
+// A workgroup takes 64 query rows = (query, head) pairs of one kv head: QBQ = 64/G consecutive
+// queries x the G heads sharing that kv head, so each K/V block is staged once for all of them.
+// Per 64-key block: S = Q K^T (v_mfma_f32_16x16x32_f16, f32 accumulate of exact f16 products).
+// ggml's soft_max_ext needs the row max before any e is formed (e = f16(exp(f16(w - max)))), so
+// S is formed three times: (1) max, (2) the exact integer sum of e (as the decode kernel), (3)
+// P16 = f16(e * (float)(1/sum)) and O += P V.  Only the fp32 order of the S and O sums differs
+// from ggml's vec_dot_f16 lane order.
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+constexpr int AP_HD = 256, AP_QS = AP_HD + 8, AP_KB = 64, AP_VS = AP_KB + 8;
+
+__device__ __forceinline__ float row16_max(float v) {  // max over the 16 lanes of a DPP row
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    v = fmaxf(v, dpp_f<0x140>(v));
+    return v;
+}
+__device__ __forceinline__ unsigned long long row16_sum(unsigned long long v) {  // exact (integers)
+    auto step = [&](auto ctrl) {
+        constexpr int C = decltype(ctrl)::value;
+        const unsigned long long t = ((unsigned long long)dpp_u<C>((uint32_t)(v >> 32)) << 32) | dpp_u<C>((uint32_t)v);
+        v += t;
+    };
+    step(std::integral_constant<int, 0xB1>());
+    step(std::integral_constant<int, 0x4E>());
+    step(std::integral_constant<int, 0x141>());
+    step(std::integral_constant<int, 0x140>());
+    return v;
+}
+
+__global__ void __launch_bounds__(256) k_attn_prefill(attnp_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint16_t *Qs = (uint16_t *)smem;           // [64][AP_QS]
+    uint16_t *Ks = Qs + 64 * AP_QS;            // [AP_KB][AP_QS]
+    uint16_t *Vt = Ks + AP_KB * AP_QS;         // [AP_HD][AP_VS]  (V^T block: dims x keys)
+    uint16_t *Ps = Vt + AP_HD * AP_VS;         // [64][AP_VS]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, kg = lane >> 4;
+    const int G = a.H / a.Hkv, QBQ = 64 / G, kvh = blockIdx.y;
+    const int tq0 = blockIdx.x * QBQ;
+    const int kvw = a.Hkv * AP_HD;
+    // stage the 64 query rows (row m -> query tq0 + m / G, head kvh*G + m % G)
+    for (int c = tid; c < 64 * (AP_HD / 8); c += 256) {
+        const int m = c / (AP_HD / 8), seg = c % (AP_HD / 8);
+        int t = tq0 + m / G;
+        t = t < a.T ? t : a.T - 1;
+        const int h = kvh * G + m % G;
+        *(uint4 *)(Qs + m * AP_QS + seg * 8) = *(const uint4 *)(a.q16 + ((int64_t)t * a.H + h) * AP_HD + seg * 8);
+    }
+    // this wave's rows: 16*wave + kg*4 + v  ->  their query positions (for the causal mask)
+    int tr[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) tr[v] = tq0 + (16 * wave + kg * 4 + v) / G;
+    const int t_last = min(tq0 + QBQ - 1, a.T - 1);
+    const int n_kb = t_last / AP_KB + 1;  // key blocks reaching the last query (keys j <= t only)
+    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    unsigned long long isum[4] = {0, 0, 0, 0};
+    float inv[4];
+    v4f o[16];
+#pragma unroll
+    for (int n = 0; n < 16; ++n) o[n] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+    auto stage_k = [&](int kb) {
+        for (int c = tid; c < AP_KB * (AP_HD / 8); c += 256) {
+            const int r = c / (AP_HD / 8), seg = c % (AP_HD / 8);
+            const int j = kb * AP_KB + r;
+            const int jc = j < a.ctx ? j : 0;
+            *(uint4 *)(Ks + r * AP_QS + seg * 8) = *(const uint4 *)(a.kc + (int64_t)jc * kvw + kvh * AP_HD + seg * 8);
+        }
+    };
+    auto scores = [&](v4f S[4]) {  // S[c][v]: row 16*wave + kg*4 + v, key kb*64 + c*16 + l16
+#pragma unroll
+        for (int c = 0; c < 4; ++c) S[c] = (v4f){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < AP_HD / 32; ++ks) {
+            const v8h av = *(const v8h *)(Qs + (16 * wave + l16) * AP_QS + ks * 32 + kg * 8);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const v8h bv = *(const v8h *)(Ks + (c * 16 + l16) * AP_QS + ks * 32 + kg * 8);
+                S[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, S[c], 0, 0, 0);
+            }
+        }
+    };
+    // the mfma output row for (c, v) is 16*wave + kg*4 + v; keys are per lane: kb*64 + c*16 + l16
+    for (int pass = 0; pass < 3; ++pass) {
+        for (int kb = 0; kb < n_kb; ++kb) {
+            __syncthreads();
+            stage_k(kb);
+            if (pass == 2)
+                for (int c = tid; c < AP_HD * (AP_KB / 8); c += 256) {
+                    const int d = c / (AP_KB / 8), seg = c % (AP_KB / 8);
+                    const int j0 = kb * AP_KB + seg * 8;
+                    const int jc = j0 + 8 <= a.ctx ? j0 : 0;
+                    *(uint4 *)(Vt + d * AP_VS + seg * 8) =
+                        *(const uint4 *)(a.vc + ((int64_t)kvh * AP_HD + d) * a.ctx + jc);
+                }
+            __syncthreads();
+            v4f S[4];
+            scores(S);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int j = kb * AP_KB + c * 16 + l16;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const bool live = j <= tr[v] && j < a.n_kv;  // mask j > pos -> -inf
+                    const float w = S[c][v] * 1.0f + 0.0f;
+                    if (pass == 0) {
+                        if (live) mx[v] = fmaxf(mx[v], w);
+                    } else {
+                        uint32_t e16 = 0;
+                        if (live) e16 = exp_f16_of(f2h(w - mx[v]));
+                        if (pass == 1) {
+                            isum[v] += (unsigned long long)(h2f(e16) * 16777216.0f);
+                        } else {
+                            Ps[(16 * wave + kg * 4 + v) * AP_VS + c * 16 + l16] = (uint16_t)f2h(h2f(e16) * inv[v]);
+                        }
+                    }
+                }
+            }
+            if (pass == 2) {
+                // O[rows][dims] += P[rows][keys] . V[keys][dims]  (Ps rows are this wave's own)
+#pragma unroll
+                for (int kk = 0; kk < AP_KB / 32; ++kk) {
+                    const v8h pv = *(const v8h *)(Ps + (16 * wave + l16) * AP_VS + kk * 32 + kg * 8);
+#pragma unroll
+                    for (int n = 0; n < 16; ++n) {
+                        const v8h vv = *(const v8h *)(Vt + (n * 16 + l16) * AP_VS + kk * 32 + kg * 8);
+                        o[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pv, vv, o[n], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        if (pass == 0) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) mx[v] = row16_max(mx[v]);
+        } else if (pass == 1) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const unsigned long long tot = row16_sum(isum[v]);
+                const double sum = (double)tot * (1.0 / 16777216.0);
+                inv[v] = (float)(1.0 / sum);
+            }
+        }
+    }
+    // out[t][h*hd + d]: lane holds rows 16*wave + kg*4 + v, dims n*16 + l16
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const int m = 16 * wave + kg * 4 + v, t = tq0 + m / G, h = kvh * G + m % G;
+        if (t >= a.T) continue;
+        float *orow = a.out + (int64_t)t * a.ldo + (int64_t)h * AP_HD;
+#pragma unroll
+        for (int n = 0; n < 16; ++n) orow[n * 16 + l16] = o[n][v];
+    }
+}
+
+// argmax over one logits row -> per-workgroup partial keys (ordered float, ~index), reduced by
+// k_advance exactly as in the decode step (first max wins, src/gemma_model.cpp:538-543)
+__global__ void __launch_bounds__(256) k_row_argmax(const float *row, int64_t n, unsigned long long *keys) {
+    unsigned long long best = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t u = __builtin_bit_cast(uint32_t, row[i]);
+        u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        const unsigned long long key = ((unsigned long long)u << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)i);
+        best = key > best ? key : best;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    __shared__ unsigned long long red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
+        keys[blockIdx.x] = best;
+    }
+}
+
+}  // namespace
+
+int launch_quant_rows(int mode, const qrow_args &a, int T, hipStream_t s) {
+    if (a.K % 32 || a.ldq % 256 || a.ldq < a.K || a.ldd * 32 < a.ldq) {
+        set_error("quant_rows: K must be a multiple of 32, ldq a multiple of 256");
+        return -1;
+    }
+    switch (mode) {
+        case QR_F32: hipLaunchKernelGGL(k_quant_rows<QR_F32>, dim3(T), dim3(256), 0, s, a); break;
+        case QR_NORM: hipLaunchKernelGGL(k_quant_rows<QR_NORM>, dim3(T), dim3(256), 0, s, a); break;
+        case QR_EMBED_NORM: hipLaunchKernelGGL(k_quant_rows<QR_EMBED_NORM>, dim3(T), dim3(256), 0, s, a); break;
+        case QR_GELU: hipLaunchKernelGGL(k_quant_rows<QR_GELU>, dim3(T), dim3(256), 0, s, a); break;
+        default: set_error("quant_rows: bad mode"); return -1;
+    }
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s) {
+    if (g.ldq % 256 || g.nb * 32 > g.ldq) {
+        set_error("gemm_q: activation image must be padded to 256 elements");
+        return -1;
+    }
+    const dim3 grid((unsigned)((g.rows + GM - 1) / GM), (unsigned)((g.T + GN - 1) / GN));
+    if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_q<T_Q4_0, EPI_STORE>), grid, dim3(256), 0, s, g);
+    else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_q<T_Q4_0, EPI_ADD>), grid, dim3(256), 0, s, g);
+    else if (wtype == T_Q8_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_q<T_Q8_0, EPI_STORE>), grid, dim3(256), 0, s, g);
+    else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_q<T_Q8_0, EPI_ADD>), grid, dim3(256), 0, s, g);
+    else {
+        set_error("gemm_q: unsupported (type, epilogue)");
+        return -1;
+    }
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_row_argmax(const float *row, int64_t n, unsigned long long *keys, int parts, hipStream_t s) {
+    hipLaunchKernelGGL(k_row_argmax, dim3(parts), dim3(256), 0, s, row, n, keys);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_rope_kv_prefill(const ropekv_args &a, int T, hipStream_t s) {
+    hipLaunchKernelGGL(k_rope_kv_prefill, dim3(T), dim3(256), 0, s, a);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_attn_prefill(const attnp_args &a, hipStream_t s) {
+    const int G = a.H / a.Hkv;
+    if (a.hd != AP_HD || a.H % a.Hkv || 64 % G || a.ctx % 8) {
+        set_error("attn_prefill: unsupported shape (head_dim 256, 64 % G == 0)");
+        return -1;
+    }
+    const size_t lds = (size_t)(64 * AP_QS + AP_KB * AP_QS + AP_HD * AP_VS + 64 * AP_VS) * 2;
+    GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_prefill, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int QBQ = 64 / G;
+    hipLaunchKernelGGL(k_attn_prefill, dim3((a.T + QBQ - 1) / QBQ, a.Hkv), dim3(256), lds, s, a);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace ghip

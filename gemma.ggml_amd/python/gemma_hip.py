@@ -167,12 +167,14 @@ class Engine:
         n = self.L.gemma_engine_tokens(self.h, _p(out), len(out))
         return out[:n]
 
-    def prefill(self, want_all=False):
+    def prefill(self, n_prompt=None, want_all=False):
+        """MFMA prefill of the prompt given to begin(); returns (token, last-row logits[, all rows])."""
         last = np.zeros(self.cfg.n_vocab, dtype=np.float32)
-        tok = self.L.gemma_engine_prefill(self.h, _p(last), None)
+        allv = np.zeros((n_prompt, self.cfg.n_vocab), dtype=np.float32) if want_all else None
+        tok = self.L.gemma_engine_prefill(self.h, _p(last), _p(allv) if want_all else None)
         if tok < 0:
             raise RuntimeError("prefill failed: " + last_error())
-        return tok, last
+        return (tok, last, allv) if want_all else (tok, last)
 
     def tensor(self, tid, nbytes):
         out = np.zeros(nbytes, dtype=np.uint8)

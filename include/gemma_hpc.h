@@ -77,6 +77,8 @@ double gemma_engine_time(gemma_engine *e, int which, int iters, double *algo_byt
 int gemma_engine_sync(gemma_engine *e);
 /* debugging: one eager step with per-layer taps [n_layer][qkv | attn_out | layer_out] */
 int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
+/* diagnostics: MFMA prefill with the residual stream after each layer -> [n_layer][T][n_embd] */
+int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps);
 /* diagnostics: one eager step with s_memrealtime phase stamps (100 MHz) of layer `layer`'s five
  * kernels (regions 0..4: qkv, attention, attn-out, gate/up, down) and the logits kernel (region 5);
  * out = 6 * 4096 * 16 u64, slot [region][workgroup][phase], unused slots 0 */
@@ -87,6 +89,9 @@ int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos
                            float rope_base, float *out, float *dbg_w, uint16_t *dbg_p, float *dbg_inv,
                            unsigned long long *dbg_t, int mode);
 
+/* per-op test entry: the prefill path's Q8_0 row quantization + int8 MFMA GEMM on host buffers */
+int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X, float *Y,
+                    int8_t *xq_out, float *da_out);
 /* measured HBM read roofline: streaming read of `bytes` on `device`, `iters` passes; GB/s */
 double gemma_hbm_read_gbs(int device, size_t bytes, int iters);
 /* per-op test entry: the softmax's exp(f16) for all 65536 codes (compared with ggml's table) */
