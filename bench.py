@@ -8,9 +8,10 @@ shapes, generated on the GPU; DESIGN.md §Synthetic weights) — no checkpoint i
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--profile-out PATH]
 
-N > 1: one process per GPU (torch.distributed.run), every rank runs its own replica of the
-single-stream decode (DESIGN.md §Multi-GPU: "replicas" until the row-split TP engine lands);
-value = tokens over all ranks / max-over-ranks time.  Rank 0 prints ONE JSON line.
+N > 1: one process per GPU (torch.distributed.run).  The headline `value` runs one independent
+Gemma-2B decode stream per GPU (weak scaling: tokens over all ranks / max-over-ranks time); the
+`tp_decode` leg runs BASELINE config 4 — Gemma-7B decode with every weight matrix row-split across
+the N GPUs and RCCL all-gathers (strong scaling of one stream).  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -23,6 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "gemma.ggml_amd", "python"))
 
 METRIC = "decode tok/s + prefill tok/s, Gemma-2B Q4_0, 1/2/4/8 MI355X; %HBM roofline"
 GEMMA_2B = dict(n_layer=18, n_embd=2048, n_head=8, n_head_kv=1, head_dim=256, n_ff=16384, n_vocab=256000)
+GEMMA_7B = dict(n_layer=28, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, n_ff=24576, n_vocab=256000)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
 KERNEL_NAMES = {0: "ffn gate/up matvec (+norm, +gelu*mul)", 1: "ffn down matvec (+resid)",
                 2: "qkv matvec (+norm)", 3: "attn-out matvec (+resid)", 4: "logits matvec (+argmax)"}
@@ -90,6 +92,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--prefill", type=int, default=2048, help="prefill leg prompt length (0 = skip)")
+    ap.add_argument("--tp-steps", type=int, default=48, help="Gemma-7B row-split decode leg steps (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -132,6 +135,40 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+
+    # row-split TP leg (BASELINE config 4): Gemma-7B Q4_0 batch-1 decode, weights row-split across
+    # the job's GPUs with RCCL all-gathers (one rank per GPU; at N = 1 the same engine unsplit)
+    tp = None
+    if args.tp_steps > 0:
+        try:
+            import torch as _t
+            rid = None
+            if world > 1:
+                idt = _t.zeros(256, dtype=_t.uint8)
+                if rank == 0:
+                    raw = G.tp_unique_id()
+                    idt[: len(raw)] = _t.tensor(list(raw), dtype=_t.uint8)
+                dist.broadcast(idt, 0)
+                rid = bytes(idt.numpy())
+            te = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=(world, rank, rid))
+            te.begin(make_prompt(16, GEMMA_7B["n_vocab"]))
+            te.step(16 + 4, use_graph=True)
+            barrier_sync()
+            t0 = time.perf_counter()
+            te.step(args.tp_steps, use_graph=True)
+            te.L.gemma_engine_sync(te.h)
+            barrier_sync()
+            tdt = time.perf_counter() - t0
+            if dist is not None:
+                tt = torch.tensor([tdt], dtype=torch.float64)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                tdt = float(tt.item())
+            te.close()
+            tp = {"model": "Gemma-7B " + args.wtype.upper(), "ranks": world, "tok_s": round(args.tp_steps / tdt, 2),
+                  "ms_per_token": round(tdt / args.tp_steps * 1e3, 4), "steps": args.tp_steps,
+                  "parallelism": f"row-split tp{world} (RCCL all-gather x4/layer)" if world > 1 else "1 GPU"}
+        except Exception as ex:  # reported, never fatal to the headline line
+            tp = {"error": str(ex)[:300]}
 
     # prefill leg (BASELINE config 3): MFMA prefill of a 2048-token synthetic prompt (all rows' logits)
     prefill = None
@@ -192,6 +229,7 @@ def main():
             "decode_tok_s": round(n_tok / dt, 2),
             "prefill_tok_s": prefill["tok_s"] if prefill else None,
             "prefill": prefill,
+            "tp_decode": tp,
             "prefill_serial_tok_s": round(args.prompt / prefill_serial_s, 2),
             "roofline": {"bound": "hbm", "kernel": KERNEL_NAMES[dominant], "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

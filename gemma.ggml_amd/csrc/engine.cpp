@@ -9,6 +9,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <memory>
 #include <mutex>
@@ -154,6 +156,14 @@ struct gemma_engine {
     std::vector<layer_dev> layers;
     uint16_t *kc = nullptr, *vc = nullptr;  // [L][ctx][kvw], [L][kvw][ctx]
     int att_mode = ATTN_PER_HEAD;
+    // row-split tensor parallelism: this rank's contiguous row range of every
+    // matrix; activations are full vectors, each matvec writes its shard in place and an in-place
+    // RCCL all-gather completes them
+    int tp_n = 1, tp_rank = 0;
+    int n_virtual = 1;  // > 1: all tp_n ranks' shards in this one engine (single-GPU parity mode, no RCCL)
+    ncclComm_t comm = nullptr;
+    int64_t sh_qkv = 0, sh_e = 0, sh_ff = 0, sh_v = 0;  // rows per rank (qkv, n_embd, n_ff, n_vocab)
+    unsigned long long *rank_keys = nullptr;           // [tp_n] one argmax key per rank
     attn_geom ag;                           // split-attention geometry and its scratch
     float *att_sbuf = nullptr;
     int *att_sync = nullptr;                // hand-off counters [Hkv][2] + sticky error word
@@ -191,12 +201,28 @@ static unsigned long long *stamp_region(gemma_engine *e, int il, int k) {
     return (e->stamp && il == e->stamp_layer) ? e->stamp + (size_t)k * kStampRegion : nullptr;
 }
 
-// largest power-of-two K split <= target that divides the block-tile count
-static int pick_ks(int64_t n_bt, int target) {
+// largest power-of-two K split <= target that divides the block-tile count and whose LDS image
+// (activation + carry stash) fits the 160 KiB of a CU (Gemma-7B's down, K = 24576, steps to KS 1)
+static int pick_ks(int wtype, int64_t n_bt, int target) {
     int ks = target;
-    while (ks > 1 && n_bt % ks) ks >>= 1;
+    while (ks > 1 && (n_bt % ks || matvec_lds_bytes(wtype, ks, n_bt, n_bt / ks) > 160 * 1024)) ks >>= 1;
     return ks;
 }
+
+// in-place all-gather of a full vector whose rank-r shard [r*cnt, (r+1)*cnt) was just written
+static int tp_gather(gemma_engine *e, float *full, int64_t cnt) {
+    if (e->tp_n == 1 || !e->comm) return 0;  // one rank, or virtual ranks (shards already in place)
+    const ncclResult_t r = ncclAllGather(full + (size_t)e->tp_rank * cnt, full, (size_t)cnt, ncclFloat, e->comm, e->stream);
+    if (r != ncclSuccess) {
+        set_error(std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        return -1;
+    }
+    return 0;
+}
+
+// layer il's shards of (virtual) rank slot vr, and the rank that slot stands for
+static inline layer_dev &layer_of(gemma_engine *e, int il, int vr) { return e->layers[(size_t)il * e->n_virtual + vr]; }
+static inline int rank_of(const gemma_engine *e, int vr) { return e->n_virtual > 1 ? vr : e->tp_rank; }
 
 static int enqueue_step(gemma_engine *e) {
     const gemma_hip_config &c = e->cfg;
@@ -204,25 +230,29 @@ static int enqueue_step(gemma_engine *e) {
     hipStream_t s = e->stream;
     const int E = c.n_embd;
     for (int il = 0; il < c.n_layer; ++il) {
-        layer_dev &L = e->layers[il];
-        // K1: [embed | rms_norm*attn_norm] + quantize -> Wq|Wk|Wv   (:677-696)
-        mv_args a;
-        a.qs = L.qkv.qs; a.sc = L.qkv.sc; a.rows = L.qkv.rows; a.n_rt = L.qkv.n_rt; a.n_bt = L.qkv.n_bt;
-        a.nb = L.qkv.nb;
-        a.norm_w = L.attn_norm; a.eps = c.eps; a.y = e->qkv;
-        int pro = PRO_NORM;
-        if (il == 0) {
-            pro = PRO_EMBED;
-            a.x = e->hist; a.tok_pos = e->pos;
-            a.emb_qs = e->embd.qs; a.emb_sc = e->embd.sc; a.emb_n_bt = e->embd.n_bt;
-            a.emb_scale = sqrtf((float)E);
-            a.emb_out = e->x;
-        } else {
-            a.x = e->x;
+        // K1: [embed | rms_norm*attn_norm] + quantize -> Wq|Wk|Wv   (:677-696); each rank its rows
+        for (int vr = 0; vr < e->n_virtual; ++vr) {
+            layer_dev &L = layer_of(e, il, vr);
+            mv_args a;
+            a.qs = L.qkv.qs; a.sc = L.qkv.sc; a.rows = L.qkv.rows; a.n_rt = L.qkv.n_rt; a.n_bt = L.qkv.n_bt;
+            a.nb = L.qkv.nb;
+            a.norm_w = L.attn_norm; a.eps = c.eps;
+            int pro = PRO_NORM;
+            if (il == 0) {
+                pro = PRO_EMBED;
+                a.x = e->hist; a.tok_pos = e->pos;
+                a.emb_qs = e->embd.qs; a.emb_sc = e->embd.sc; a.emb_n_bt = e->embd.n_bt;
+                a.emb_scale = sqrtf((float)E);
+                a.emb_out = e->x;
+            } else {
+                a.x = e->x;
+            }
+            a.dbg_t = stamp_region(e, il, 0);
+            a.y = e->qkv + (size_t)rank_of(e, vr) * e->sh_qkv;  // this rank's rows of q|k|v
+            if (launch_matvec(wt, pick_ks(wt, L.qkv.n_bt, e->ks_small), pro, EPI_STORE, a, (int)L.qkv.n_rt, s)) return -1;
         }
-        a.dbg_t = stamp_region(e, il, 0);
-        if (launch_matvec(wt, pick_ks(L.qkv.n_bt, e->ks_small), pro, EPI_STORE, a, (int)L.qkv.n_rt, s)) return -1;
-        // K2: rope + scale + kv store + KQ + softmax + KQV  (:698-718, :454-518)
+        if (tp_gather(e, e->qkv, e->sh_qkv)) return -1;
+        // K2: rope + scale + kv store + KQ + softmax + KQV  (:698-718, :454-518); replicated
         attn_args t;
         t.qkv = e->qkv;
         t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
@@ -240,46 +270,77 @@ static int enqueue_step(gemma_engine *e) {
         if (e->dbg)
             GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows, e->attn, (size_t)e->qw * 4, hipMemcpyDeviceToDevice, s));
         // K3: quantize(attn) -> Wo, + inpL  (:493, :723)
-        mv_args b;
-        b.qs = L.o.qs; b.sc = L.o.sc; b.rows = L.o.rows; b.n_rt = L.o.n_rt; b.n_bt = L.o.n_bt; b.nb = L.o.nb;
-        b.x = e->attn; b.y = e->sa; b.resid = e->x;
-        b.dbg_t = stamp_region(e, il, 2);
-        if (launch_matvec(wt, pick_ks(L.o.n_bt, e->ks_small), PRO_F32, EPI_ADD, b, (int)L.o.n_rt, s)) return -1;
+        for (int vr = 0; vr < e->n_virtual; ++vr) {
+            layer_dev &L = layer_of(e, il, vr);
+            const size_t r0 = (size_t)rank_of(e, vr) * e->sh_e;
+            mv_args b;
+            b.qs = L.o.qs; b.sc = L.o.sc; b.rows = L.o.rows; b.n_rt = L.o.n_rt; b.n_bt = L.o.n_bt; b.nb = L.o.nb;
+            b.x = e->attn; b.y = e->sa + r0; b.resid = e->x + r0;
+            b.dbg_t = stamp_region(e, il, 2);
+            if (launch_matvec(wt, pick_ks(wt, L.o.n_bt, e->ks_small), PRO_F32, EPI_ADD, b, (int)L.o.n_rt, s)) return -1;
+        }
+        if (tp_gather(e, e->sa, e->sh_e)) return -1;
         // K4: rms_norm*ffn_norm + quantize -> gate & up -> gelu(gate)*up  (:724, :446-449)
-        mv_args g;
-        g.qs = L.gate.qs; g.sc = L.gate.sc; g.qs2 = L.up.qs; g.sc2 = L.up.sc;
-        g.rows = L.gate.rows; g.n_rt = L.gate.n_rt; g.n_bt = L.gate.n_bt; g.nb = L.gate.nb;
-        g.x = e->sa; g.norm_w = L.ffn_norm; g.eps = c.eps; g.y = e->h;
-        g.gelu_tab = e->gelu_tab; g.gelu_clamp = c.gelu_clamp;
-        g.dbg_t = stamp_region(e, il, 3);
-        if (launch_matvec(wt, 1, PRO_NORM, EPI_GELU_MUL, g, (int)std::min<int64_t>((L.gate.n_rt + 3) / 4, e->grid_big), s))
-            return -1;
+        for (int vr = 0; vr < e->n_virtual; ++vr) {
+            layer_dev &L = layer_of(e, il, vr);
+            mv_args g;
+            g.qs = L.gate.qs; g.sc = L.gate.sc; g.qs2 = L.up.qs; g.sc2 = L.up.sc;
+            g.rows = L.gate.rows; g.n_rt = L.gate.n_rt; g.n_bt = L.gate.n_bt; g.nb = L.gate.nb;
+            g.x = e->sa; g.norm_w = L.ffn_norm; g.eps = c.eps; g.y = e->h + (size_t)rank_of(e, vr) * e->sh_ff;
+            g.gelu_tab = e->gelu_tab; g.gelu_clamp = c.gelu_clamp;
+            g.dbg_t = stamp_region(e, il, 3);
+            if (launch_matvec(wt, 1, PRO_NORM, EPI_GELU_MUL, g, (int)std::min<int64_t>((L.gate.n_rt + 3) / 4, e->grid_big),
+                              s))
+                return -1;
+        }
+        if (tp_gather(e, e->h, e->sh_ff)) return -1;
         // K5: quantize(h) -> Wdown, + sa  (:450, :731)
-        mv_args d;
-        d.qs = L.down.qs; d.sc = L.down.sc; d.rows = L.down.rows; d.n_rt = L.down.n_rt; d.n_bt = L.down.n_bt;
-        d.nb = L.down.nb;
-        d.x = e->h; d.y = e->x; d.resid = e->sa;
-        d.dbg_t = stamp_region(e, il, 4);
-        if (launch_matvec(wt, pick_ks(L.down.n_bt, e->ks_down), PRO_F32, EPI_ADD, d, (int)L.down.n_rt, s)) return -1;
+        for (int vr = 0; vr < e->n_virtual; ++vr) {
+            layer_dev &L = layer_of(e, il, vr);
+            const size_t r0 = (size_t)rank_of(e, vr) * e->sh_e;
+            mv_args d;
+            d.qs = L.down.qs; d.sc = L.down.sc; d.rows = L.down.rows; d.n_rt = L.down.n_rt; d.n_bt = L.down.n_bt;
+            d.nb = L.down.nb;
+            d.x = e->h; d.y = e->x + r0; d.resid = e->sa + r0;
+            d.dbg_t = stamp_region(e, il, 4);
+            if (launch_matvec(wt, pick_ks(wt, L.down.n_bt, e->ks_down), PRO_F32, EPI_ADD, d, (int)L.down.n_rt, s)) return -1;
+        }
+        if (tp_gather(e, e->x, e->sh_e)) return -1;
         if (e->dbg)
             GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows + e->qw, e->x, (size_t)E * 4, hipMemcpyDeviceToDevice, s));
     }
     // K6: rms_norm*output_norm + quantize -> tied output -> logits + argmax  (:736-740, :532-546)
-    mv_args o;
-    o.qs = e->embd.qs; o.sc = e->embd.sc; o.rows = e->embd.rows; o.n_rt = e->embd.n_rt; o.n_bt = e->embd.n_bt;
-    o.nb = e->embd.nb;
-    o.x = e->x; o.norm_w = e->out_norm; o.eps = c.eps; o.y = e->logits; o.argmax_key = e->key;
-    const int lg_grid = (int)std::min<int64_t>((e->embd.n_rt + 3) / 4, e->grid_big);
-    o.dbg_t = e->stamp ? e->stamp + 5 * kStampRegion : nullptr;
-    if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, lg_grid, s)) return -1;
-    // K7: token feedback (greedy_sample -> input.push_back, :282-285), position += 1
-    // the prompt is never overwritten: hist writes only land at positions >= n_prompt
+    // K7: token feedback (greedy_sample -> input.push_back, :282-285), position += 1; the prompt is
+    // never overwritten: hist writes only land at positions >= n_prompt
     rope_row rr;
     rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
-    return launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
+    int lg_grid = 0;
+    for (int vr = 0; vr < e->n_virtual; ++vr) {
+        const int rk = rank_of(e, vr);
+        const tiled_mat out_rows = sub_rows(e->embd, (int64_t)rk * e->sh_v, e->sh_v);  // tied output, this rank's vocab
+        mv_args o;
+        o.qs = out_rows.qs; o.sc = out_rows.sc; o.rows = out_rows.rows; o.n_rt = out_rows.n_rt; o.n_bt = out_rows.n_bt;
+        o.nb = out_rows.nb;
+        o.x = e->x; o.norm_w = e->out_norm; o.eps = c.eps; o.y = e->logits + (size_t)rk * e->sh_v;
+        o.argmax_key = e->key;
+        lg_grid = (int)std::min<int64_t>((out_rows.n_rt + 3) / 4, e->grid_big);
+        o.dbg_t = e->stamp ? e->stamp + 5 * kStampRegion : nullptr;
+        if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, lg_grid, s)) return -1;
+        // TP: one key per rank, its index made global
+        if (e->tp_n > 1 && launch_reduce_keys(e->key, lg_grid, (int64_t)rk * e->sh_v, e->rank_keys + rk, s)) return -1;
+    }
+    if (e->tp_n == 1) return launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
+    if (e->comm) {
+        const ncclResult_t nr = ncclAllGather(e->rank_keys + e->tp_rank, e->rank_keys, 1, ncclUint64, e->comm, s);
+        if (nr != ncclSuccess) {
+            set_error(std::string("ncclAllGather(keys): ") + ncclGetErrorString(nr));
+            return -1;
+        }
+    }
+    return launch_advance(e->rank_keys, e->tp_n, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
 }
 
-extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int device) {
+static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int tp_n, int tp_rank, const void *nccl_id) {
     set_error("");
     const gemma_hip_config &c = *cfg;
     if (c.head_dim % 32 || c.n_embd % 32 || c.n_ff % 32 || c.n_ctx % 32 || c.n_head % c.n_head_kv ||
@@ -298,6 +359,19 @@ extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int de
     e->qw = c.n_head * c.head_dim;
     e->kvw = c.n_head_kv * c.head_dim;
     e->qkv_rows = e->qw + 2 * e->kvw;
+    e->tp_n = tp_n;
+    e->tp_rank = tp_rank;
+    // every matrix is cut into tp_n contiguous row ranges of whole 8-row tiles
+    if (tp_n < 1 || tp_rank < 0 || tp_rank >= tp_n || e->qkv_rows % (8 * tp_n) || c.n_embd % (8 * tp_n) ||
+        c.n_ff % (8 * tp_n) || c.n_vocab % (8 * tp_n)) {
+        set_error("gemma_engine_create: row split needs every matrix's rows to divide into 8-row tiles per rank");
+        delete e;
+        return nullptr;
+    }
+    e->sh_qkv = e->qkv_rows / tp_n;
+    e->sh_e = c.n_embd / tp_n;
+    e->sh_ff = c.n_ff / tp_n;
+    e->sh_v = c.n_vocab / tp_n;
     if (const char *v = getenv("GHIP_KS_SMALL")) e->ks_small = atoi(v);
     if (const char *v = getenv("GHIP_KS_DOWN")) e->ks_down = atoi(v);
     if (const char *v = getenv("GHIP_GRID_BIG")) e->grid_big = atoi(v);
@@ -309,27 +383,42 @@ extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int de
     launch_synth_tiled(e->embd, tensor_key(seed, TID_EMBD), synth_scale(1.0 / sqrt((double)c.n_embd)), 0, s);
     GHIP_FATAL(hipMalloc(&e->out_norm, (size_t)c.n_embd * 4));
     launch_synth_norm(e->out_norm, c.n_embd, tensor_key(seed, TID_OUT_NORM), synth_scale(0.05), s);
-    e->layers.resize(c.n_layer);
+    e->n_virtual = (tp_n > 1 && !nccl_id) ? tp_n : 1;
+    e->layers.resize((size_t)c.n_layer * e->n_virtual);
     const double se = 1.0 / sqrt((double)c.n_embd), sq = 1.0 / sqrt((double)e->qw), sf = 1.0 / sqrt((double)c.n_ff);
-    for (int il = 0; il < c.n_layer; ++il) {
-        layer_dev &L = e->layers[il];
-        GHIP_FATAL(hipMalloc(&L.attn_norm, (size_t)c.n_embd * 4));
-        GHIP_FATAL(hipMalloc(&L.ffn_norm, (size_t)c.n_embd * 4));
-        launch_synth_norm(L.attn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_ATTN_NORM)), synth_scale(0.05), s);
-        launch_synth_norm(L.ffn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_FFN_NORM)), synth_scale(0.05), s);
-        L.qkv = alloc_tiled(wt, e->qkv_rows, c.n_embd, s);
-        launch_synth_tiled(sub_rows(L.qkv, 0, e->qw), tensor_key(seed, tid_layer(il, L_Q)), synth_scale(se), 0, s);
-        launch_synth_tiled(sub_rows(L.qkv, e->qw, e->kvw), tensor_key(seed, tid_layer(il, L_K)), synth_scale(se), 0, s);
-        launch_synth_tiled(sub_rows(L.qkv, e->qw + e->kvw, e->kvw), tensor_key(seed, tid_layer(il, L_V)),
-                           synth_scale(se), 0, s);
-        L.o = alloc_tiled(wt, c.n_embd, e->qw, s);
-        launch_synth_tiled(L.o, tensor_key(seed, tid_layer(il, L_O)), synth_scale(4.0 * sq), 0, s);
-        L.gate = alloc_tiled(wt, c.n_ff, c.n_embd, s);
-        launch_synth_tiled(L.gate, tensor_key(seed, tid_layer(il, L_GATE)), synth_scale(se), 0, s);
-        L.up = alloc_tiled(wt, c.n_ff, c.n_embd, s);
-        launch_synth_tiled(L.up, tensor_key(seed, tid_layer(il, L_UP)), synth_scale(se), 0, s);
-        L.down = alloc_tiled(wt, c.n_embd, c.n_ff, s);
-        launch_synth_tiled(L.down, tensor_key(seed, tid_layer(il, L_DOWN)), synth_scale(4.0 * sf), 0, s);
+    for (int il = 0; il < c.n_layer; ++il)
+    for (int vr = 0; vr < e->n_virtual; ++vr) {
+        layer_dev &L = layer_of(e, il, vr);
+        const int tp_rank = rank_of(e, vr);
+        if (vr == 0) {
+            GHIP_FATAL(hipMalloc(&L.attn_norm, (size_t)c.n_embd * 4));
+            GHIP_FATAL(hipMalloc(&L.ffn_norm, (size_t)c.n_embd * 4));
+            launch_synth_norm(L.attn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_ATTN_NORM)), synth_scale(0.05), s);
+            launch_synth_norm(L.ffn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_FFN_NORM)), synth_scale(0.05), s);
+        } else {  // norms are replicated: the slot-0 copy serves every virtual rank
+            L.attn_norm = layer_of(e, il, 0).attn_norm;
+            L.ffn_norm = layer_of(e, il, 0).ffn_norm;
+        }
+        // this rank's rows [r0, r0 + n) of the fused [Wq | Wk | Wv]: the pieces of each source tensor
+        const int64_t q0 = (int64_t)tp_rank * e->sh_qkv, qn = e->sh_qkv;
+        L.qkv = alloc_tiled(wt, qn, c.n_embd, s);
+        const int64_t src_start[3] = {0, e->qw, e->qw + e->kvw}, src_rows[3] = {e->qw, e->kvw, e->kvw};
+        const int src_tid[3] = {L_Q, L_K, L_V};
+        for (int k = 0; k < 3; ++k) {
+            const int64_t a0 = std::max(q0, src_start[k]), a1 = std::min(q0 + qn, src_start[k] + src_rows[k]);
+            if (a1 > a0)
+                launch_synth_tiled(sub_rows(L.qkv, a0 - q0, a1 - a0), tensor_key(seed, tid_layer(il, src_tid[k])),
+                                   synth_scale(se), a0 - src_start[k], s);
+        }
+        L.o = alloc_tiled(wt, e->sh_e, e->qw, s);
+        launch_synth_tiled(L.o, tensor_key(seed, tid_layer(il, L_O)), synth_scale(4.0 * sq), (int64_t)tp_rank * e->sh_e, s);
+        L.gate = alloc_tiled(wt, e->sh_ff, c.n_embd, s);
+        launch_synth_tiled(L.gate, tensor_key(seed, tid_layer(il, L_GATE)), synth_scale(se), (int64_t)tp_rank * e->sh_ff, s);
+        L.up = alloc_tiled(wt, e->sh_ff, c.n_embd, s);
+        launch_synth_tiled(L.up, tensor_key(seed, tid_layer(il, L_UP)), synth_scale(se), (int64_t)tp_rank * e->sh_ff, s);
+        L.down = alloc_tiled(wt, e->sh_e, c.n_ff, s);
+        launch_synth_tiled(L.down, tensor_key(seed, tid_layer(il, L_DOWN)), synth_scale(4.0 * sf), (int64_t)tp_rank * e->sh_e,
+                           s);
     }
     // caches, tables, activations
     const size_t kv_elems = (size_t)c.n_layer * c.n_ctx * e->kvw;
@@ -375,7 +464,14 @@ extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int de
     GHIP_FATAL(hipMalloc(&e->hist, (size_t)(c.n_ctx + 1) * 4));
     GHIP_FATAL(hipMemsetAsync(e->key, 0, (size_t)e->grid_big * 8, s));
     GHIP_FATAL(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
+    GHIP_FATAL(hipMalloc(&e->rank_keys, (size_t)tp_n * 8));
     GHIP_FATAL(hipStreamSynchronize(s));
+    if (tp_n > 1 && nccl_id) {
+        ncclUniqueId id;
+        memcpy(&id, nccl_id, sizeof(id));
+        const ncclResult_t nr = ncclCommInitRank(&e->comm, tp_n, id, tp_rank);
+        if (nr != ncclSuccess) set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+    }
     if (!last_error().empty()) {
         gemma_engine_free(e);
         return nullptr;
@@ -383,16 +479,50 @@ extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int de
     return e;
 }
 
+extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int device) {
+    return engine_create(cfg, device, 1, 0, nullptr);
+}
+
+// row-split tensor parallelism: one process per GPU; rank 0 makes the id, every rank gets a copy
+extern "C" int gemma_tp_unique_id(void *out, int cap) {
+    set_error("");
+    if (cap < (int)sizeof(ncclUniqueId)) {
+        set_error("gemma_tp_unique_id: buffer too small");
+        return -1;
+    }
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        set_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+        return -1;
+    }
+    memcpy(out, &id, sizeof(id));
+    return (int)sizeof(id);
+}
+
+// nccl_id == NULL with n_ranks > 1: every rank's shards in this one engine on one GPU (virtual
+// ranks; the parity mode for boxes with a single GPU, where RCCL refuses two ranks per device)
+extern "C" gemma_engine *gemma_engine_create_tp(const gemma_hip_config *cfg, int device, int n_ranks, int rank,
+                                                const void *nccl_id) {
+    return engine_create(cfg, device, n_ranks, nccl_id ? rank : 0, nccl_id);
+}
+
 extern "C" void gemma_engine_free(gemma_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->stream);
+    if (e->comm) (void)ncclCommDestroy(e->comm);
+    if (e->rank_keys) (void)hipFree(e->rank_keys);
     if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
     if (e->graph) (void)hipGraphDestroy(e->graph);
     free_tiled(e->embd);
-    for (auto &L : e->layers) {
+    for (size_t i = 0; i < e->layers.size(); ++i) {
+        layer_dev &L = e->layers[i];
         free_tiled(L.qkv); free_tiled(L.o); free_tiled(L.gate); free_tiled(L.up); free_tiled(L.down);
-        (void)hipFree(L.attn_norm); (void)hipFree(L.ffn_norm);
+        if (i % e->n_virtual == 0) {  // norms are shared by a layer's virtual-rank slots
+            (void)hipFree(L.attn_norm);
+            (void)hipFree(L.ffn_norm);
+        }
     }
     void *bufs[] = {e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
                     e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf.X, e->pf.SA, e->pf.QKV, e->pf.ATT, e->pf.G, e->pf.U,
@@ -457,6 +587,7 @@ extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_
     if (use_graph && !e->graph_exec) {
         // first eager step sets the kernels' LDS attributes before capture
         if (enqueue_step(e)) return -1;
+        if (logits && tp_gather(e, e->logits, e->sh_v)) return -1;
         GHIP_CHECK(hipStreamSynchronize(e->stream));
         if (logits) GHIP_CHECK(hipMemcpy(logits, e->logits, (size_t)c.n_vocab * 4, hipMemcpyDeviceToHost));
         e->host_pos += 1;
@@ -468,6 +599,7 @@ extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_
         if (use_graph) GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
         else if (enqueue_step(e)) return -1;
         if (logits) {
+            if (tp_gather(e, e->logits, e->sh_v)) return -1;  // TP: the other ranks' vocab rows
             GHIP_CHECK(hipMemcpyAsync(logits + (size_t)i * c.n_vocab, e->logits, (size_t)c.n_vocab * 4,
                                       hipMemcpyDeviceToHost, e->stream));
             GHIP_CHECK(hipStreamSynchronize(e->stream));
@@ -558,19 +690,19 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
             break;
         case 1:
             set_mat(L.down);
-            a.x = e->h; a.y = e->x; a.resid = e->sa; ks = pick_ks(L.down.n_bt, e->ks_down); epi = EPI_ADD;
+            a.x = e->h; a.y = e->x; a.resid = e->sa; ks = pick_ks(wt, L.down.n_bt, e->ks_down); epi = EPI_ADD;
             grid = (int)L.down.n_rt;
             bytes = (double)L.down.algo_bytes() + c.n_ff * 4.0 + c.n_embd * 8.0;
             break;
         case 2:
             set_mat(L.qkv);
-            a.x = e->x; a.norm_w = L.attn_norm; a.eps = c.eps; a.y = e->qkv; ks = pick_ks(L.qkv.n_bt, e->ks_small); pro = PRO_NORM;
+            a.x = e->x; a.norm_w = L.attn_norm; a.eps = c.eps; a.y = e->qkv; ks = pick_ks(wt, L.qkv.n_bt, e->ks_small); pro = PRO_NORM;
             grid = (int)L.qkv.n_rt;
             bytes = (double)L.qkv.algo_bytes() + c.n_embd * 8.0 + e->qkv_rows * 4.0;
             break;
         case 3:
             set_mat(L.o);
-            a.x = e->attn; a.y = e->sa; a.resid = e->x; ks = pick_ks(L.o.n_bt, e->ks_small); epi = EPI_ADD;
+            a.x = e->attn; a.y = e->sa; a.resid = e->x; ks = pick_ks(wt, L.o.n_bt, e->ks_small); epi = EPI_ADD;
             grid = (int)L.o.n_rt;
             bytes = (double)L.o.algo_bytes() + e->qw * 4.0 + c.n_embd * 8.0;
             break;
@@ -726,6 +858,10 @@ extern "C" int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *
     const int T = e->n_prompt;
     if (T <= 0 || e->host_pos != 0) {
         set_error("gemma_engine_prefill: call right after gemma_engine_begin");
+        return -1;
+    }
+    if (e->tp_n > 1) {
+        set_error("gemma_engine_prefill: the MFMA prefill is single-GPU (row-split engines prefill token by token)");
         return -1;
     }
     if (prefill_alloc(e, T)) return -1;

@@ -148,6 +148,7 @@ int launch_embed(const uint8_t *qs, const uint8_t *sc, int wtype, int64_t n_bt, 
 // reduces the n_parts per-workgroup argmax keys, appends the token, advances the position
 int launch_exp_f16_all(uint16_t *out, hipStream_t s);
 int launch_stream_read(const void *buf, size_t bytes, unsigned *sink, hipStream_t s);  // roofline probe  // the softmax's exp for all 65536 f16 codes (tests)
+int launch_reduce_keys(const unsigned long long *keys, int n, int64_t row_base, unsigned long long *out, hipStream_t s);
 struct rope_row {  // k_advance also publishes the new position's RoPE row: cur = [cos | sin | (int)pos]
     const float *cos = nullptr, *sin = nullptr;
     float *cur = nullptr;

@@ -661,7 +661,9 @@ int dispatch_ks(int ks, int pro, int epi, const mv_args &a, int g, hipStream_t s
 }  // namespace
 
 size_t matvec_lds_bytes(int wtype, int ks, int64_t n_bt, int64_t seg) {
-    return wtype == T_Q4_0 ? make_lds_map<T_Q4_0, true>(ks, n_bt, seg).total : make_lds_map<T_Q8_0, true>(ks, n_bt, seg).total;
+    const bool nsa = ks != 8;  // as launch_t
+    if (wtype == T_Q4_0) return nsa ? make_lds_map<T_Q4_0, true>(ks, n_bt, seg).total : make_lds_map<T_Q4_0, false>(ks, n_bt, seg).total;
+    return make_lds_map<T_Q8_0, true>(ks, n_bt, seg).total;
 }
 
 int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int grid_x, hipStream_t s) {

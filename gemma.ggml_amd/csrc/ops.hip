@@ -795,6 +795,27 @@ __global__ void k_exp_f16_all(uint16_t *out) {
     if (i < 65536) out[i] = (uint16_t)exp_f16_of((uint32_t)i);
 }
 
+// TP: this rank's per-workgroup keys -> one key whose index is global (local + row_base); the order
+// of keys is preserved (larger value first, then smaller global index), so the merged argmax is
+// the single-GPU one
+__global__ void __launch_bounds__(256) k_reduce_keys(const unsigned long long *keys, int n, int64_t row_base,
+                                                     unsigned long long *out) {
+    __shared__ unsigned long long red[4];
+    unsigned long long best = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) best = keys[i] > best ? keys[i] : best;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
+    const uint32_t local = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull);
+    *out = (best & 0xFFFFFFFF00000000ull) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)(local + row_base));
+}
+
 __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys, int n_parts, int *token, int *pos,
                                                  int *hist, int hist_cap, const int *n_fixed, rope_row r) {
     __shared__ unsigned long long red[4];
@@ -965,6 +986,12 @@ int launch_stream_read(const void *buf, size_t bytes, unsigned *sink, hipStream_
 
 int launch_exp_f16_all(uint16_t *out, hipStream_t s) {
     hipLaunchKernelGGL(k_exp_f16_all, dim3(256), dim3(256), 0, s, out);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_reduce_keys(const unsigned long long *keys, int n, int64_t row_base, unsigned long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_reduce_keys, dim3(1), dim3(256), 0, s, keys, n, row_base, out);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

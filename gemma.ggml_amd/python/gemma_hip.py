@@ -19,7 +19,8 @@ GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
 EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
            "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
            "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
-           "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_hbm_read_gbs"]
+           "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_hbm_read_gbs",
+           "gemma_tp_unique_id", "gemma_engine_create_tp"]
 
 
 def build():
@@ -69,6 +70,10 @@ def lib():
     L.gemma_engine_debug_step.argtypes = [vp, vp, vp]
     L.gemma_engine_stamp_step.restype = C.c_int
     L.gemma_engine_stamp_step.argtypes = [vp, C.c_int, vp]
+    L.gemma_tp_unique_id.restype = C.c_int
+    L.gemma_tp_unique_id.argtypes = [vp, C.c_int]
+    L.gemma_engine_create_tp.restype = vp
+    L.gemma_engine_create_tp.argtypes = [C.POINTER(GemmaConfig), C.c_int, C.c_int, C.c_int, vp]
     L.gemma_engine_create.restype = vp
     L.gemma_engine_create.argtypes = [C.POINTER(GemmaConfig), C.c_int]
     L.gemma_engine_free.argtypes = [vp]
@@ -130,11 +135,17 @@ def mul_mat(src0_bytes, src0_type, ne01, nb01, shared_edge, wdata, row_size, nco
 
 class Engine:
     def __init__(self, shape, n_ctx=512, wtype=GGML_TYPE_Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0,
-                 gelu_clamp=0, device=0):
+                 gelu_clamp=0, device=0, tp=None):
+        """tp = (n_ranks, rank, rccl_id_bytes) for the row-split engine (one process per GPU);
+        rccl_id_bytes None = all ranks' shards virtual in this engine (single-GPU parity mode)."""
         self.cfg = GemmaConfig(n_ctx=n_ctx, wtype=wtype, eps=eps, rope_base=rope_base, seed=seed,
                                gelu_clamp=gelu_clamp, **shape)
         self.L = lib()
-        self.h = self.L.gemma_engine_create(C.byref(self.cfg), device)
+        if tp is not None and tp[0] > 1:
+            idbuf = C.create_string_buffer(bytes(tp[2]), len(tp[2])) if tp[2] is not None else None
+            self.h = self.L.gemma_engine_create_tp(C.byref(self.cfg), device, tp[0], tp[1], idbuf)
+        else:
+            self.h = self.L.gemma_engine_create(C.byref(self.cfg), device)
         if not self.h:
             raise RuntimeError("gemma_engine_create failed: " + last_error())
 
@@ -195,3 +206,12 @@ class Engine:
         if us < 0:
             raise RuntimeError("time failed: " + last_error())
         return us, b.value
+
+
+def tp_unique_id():
+    """RCCL unique id for gemma_engine_create_tp (call on rank 0, broadcast the bytes)."""
+    buf = C.create_string_buffer(256)
+    n = lib().gemma_tp_unique_id(buf, 256)
+    if n <= 0:
+        raise RuntimeError("gemma_tp_unique_id failed: " + last_error())
+    return buf.raw[:n]

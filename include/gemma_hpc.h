@@ -55,6 +55,15 @@ typedef struct gemma_hip_config {
 typedef struct gemma_engine gemma_engine;
 
 gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int device);
+/* row-split tensor parallelism: one process per GPU; rank r holds rows
+ * [r*rows/n, (r+1)*rows/n) of every matrix and RCCL all-gathers complete each activation vector
+ * (4 per layer + one argmax key per rank), so logits are bit-identical to one GPU.
+ * gemma_tp_unique_id fills `out` (>= 128 B) on rank 0; every rank passes a copy to create_tp.
+ * nccl_id == NULL: all n_ranks shards in one engine on one GPU ("virtual ranks", same shards and
+ * key merge, shards written in place instead of gathered) for single-GPU parity tests. */
+int gemma_tp_unique_id(void *out, int cap);
+gemma_engine *gemma_engine_create_tp(const gemma_hip_config *cfg, int device, int n_ranks, int rank,
+                                     const void *nccl_id);
 void gemma_engine_free(gemma_engine *e);
 /* start a sequence: KV cache cleared, prompt stored on the device */
 int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_prompt);
