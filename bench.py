@@ -92,6 +92,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--prefill", type=int, default=2048, help="prefill leg prompt length (0 = skip)")
+    ap.add_argument("--no-tune", action="store_true", help="default launch plan instead of the measured one")
     ap.add_argument("--tp-steps", type=int, default=48, help="Gemma-7B row-split decode leg steps (0 = skip)")
     args = ap.parse_args()
 
@@ -116,6 +117,7 @@ def main():
             dist.barrier()
 
     eng = G.Engine(GEMMA_2B, n_ctx=args.ctx, wtype=wtype, device=local_rank)
+    plan = eng.tune(8) if not args.no_tune else eng.plan()  # engine setup (untimed): launch shapes
     prompt = make_prompt(args.prompt, GEMMA_2B["n_vocab"])
     eng.begin(prompt)
     # prompt pass on the ordered (bit-exact) per-token path; timed as the serial prefill figure
@@ -151,6 +153,7 @@ def main():
                 dist.broadcast(idt, 0)
                 rid = bytes(idt.numpy())
             te = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=(world, rank, rid))
+            tplan = te.tune(6) if not args.no_tune else te.plan()
             te.begin(make_prompt(16, GEMMA_7B["n_vocab"]))
             te.step(16 + 4, use_graph=True)
             barrier_sync()
@@ -166,7 +169,8 @@ def main():
             te.close()
             tp = {"model": "Gemma-7B " + args.wtype.upper(), "ranks": world, "tok_s": round(args.tp_steps / tdt, 2),
                   "ms_per_token": round(tdt / args.tp_steps * 1e3, 4), "steps": args.tp_steps,
-                  "parallelism": f"row-split tp{world} (RCCL all-gather x4/layer)" if world > 1 else "1 GPU"}
+                  "parallelism": f"row-split tp{world} (RCCL all-gather x4/layer)" if world > 1 else "1 GPU",
+                  "launch_plan": tplan}
         except Exception as ex:  # reported, never fatal to the headline line
             tp = {"error": str(ex)[:300]}
 
@@ -230,6 +234,7 @@ def main():
             "prefill_tok_s": prefill["tok_s"] if prefill else None,
             "prefill": prefill,
             "tp_decode": tp,
+            "launch_plan": {k: {"k_split": v[0], "rows_per_wg": v[1]} for k, v in plan.items()},
             "prefill_serial_tok_s": round(args.prompt / prefill_serial_s, 2),
             "roofline": {"bound": "hbm", "kernel": KERNEL_NAMES[dominant], "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

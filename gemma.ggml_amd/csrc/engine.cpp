@@ -146,6 +146,12 @@ struct layer_dev {
     tiled_mat qkv, o, gate, up, down;
 };
 
+// matrix classes of a decode step and their launch plan (K split, row-tile groups per workgroup)
+enum { MC_QKV = 0, MC_O, MC_GU, MC_DOWN, MC_LOGITS, MC_N };
+struct launch_plan {
+    int ks = 1, rpw = 1;
+};
+
 struct gemma_engine {
     gemma_hip_config cfg{};
     int device = 0;
@@ -177,9 +183,10 @@ struct gemma_engine {
     int host_pos = 0;  // mirror of *pos (steps are deterministic)
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
-    // launch geometry
+    // launch geometry: one plan per matrix class (defaults below; gemma_engine_tune measures)
     int ks_small = 4, ks_down = 8;
     int grid_big = 2048;
+    launch_plan plan[MC_N];
     // prefill scratch (lazily allocated)
     // prefill buffers (lazily sized for the prompt length)
     struct {
@@ -199,6 +206,16 @@ struct gemma_engine {
 static constexpr size_t kStampRegion = 4096 * 16;  // u64 per kernel: <= 4096 workgroups x 16 stamps
 static unsigned long long *stamp_region(gemma_engine *e, int il, int k) {
     return (e->stamp && il == e->stamp_layer) ? e->stamp + (size_t)k * kStampRegion : nullptr;
+}
+
+// workgroups of a matvec launch: a KS = 1 workgroup runs 4 waves on 4 row tiles at a time, a
+// KS > 1 workgroup its KS waves on one row tile; each workgroup repeats for rpw row-tile groups
+static int mv_grid(const gemma_engine *e, int cls, int64_t n_rt) {
+    const launch_plan &p = e->plan[cls];
+    const int64_t per = (p.ks == 1 ? 4 : 1) * (int64_t)std::max(p.rpw, 1);
+    int64_t g = (n_rt + per - 1) / per;
+    if (cls == MC_LOGITS || cls == MC_GU) g = std::min<int64_t>(g, e->grid_big);  // key slots
+    return (int)std::max<int64_t>(g, 1);
 }
 
 // largest power-of-two K split <= target that divides the block-tile count and whose LDS image
@@ -249,7 +266,7 @@ static int enqueue_step(gemma_engine *e) {
             }
             a.dbg_t = stamp_region(e, il, 0);
             a.y = e->qkv + (size_t)rank_of(e, vr) * e->sh_qkv;  // this rank's rows of q|k|v
-            if (launch_matvec(wt, pick_ks(wt, L.qkv.n_bt, e->ks_small), pro, EPI_STORE, a, (int)L.qkv.n_rt, s)) return -1;
+            if (launch_matvec(wt, pick_ks(wt, L.qkv.n_bt, e->plan[MC_QKV].ks), pro, EPI_STORE, a, mv_grid(e, MC_QKV, L.qkv.n_rt), s)) return -1;
         }
         if (tp_gather(e, e->qkv, e->sh_qkv)) return -1;
         // K2: rope + scale + kv store + KQ + softmax + KQV  (:698-718, :454-518); replicated
@@ -277,7 +294,7 @@ static int enqueue_step(gemma_engine *e) {
             b.qs = L.o.qs; b.sc = L.o.sc; b.rows = L.o.rows; b.n_rt = L.o.n_rt; b.n_bt = L.o.n_bt; b.nb = L.o.nb;
             b.x = e->attn; b.y = e->sa + r0; b.resid = e->x + r0;
             b.dbg_t = stamp_region(e, il, 2);
-            if (launch_matvec(wt, pick_ks(wt, L.o.n_bt, e->ks_small), PRO_F32, EPI_ADD, b, (int)L.o.n_rt, s)) return -1;
+            if (launch_matvec(wt, pick_ks(wt, L.o.n_bt, e->plan[MC_O].ks), PRO_F32, EPI_ADD, b, mv_grid(e, MC_O, L.o.n_rt), s)) return -1;
         }
         if (tp_gather(e, e->sa, e->sh_e)) return -1;
         // K4: rms_norm*ffn_norm + quantize -> gate & up -> gelu(gate)*up  (:724, :446-449)
@@ -289,8 +306,7 @@ static int enqueue_step(gemma_engine *e) {
             g.x = e->sa; g.norm_w = L.ffn_norm; g.eps = c.eps; g.y = e->h + (size_t)rank_of(e, vr) * e->sh_ff;
             g.gelu_tab = e->gelu_tab; g.gelu_clamp = c.gelu_clamp;
             g.dbg_t = stamp_region(e, il, 3);
-            if (launch_matvec(wt, 1, PRO_NORM, EPI_GELU_MUL, g, (int)std::min<int64_t>((L.gate.n_rt + 3) / 4, e->grid_big),
-                              s))
+            if (launch_matvec(wt, 1, PRO_NORM, EPI_GELU_MUL, g, mv_grid(e, MC_GU, L.gate.n_rt), s))
                 return -1;
         }
         if (tp_gather(e, e->h, e->sh_ff)) return -1;
@@ -303,7 +319,7 @@ static int enqueue_step(gemma_engine *e) {
             d.nb = L.down.nb;
             d.x = e->h; d.y = e->x + r0; d.resid = e->sa + r0;
             d.dbg_t = stamp_region(e, il, 4);
-            if (launch_matvec(wt, pick_ks(wt, L.down.n_bt, e->ks_down), PRO_F32, EPI_ADD, d, (int)L.down.n_rt, s)) return -1;
+            if (launch_matvec(wt, pick_ks(wt, L.down.n_bt, e->plan[MC_DOWN].ks), PRO_F32, EPI_ADD, d, mv_grid(e, MC_DOWN, L.down.n_rt), s)) return -1;
         }
         if (tp_gather(e, e->x, e->sh_e)) return -1;
         if (e->dbg)
@@ -323,7 +339,7 @@ static int enqueue_step(gemma_engine *e) {
         o.nb = out_rows.nb;
         o.x = e->x; o.norm_w = e->out_norm; o.eps = c.eps; o.y = e->logits + (size_t)rk * e->sh_v;
         o.argmax_key = e->key;
-        lg_grid = (int)std::min<int64_t>((out_rows.n_rt + 3) / 4, e->grid_big);
+        lg_grid = mv_grid(e, MC_LOGITS, out_rows.n_rt);
         o.dbg_t = e->stamp ? e->stamp + 5 * kStampRegion : nullptr;
         if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, lg_grid, s)) return -1;
         // TP: one key per rank, its index made global
@@ -472,6 +488,15 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         const ncclResult_t nr = ncclCommInitRank(&e->comm, tp_n, id, tp_rank);
         if (nr != ncclSuccess) set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
     }
+    {
+        // default launch plan (the shapes of every rank's shards are equal)
+        const layer_dev &L0 = e->layers[0];
+        e->plan[MC_QKV] = {pick_ks(wt, L0.qkv.n_bt, e->ks_small), 1};
+        e->plan[MC_O] = {pick_ks(wt, L0.o.n_bt, e->ks_small), 1};
+        e->plan[MC_GU] = {1, 1};
+        e->plan[MC_DOWN] = {pick_ks(wt, L0.down.n_bt, e->ks_down), 1};
+        e->plan[MC_LOGITS] = {1, 1};
+    }
     if (!last_error().empty()) {
         gemma_engine_free(e);
         return nullptr;
@@ -507,14 +532,15 @@ extern "C" gemma_engine *gemma_engine_create_tp(const gemma_hip_config *cfg, int
     return engine_create(cfg, device, n_ranks, nccl_id ? rank : 0, nccl_id);
 }
 
+static void drop_graph(gemma_engine *e);
+
 extern "C" void gemma_engine_free(gemma_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->rank_keys) (void)hipFree(e->rank_keys);
-    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
-    if (e->graph) (void)hipGraphDestroy(e->graph);
+    drop_graph(e);
     free_tiled(e->embd);
     for (size_t i = 0; i < e->layers.size(); ++i) {
         layer_dev &L = e->layers[i];
@@ -685,32 +711,32 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
             a.qs2 = L.up.qs; a.sc2 = L.up.sc;
             a.x = e->sa; a.norm_w = L.ffn_norm; a.eps = c.eps; a.y = e->h; a.gelu_tab = e->gelu_tab;
             pro = PRO_NORM; epi = EPI_GELU_MUL;
-            grid = (int)std::min<int64_t>((L.gate.n_rt + 3) / 4, e->grid_big);
+            grid = mv_grid(e, MC_GU, L.gate.n_rt);
             bytes = (double)L.gate.algo_bytes() + L.up.algo_bytes() + c.n_embd * 4.0 * 2 + c.n_ff * 4.0;
             break;
         case 1:
             set_mat(L.down);
-            a.x = e->h; a.y = e->x; a.resid = e->sa; ks = pick_ks(wt, L.down.n_bt, e->ks_down); epi = EPI_ADD;
-            grid = (int)L.down.n_rt;
+            a.x = e->h; a.y = e->x; a.resid = e->sa; ks = pick_ks(wt, L.down.n_bt, e->plan[MC_DOWN].ks); epi = EPI_ADD;
+            grid = mv_grid(e, MC_DOWN, L.down.n_rt);
             bytes = (double)L.down.algo_bytes() + c.n_ff * 4.0 + c.n_embd * 8.0;
             break;
         case 2:
             set_mat(L.qkv);
-            a.x = e->x; a.norm_w = L.attn_norm; a.eps = c.eps; a.y = e->qkv; ks = pick_ks(wt, L.qkv.n_bt, e->ks_small); pro = PRO_NORM;
-            grid = (int)L.qkv.n_rt;
+            a.x = e->x; a.norm_w = L.attn_norm; a.eps = c.eps; a.y = e->qkv; ks = pick_ks(wt, L.qkv.n_bt, e->plan[MC_QKV].ks); pro = PRO_NORM;
+            grid = mv_grid(e, MC_QKV, L.qkv.n_rt);
             bytes = (double)L.qkv.algo_bytes() + c.n_embd * 8.0 + e->qkv_rows * 4.0;
             break;
         case 3:
             set_mat(L.o);
-            a.x = e->attn; a.y = e->sa; a.resid = e->x; ks = pick_ks(wt, L.o.n_bt, e->ks_small); epi = EPI_ADD;
-            grid = (int)L.o.n_rt;
+            a.x = e->attn; a.y = e->sa; a.resid = e->x; ks = pick_ks(wt, L.o.n_bt, e->plan[MC_O].ks); epi = EPI_ADD;
+            grid = mv_grid(e, MC_O, L.o.n_rt);
             bytes = (double)L.o.algo_bytes() + e->qw * 4.0 + c.n_embd * 8.0;
             break;
         case 4:
             set_mat(e->embd);
             a.x = e->x; a.norm_w = e->out_norm; a.eps = c.eps; a.y = e->logits; a.argmax_key = e->key;
             pro = PRO_NORM; epi = EPI_ARGMAX;
-            grid = (int)std::min<int64_t>((e->embd.n_rt + 3) / 4, e->grid_big);
+            grid = mv_grid(e, MC_LOGITS, e->embd.n_rt);
             bytes = (double)e->embd.algo_bytes() + c.n_embd * 8.0 + c.n_vocab * 4.0;
             break;
         default:
@@ -760,6 +786,116 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
     (void)hipEventDestroy(t1);
     if (algo_bytes) *algo_bytes = bytes;
     return (double)ms * 1000.0 / iters;
+}
+
+// ---- launch-plan tuning -----------------------------------------------------------------------
+// Coordinate descent over the matrix classes: for each class every feasible (K split, row-tile
+// groups per workgroup) is timed as whole decode steps (hipGraph replays on a fresh context), the
+// other classes held at their current best.  Whole steps keep the cache state of real decoding
+// (a matrix timed alone would be served from the 256 MB Infinity Cache).  Every candidate computes
+// the same bits (the K split keeps the block order), so tuning changes speed only.  The decode
+// state is clobbered: call gemma_engine_begin afterwards.  In a TP job every rank runs the same
+// candidate sequence (same collectives per step); ranks may settle on different plans.
+static void drop_graph(gemma_engine *e) {
+    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
+    if (e->graph) (void)hipGraphDestroy(e->graph);
+    e->graph_exec = nullptr;
+    e->graph = nullptr;
+}
+
+extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    const gemma_hip_config &c = e->cfg;
+    const int wt = c.wtype;
+    const int32_t prompt[4] = {2, 2, 2, 2};
+    iters = std::max(2, std::min(iters, c.n_ctx - 12));
+    if (iters < 2 || c.n_ctx < 16) {
+        set_error("gemma_engine_tune: context too small");
+        return -1;
+    }
+    hipEvent_t t0, t1;
+    GHIP_CHECK(hipEventCreate(&t0));
+    GHIP_CHECK(hipEventCreate(&t1));
+    auto trial = [&]() -> double {
+        drop_graph(e);
+        if (gemma_engine_begin(e, prompt, 4)) return -1.0;
+        if (gemma_engine_step(e, 1, nullptr, 1)) return -1.0;  // eager step + capture
+        for (int i = 0; i < 2; ++i)
+            if (hipGraphLaunch(e->graph_exec, e->stream) != hipSuccess) return -1.0;
+        if (hipEventRecord(t0, e->stream) != hipSuccess) return -1.0;
+        for (int i = 0; i < iters; ++i)
+            if (hipGraphLaunch(e->graph_exec, e->stream) != hipSuccess) return -1.0;
+        if (hipEventRecord(t1, e->stream) != hipSuccess || hipEventSynchronize(t1) != hipSuccess) return -1.0;
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, t0, t1);
+        return (double)ms * 1000.0 / iters;
+    };
+    const layer_dev &L0 = e->layers[0];
+    const int64_t nbt[MC_N] = {L0.qkv.n_bt, L0.o.n_bt, L0.gate.n_bt, L0.down.n_bt, e->embd.n_bt};
+    int rc = 0;
+    double best = trial();
+    if (best < 0) rc = -1;
+    const int order[MC_N] = {MC_DOWN, MC_GU, MC_QKV, MC_O, MC_LOGITS};
+    for (int oi = 0; oi < MC_N && rc == 0; ++oi) {
+        const int cls = order[oi];
+        std::vector<launch_plan> cands;
+        const bool splits = cls == MC_QKV || cls == MC_O || cls == MC_DOWN;
+        for (int ks = 1; ks <= (splits ? 8 : 1); ks *= 2) {
+            if (pick_ks(wt, nbt[cls], ks) != ks) continue;  // not a divisor, or the LDS image overflows
+            const int rmax = cls == MC_LOGITS ? 16 : ks == 1 ? 2 : 4;
+            for (int rpw = 1; rpw <= rmax; rpw *= 2) cands.push_back({ks, rpw});
+        }
+        const launch_plan keep = e->plan[cls];
+        launch_plan win = keep;
+        for (const launch_plan &p : cands) {
+            if (p.ks == keep.ks && p.rpw == keep.rpw) continue;
+            e->plan[cls] = p;
+            const double t = trial();
+            if (t < 0) {
+                rc = -1;
+                break;
+            }
+            if (t < best) {
+                best = t;
+                win = p;
+            }
+        }
+        e->plan[cls] = win;
+    }
+    drop_graph(e);
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    e->host_pos = 0;
+    return rc;
+}
+
+// the current plan: out[2*cls] = K split, out[2*cls+1] = row-tile groups per workgroup
+// (classes qkv, o, gate/up, down, logits); returns the number of ints written
+extern "C" int gemma_engine_plan(gemma_engine *e, int *out, int cap) {
+    int n = 0;
+    for (int cls = 0; cls < MC_N && n + 2 <= cap; ++cls) {
+        out[n++] = e->plan[cls].ks;
+        out[n++] = e->plan[cls].rpw;
+    }
+    return n;
+}
+
+extern "C" int gemma_engine_set_plan(gemma_engine *e, const int *in, int n) {
+    const gemma_hip_config &c = e->cfg;
+    const layer_dev &L0 = e->layers[0];
+    const int64_t nbt[MC_N] = {L0.qkv.n_bt, L0.o.n_bt, L0.gate.n_bt, L0.down.n_bt, e->embd.n_bt};
+    for (int cls = 0; cls < MC_N && 2 * cls + 1 < n; ++cls) {
+        const int ks = in[2 * cls], rpw = in[2 * cls + 1];
+        const bool splits = cls == MC_QKV || cls == MC_O || cls == MC_DOWN;
+        if (ks < 1 || (!splits && ks != 1) || pick_ks(c.wtype, nbt[cls], ks) != ks || rpw < 1 || rpw > 64) {
+            set_error("gemma_engine_set_plan: infeasible plan");
+            return -1;
+        }
+        e->plan[cls] = {ks, rpw};
+    }
+    drop_graph(e);
+    return 0;
 }
 
 static int prefill_alloc(gemma_engine *e, int T) {

@@ -33,12 +33,14 @@ __device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) {
 // ns:  uint4 [nb_pad/4][8 lanes] = -8*sum(a) per (block, lane) (Q4_0 only, when NSA; otherwise
 //      recomputed with one more v_dot4 to save LDS)
 // da:  float [nb_pad] (fp32 of the fp16 activation scale)
-// stash (KS > 1): s float [64 lanes][SBP], d float [8 rows][SBP]; a lane's (or row's) segments
-//      1..KS-1 are contiguous, so the carry chain reads one linear run (SBP = (KS-1)*seg + 4 pad)
+// stash (KS > 1): s [64 lanes][SBP], d float [8 rows][SBPD]; a lane's (or row's) segments
+//      1..KS-1 are contiguous, so the carry chain reads one linear run (SBP = (KS-1)*seg + pad).
+//      s is int16 for Q4_0 (|sum of 4 (nib-8)*a| <= 4*8*127 = 4064: exact, half the LDS and half
+//      the carrier's reads) and fp32 for Q8_0 (|sum| up to 4*127*128 needs 17 bits)
 constexpr int STASH_PAD = 4;
 struct lds_map {
     size_t act, ns, da, stash_s, stash_d, red, total;
-    int sbp;
+    int sbp, sbpd;  // s stride in elements (int16 or float), d stride in floats
 };
 template <int WT, bool NSA>
 __host__ __device__ inline lds_map make_lds_map(int ks, int64_t n_bt, int64_t seg_tiles) {
@@ -52,11 +54,13 @@ __host__ __device__ inline lds_map make_lds_map(int ks, int64_t n_bt, int64_t se
     m.da = off;
     off += nb_pad * 4;
     off = (off + 15) & ~(size_t)15;
-    m.sbp = ks > 1 ? (int)((ks - 1) * seg_tiles * BT) + STASH_PAD : 0;
+    constexpr int SW = WT == T_Q4_0 ? 2 : 4;  // bytes per stashed s
+    m.sbp = ks > 1 ? (int)((ks - 1) * seg_tiles * BT) + STASH_PAD * 4 / SW : 0;
+    m.sbpd = ks > 1 ? (int)((ks - 1) * seg_tiles * BT) + STASH_PAD : 0;
     m.stash_s = off;
-    off += (size_t)64 * m.sbp * 4;
+    off += (size_t)64 * m.sbp * SW;
     m.stash_d = off;
-    off += (size_t)8 * m.sbp * 4;
+    off += (size_t)8 * m.sbpd * 4;
     m.red = off;
     off += 64 * 8;
     m.total = off;
@@ -274,7 +278,8 @@ __device__ __forceinline__ float mix_hi(uint32_t h2, float y) {
 // STASH: store the exact (d, (float)isum) terms for the carry instead of accumulating
 template <int WT, bool STASH, bool NSA>
 __device__ __forceinline__ float tile_dot(uint4 q, uint4 scv, const uint8_t *smem, const lds_map &m, int64_t bt, int l,
-                                          float acc, float *st_s, float *st_d, int j0) {
+                                          float acc, void *st_s_, float *st_d, int j0) {
+    float *st_s = (float *)st_s_;
     const float *da = (const float *)(smem + m.da);
     const uint4 *act = (const uint4 *)(smem + m.act);
     const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
@@ -290,6 +295,8 @@ __device__ __forceinline__ float tile_dot(uint4 q, uint4 scv, const uint8_t *sme
         const float4 DA0 = *(const float4 *)(da + bt * 8), DA1 = *(const float4 *)(da + bt * 8 + 4);
         const float dav[8] = {DA0.x, DA0.y, DA0.z, DA0.w, DA1.x, DA1.y, DA1.z, DA1.w};
         const uint32_t sv[4] = {scv.x, scv.y, scv.z, scv.w};
+        uint32_t pk[4];
+        float dk[8];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const uint32_t lo = qv[p] & 0x0F0F0F0Fu, hi = (qv[p] >> 4) & 0x0F0F0F0Fu;
@@ -301,11 +308,19 @@ __device__ __forceinline__ float tile_dot(uint4 q, uint4 scv, const uint8_t *sme
             const float d0 = mix_lo(sv[p], dav[2 * p]);
             const float d1 = mix_hi(sv[p], dav[2 * p + 1]);
             if (STASH) {
-                *(float2 *)(st_s + j0 + 2 * p) = make_float2((float)s0, (float)s1);
-                if (l == 0) *(float2 *)(st_d + j0 + 2 * p) = make_float2(d0, d1);
+                pk[p] = ((uint32_t)s0 & 0xFFFFu) | ((uint32_t)s1 << 16);
+                dk[2 * p] = d0;
+                dk[2 * p + 1] = d1;
             } else {
                 acc = __builtin_fmaf(d0, (float)s0, acc);
                 acc = __builtin_fmaf(d1, (float)s1, acc);
+            }
+        }
+        if (STASH) {
+            *(uint4 *)((int16_t *)st_s_ + j0) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            if (l == 0) {
+                *(float4 *)(st_d + j0) = make_float4(dk[0], dk[1], dk[2], dk[3]);
+                *(float4 *)(st_d + j0 + 4) = make_float4(dk[4], dk[5], dk[6], dk[7]);
             }
         }
     } else {
@@ -421,13 +436,149 @@ __device__ __forceinline__ float carry_run(const float4 *ps, const float4 *pd, i
     return acc;
 }
 
+// Q4_0 form: chunks of 8 blocks = one b128 of int16 sums + two b128 of d.  total % (2G) == 0; the
+// reloads are unconditional (a set is refilled in place right after its FMAs, so the register
+// allocator needs no copies and the waitcnt before a set's FMAs only covers that set).  The final
+// reloads run up to 2G chunks past the run: they stay inside the LDS image (the stash pads and the
+// regions behind it) and are never used.
+template <int G>
+__device__ __forceinline__ float carry_run16(const uint4 *ps, const float4 *pd, int total, float acc) {
+    uint4 as[G], bs[G];
+    float4 ad[G][2], bd[G][2];
+    auto load = [&](uint4 (&S)[G], float4 (&D)[G][2], int c0) {
+#pragma unroll
+        for (int r = 0; r < G; ++r) {
+            S[r] = ps[c0 + r];
+            D[r][0] = pd[2 * (c0 + r)];
+            D[r][1] = pd[2 * (c0 + r) + 1];
+        }
+    };
+    auto chain = [&](const uint4 (&S)[G], const float4 (&D)[G][2]) {
+#pragma unroll
+        for (int r = 0; r < G; ++r) {
+            const uint32_t w[4] = {S[r].x, S[r].y, S[r].z, S[r].w};
+            const float d[8] = {D[r][0].x, D[r][0].y, D[r][0].z, D[r][0].w,
+                                D[r][1].x, D[r][1].y, D[r][1].z, D[r][1].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                acc = __builtin_fmaf(d[2 * k], (float)(int)(int16_t)(w[k] & 0xFFFFu), acc);
+                acc = __builtin_fmaf(d[2 * k + 1], (float)((int)w[k] >> 16), acc);
+            }
+        }
+    };
+    load(as, ad, 0);
+    load(bs, bd, G);
+    for (int c = 0; c < total; c += 2 * G) {
+        asm volatile("" ::: "memory");
+        chain(as, ad);
+        asm volatile("" ::: "memory");
+        load(as, ad, c + 2 * G);
+        asm volatile("" ::: "memory");
+        chain(bs, bd);
+        asm volatile("" ::: "memory");
+        load(bs, bd, c + 3 * G);
+    }
+    return acc;
+}
+
+// Explicitly pipelined carry: NS = 4 chunk sets in flight.  Each set is refilled in place right
+// after its FMAs, and sched_barrier(0) pins every load group and FMA group where it is written, so
+// the scheduler can neither sink a refill next to its use nor hoist it above the FMAs that still
+// read the set (the compiler's own waitcnt insertion then waits, before a set's FMAs, only for that
+// set: LDS ops retire in order).  The ring over-reads up to NS chunks past the run (inside the LDS
+// image: stash pads, the d stash, the red area); those values are never used.
+template <bool I16>
+struct carry_set {
+    uint4 s;
+    float4 d0, d1;
+};
+template <bool I16>
+__device__ __forceinline__ void carry_load(carry_set<I16> &k, const uint4 *ps, const float4 *pd, int c) {
+    k.s = ps[c];
+    if (I16) {
+        k.d0 = pd[2 * c];
+        k.d1 = pd[2 * c + 1];
+    } else {
+        k.d0 = pd[c];
+    }
+}
+template <bool I16>
+__device__ __forceinline__ float carry_fma(const carry_set<I16> &k, float acc) {
+    if (I16) {
+        const float d[8] = {k.d0.x, k.d0.y, k.d0.z, k.d0.w, k.d1.x, k.d1.y, k.d1.z, k.d1.w};
+        const uint32_t w[4] = {k.s.x, k.s.y, k.s.z, k.s.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc = __builtin_fmaf(d[2 * j], (float)(int)(int16_t)(w[j] & 0xFFFFu), acc);
+            acc = __builtin_fmaf(d[2 * j + 1], (float)((int)w[j] >> 16), acc);
+        }
+    } else {
+        acc = __builtin_fmaf(k.d0.x, __builtin_bit_cast(float, k.s.x), acc);
+        acc = __builtin_fmaf(k.d0.y, __builtin_bit_cast(float, k.s.y), acc);
+        acc = __builtin_fmaf(k.d0.z, __builtin_bit_cast(float, k.s.z), acc);
+        acc = __builtin_fmaf(k.d0.w, __builtin_bit_cast(float, k.s.w), acc);
+    }
+    return acc;
+}
+
+// chunks [0, total) of the run; total % 4 == 0.  I16 (Q4_0): chunk = 8 blocks (s: 8 x int16 in one
+// uint4, d: two float4); else (Q8_0): 4 blocks (s: 4 x f32, d: one float4).
+template <bool I16>
+__device__ __forceinline__ float carry_ring(const uint4 *ps, const float4 *pd, int total, float acc) {
+    carry_set<I16> A, B, C, D;
+    carry_load<I16>(A, ps, pd, 0);
+    carry_load<I16>(B, ps, pd, 1);
+    carry_load<I16>(C, ps, pd, 2);
+    carry_load<I16>(D, ps, pd, 3);
+    for (int c = 0; c < total; c += 4) {
+        __builtin_amdgcn_sched_barrier(0);
+        acc = carry_fma<I16>(A, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        carry_load<I16>(A, ps, pd, c + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = carry_fma<I16>(B, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        carry_load<I16>(B, ps, pd, c + 5);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = carry_fma<I16>(C, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        carry_load<I16>(C, ps, pd, c + 6);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = carry_fma<I16>(D, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        carry_load<I16>(D, ps, pd, c + 7);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    return acc;
+}
+
 // gl = row * 8 + lane-of-row in the wave-0 numbering of the stash
-template <int KS>
-__device__ __forceinline__ float carry_chain(const float *st_s, const float *st_d, int sbp, int seg_blocks, int gl,
-                                             float acc) {
-    const float4 *ps = (const float4 *)(st_s + (size_t)gl * sbp);
-    const float4 *pd = (const float4 *)(st_d + (size_t)(gl >> 3) * sbp);
+template <int WT, int KS>
+__device__ __forceinline__ float carry_chain(const void *st_s, const float *st_d, const lds_map &m, int seg_blocks,
+                                             int gl, float acc) {
+    const float4 *pd = (const float4 *)(st_d + (size_t)(gl >> 3) * m.sbpd);
+    if (WT == T_Q4_0) {
+        const uint4 *ps = (const uint4 *)((const int16_t *)st_s + (size_t)gl * m.sbp);
+        const int total = (KS - 1) * (seg_blocks >> 3);  // chunks of 8 blocks
+        if (total % 4 == 0) return carry_ring<true>(ps, pd, total, acc);
+        if (total % 4 == 0) return carry_run16<2>(ps, pd, total, acc);
+        if (total % 2 == 0) return carry_run16<1>(ps, pd, total, acc);
+        // odd: the last chunk alone, after an even run
+        acc = total > 1 ? carry_run16<1>(ps, pd, total - 1, acc) : acc;
+        const uint4 S = ps[total - 1];
+        const float4 D0 = pd[2 * (total - 1)], D1 = pd[2 * (total - 1) + 1];
+        const uint32_t w[4] = {S.x, S.y, S.z, S.w};
+        const float d[8] = {D0.x, D0.y, D0.z, D0.w, D1.x, D1.y, D1.z, D1.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            acc = __builtin_fmaf(d[2 * k], (float)(int)(int16_t)(w[k] & 0xFFFFu), acc);
+            acc = __builtin_fmaf(d[2 * k + 1], (float)((int)w[k] >> 16), acc);
+        }
+        return acc;
+    }
+    const float4 *ps = (const float4 *)((const float *)st_s + (size_t)gl * m.sbp);
     const int total = (KS - 1) * (seg_blocks >> 2);  // chunks of 4 blocks
+    if (total % 4 == 0) return carry_ring<false>((const uint4 *)ps, pd, total, acc);
     // whole double-steps: no bounds test inside the dependent chain
     if (total % 8 == 0) return carry_run<4, true>(ps, pd, total, acc);
     if (total % 4 == 0) return carry_run<2, true>(ps, pd, total, acc);
@@ -510,9 +661,11 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
 
     // 3) stream
     const int seg_blocks = nbt * BT;
-    float *st_s = (float *)(smem + m.stash_s), *st_d = (float *)(smem + m.stash_d);
-    float *my_s = st_s + (size_t)lane * m.sbp + (size_t)(wave > 0 ? wave - 1 : 0) * nbt * BT;
-    float *my_d = st_d + (size_t)rr * m.sbp + (size_t)(wave > 0 ? wave - 1 : 0) * nbt * BT;
+    constexpr int SW = WT == T_Q4_0 ? 2 : 4;
+    uint8_t *st_s = smem + m.stash_s;
+    float *st_d = (float *)(smem + m.stash_d);
+    void *my_s = st_s + ((size_t)lane * m.sbp + (size_t)(wave > 0 ? wave - 1 : 0) * nbt * BT) * SW;
+    float *my_d = st_d + (size_t)rr * m.sbpd + (size_t)(wave > 0 ? wave - 1 : 0) * nbt * BT;
     unsigned long long best = 0;
     cursor cc{rt0, 0, 0};
     float acc = 0.0f, va = 0.0f;
@@ -556,7 +709,7 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
                             const int gl = wave * RPW * 8 + lane;
                             if (wave < NCAR && lane < RPW * 8) {
                                 float c = hand[gl];
-                                if (!(a.ablate & 4)) c = carry_chain<KS>(st_s, st_d, m.sbp, seg_blocks, gl, c);
+                                if (!(a.ablate & 4)) c = carry_chain<WT, KS>(st_s, st_d, m, seg_blocks, gl, c);
                                 if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 8] = __builtin_amdgcn_s_memrealtime();
                                 const float v = fold8(c);
                                 if ((lane & 7) == 0) epilogue<EPI>(a, col, cc.rt * 8 + (gl >> 3), v, 0.0f, best);

@@ -19,7 +19,8 @@ GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
 EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
            "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
            "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
-           "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_hbm_read_gbs",
+           "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
+           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_hbm_read_gbs",
            "gemma_tp_unique_id", "gemma_engine_create_tp"]
 
 
@@ -89,6 +90,9 @@ def lib():
     L.gemma_engine_prefill.argtypes = [vp, vp, vp]
     L.gemma_engine_tensor.restype = C.c_int64
     L.gemma_engine_tensor.argtypes = [vp, C.c_int, vp, i64]
+    L.gemma_engine_tune.argtypes = [vp, C.c_int]
+    L.gemma_engine_plan.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
+    L.gemma_engine_set_plan.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     L.gemma_engine_time.restype = C.c_double
     L.gemma_engine_time.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double)]
     L.gemma_hbm_read_gbs.restype = C.c_double
@@ -199,6 +203,27 @@ class Engine:
         out = np.zeros(6 * 4096 * 16, dtype=np.uint64)
         self._chk(self.L.gemma_engine_stamp_step(self.h, layer, _p(out)), "stamp_step")
         return out.reshape(6, 4096, 16)
+
+    PLAN_CLASSES = ("qkv", "attn_out", "gate_up", "down", "logits")
+
+    def tune(self, iters=8):
+        """measure the launch plan (clobbers the decode state: begin() afterwards); returns it"""
+        if self.L.gemma_engine_tune(self.h, iters) != 0:
+            raise RuntimeError("tune failed: " + last_error())
+        return self.plan()
+
+    def plan(self):
+        buf = (C.c_int * 10)()
+        n = self.L.gemma_engine_plan(self.h, buf, 10)
+        return {k: (buf[2 * i], buf[2 * i + 1]) for i, k in enumerate(self.PLAN_CLASSES[: n // 2])}
+
+    def set_plan(self, plan):
+        flat = []
+        for k in self.PLAN_CLASSES:
+            flat += list(plan[k])
+        arr = (C.c_int * len(flat))(*flat)
+        if self.L.gemma_engine_set_plan(self.h, arr, len(flat)) != 0:
+            raise RuntimeError("set_plan failed: " + last_error())
 
     def time_kernel(self, which, iters):
         b = C.c_double()

@@ -84,6 +84,13 @@ int64_t gemma_engine_tensor(gemma_engine *e, int tid, void *dst, int64_t cap);
  * 2 = qkv, 3 = attn out, 4 = output/logits, 5 = whole decode step (graph) */
 double gemma_engine_time(gemma_engine *e, int which, int iters, double *algo_bytes);
 int gemma_engine_sync(gemma_engine *e);
+/* launch plan per matrix class (0 qkv, 1 attn-out, 2 gate/up, 3 down, 4 logits): K split and
+ * row-tile groups per workgroup.  tune: coordinate descent over whole decode steps (hipGraph
+ * replays of `iters` tokens per candidate); bit-identical results for every plan; clobbers the
+ * decode state (call gemma_engine_begin afterwards).  plan/set_plan: 2 ints per class. */
+int gemma_engine_tune(gemma_engine *e, int iters);
+int gemma_engine_plan(gemma_engine *e, int *out, int cap);
+int gemma_engine_set_plan(gemma_engine *e, const int *in, int n);
 /* debugging: one eager step with per-layer taps [n_layer][qkv | attn_out | layer_out] */
 int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
 /* diagnostics: MFMA prefill with the residual stream after each layer -> [n_layer][T][n_embd] */

@@ -9,12 +9,19 @@ import numpy as np
 
 sys.path.insert(0, "gemma.ggml_amd/python")
 sys.path.insert(0, ".")
+import os
+
 import gemma_hip as G
-from bench import GEMMA_2B, make_prompt
+from bench import GEMMA_2B, GEMMA_7B, make_prompt
 
 layer = int(sys.argv[1]) if len(sys.argv) > 1 else 9
-e = G.Engine(GEMMA_2B, n_ctx=512, device=0)
-e.begin(make_prompt(128, GEMMA_2B["n_vocab"]))
+shape = GEMMA_7B if (len(sys.argv) > 2 and sys.argv[2] == "7b") else GEMMA_2B
+e = G.Engine(shape, n_ctx=512, device=0)
+if os.environ.get("PLAN"):  # qkv, o, gate/up, down, logits: ks,rpw pairs
+    v = [int(t) for t in os.environ["PLAN"].split(",")]
+    e.set_plan({k: (v[2 * i], v[2 * i + 1]) for i, k in enumerate(e.PLAN_CLASSES)})
+print("plan", e.plan())
+e.begin(make_prompt(128, shape["n_vocab"]))
 e.step(140, use_graph=True)
 names = ["qkv", "attention", "attn-out", "gate/up", "down", "logits"]
 phases = {0: ["issue", "prologue", "sync", "stream", "end", "own", "carry0", "fma", "store", "sync2"], 1: ["p1", "p2", "p3", "p4", "p5", "p6", "p7"]}  # attention: see AH_STAMP / ATT_STAMP

@@ -85,7 +85,7 @@ def _rand_f32(rng, *shape, scale=1.0):
 @pytest.mark.parametrize("ks", [1, 2, 4, 8])
 @pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
 @pytest.mark.parametrize("rows,k,ncols", [(8, 256, 1), (2048, 2048, 1), (256, 16384, 1), (40, 96, 3), (1000, 2048, 5),
-                                          (13, 64, 2)])
+                                          (13, 64, 2), (64, 24576, 1)])
 def test_mul_mat_quant_bitexact(wtype, rows, k, ncols, ks):
     import gemma_hip as G
     rng = np.random.default_rng(rows * 7 + k + ncols)
@@ -209,3 +209,31 @@ def test_row_split_virtual_ranks_gemma7b_layers():
     e.close()
     assert toks == list(seq_ref)
     assert np.array_equal(lg[len(prompt) - 1:].view(np.uint32), lg_ref.view(np.uint32))
+
+
+@gpu
+def test_tuned_plan_bitexact():
+    """gemma_engine_tune picks (K split, rows per workgroup) per matrix class by timing; every plan
+    must give the oracle's bits.  Also runs every split of the down class explicitly."""
+    shape = dict(O.TINY)
+    prompt = O.make_prompt(6, shape["n_vocab"])
+    m = O.Model(O.make_config(shape, n_ctx=128))
+    seq_ref, lg_ref = m.generate(prompt, 5)
+    e = _engine(shape, n_ctx=128)
+    plans = [e.tune(iters=4)]
+    base = dict(plans[0])
+    for ks in (1, 2, 4, 8):
+        for rpw in (1, 2):
+            p = dict(base, down=(ks, rpw), qkv=(ks if ks <= 4 else 4, rpw), attn_out=(min(ks, 2), 3 - rpw))
+            try:
+                e.set_plan(p)
+            except RuntimeError:
+                continue  # infeasible split for this shape
+            plans.append(p)
+    for p in plans:
+        e.set_plan(p)
+        e.begin(prompt)
+        lg = e.step(len(prompt) + 5, want_logits=True, use_graph=True)
+        assert list(e.tokens()[: len(seq_ref)]) == list(seq_ref), p
+        assert np.array_equal(lg[len(prompt) - 1:].view(np.uint32), lg_ref.view(np.uint32)), p
+    e.close()
