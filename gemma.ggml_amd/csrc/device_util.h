@@ -97,4 +97,36 @@ __device__ __forceinline__ uint32_t exp_f16_of(uint32_t x16) {
     return f2h(__expf(h2f(x16)));
 }
 
+// ---- Q8_0 activation image (DESIGN.md §Activation image) ----------------------------------------
+// The LDS layout the matvec streams against, also used in HBM between a producer kernel and its
+// consumer: act u32 [nb/4][8 lanes][4] — dword ((b>>2)*8 + l)*4 + (b&3) holds elements 4l..4l+3
+// of block b as int8; ns (optional, Q4_0) the same layout holding -8*sum of those 4; da f32 [nb].
+// quantize_row_q8_0: amax = max|v|, d = fp16(amax/127), id = amax ? 127/amax : 0,
+// q = rint(v*id).  A quad of threads (consecutive lanes q = 0..3, all active) owns one block;
+// thread q holds elements 8q..8q+7.
+__device__ __forceinline__ void image_put_quad(uint32_t *act, uint32_t *ns, float *da, int64_t b, int q,
+                                               const float v[8]) {
+    float amax = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    amax = fmaxf(amax, dpp_f<0xB1>(amax));  // quad xor 1
+    amax = fmaxf(amax, dpp_f<0x4E>(amax));  // quad xor 2
+    const float d = amax / 127.f;
+    const uint32_t d16 = f2h(d);
+    const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int l = 2 * q + h;
+        int qi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qi[k] = (int)__builtin_rintf(v[4 * h + k] * id);
+        const uint32_t packed = (uint32_t)(qi[0] & 0xFF) | ((uint32_t)(qi[1] & 0xFF) << 8) |
+                                ((uint32_t)(qi[2] & 0xFF) << 16) | ((uint32_t)(qi[3] & 0xFF) << 24);
+        const int64_t idx = ((b >> 2) * 8 + l) * 4 + (b & 3);
+        act[idx] = packed;
+        if (ns) ns[idx] = (uint32_t)(-8 * (qi[0] + qi[1] + qi[2] + qi[3]));
+    }
+    if (q == 0) da[b] = h2f(d16);
+}
+
 }  // namespace ghip

@@ -150,6 +150,7 @@ struct layer_dev {
 enum { MC_QKV = 0, MC_O, MC_GU, MC_DOWN, MC_LOGITS, MC_N };
 struct launch_plan {
     int ks = 1, rpw = 1;
+    int img = 0;  // attn-out / down: read the producer-written Q8_0 image (PRO_IMG) instead of f32
 };
 
 struct gemma_engine {
@@ -177,6 +178,10 @@ struct gemma_engine {
     float *rope_cos = nullptr, *rope_sin = nullptr, *rope_cur = nullptr;
     // activations
     float *x = nullptr, *qkv = nullptr, *attn = nullptr, *sa = nullptr, *h = nullptr, *logits = nullptr;
+    // Q8_0 activation images written by their producers (attention, gate/up) for attn-out and down
+    // (DESIGN.md §Activation image); null when a shape does not allow them (then PRO_F32)
+    uint32_t *att_act = nullptr, *h_act = nullptr;
+    float *att_da = nullptr, *h_da = nullptr;
     unsigned long long *key = nullptr;
     int *pos = nullptr, *token = nullptr, *hist = nullptr, *nfix = nullptr;
     int n_prompt = 0;
@@ -237,6 +242,23 @@ static int tp_gather(gemma_engine *e, float *full, int64_t cnt) {
     return 0;
 }
 
+// in-place all-gather of the h image: per rank `act_bytes` of act (u32 groups) and `nda` scales
+static int tp_gather_bytes(gemma_engine *e, uint32_t *act, int64_t act_bytes, float *da, int64_t nda) {
+    if (e->tp_n == 1 || !e->comm) return 0;
+    ncclGroupStart();
+    ncclResult_t r = ncclAllGather((uint8_t *)act + (size_t)e->tp_rank * act_bytes, act, (size_t)act_bytes, ncclUint8,
+                                   e->comm, e->stream);
+    const ncclResult_t r2 = ncclAllGather(da + (size_t)e->tp_rank * nda, da, (size_t)nda, ncclFloat, e->comm, e->stream);
+    const ncclResult_t r3 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r == ncclSuccess) r = r3;
+    if (r != ncclSuccess) {
+        set_error(std::string("ncclAllGather(image): ") + ncclGetErrorString(r));
+        return -1;
+    }
+    return 0;
+}
+
 // layer il's shards of (virtual) rank slot vr, and the rank that slot stands for
 static inline layer_dev &layer_of(gemma_engine *e, int il, int vr) { return e->layers[(size_t)il * e->n_virtual + vr]; }
 static inline int rank_of(const gemma_engine *e, int vr) { return e->n_virtual > 1 ? vr : e->tp_rank; }
@@ -276,6 +298,8 @@ static int enqueue_step(gemma_engine *e) {
         t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
         t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.rope_cur = e->rope_cur; t.exp_tab = e->exp_tab;
         t.pos = e->pos; t.out = e->attn;
+        const bool att_img = e->att_act && e->att_mode == ATTN_PER_HEAD && e->plan[MC_O].img;
+        if (att_img) { t.out_act = e->att_act; t.out_da = e->att_da; }
         t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
         t.q_scale = 1.0f / sqrtf((float)c.head_dim);
         t.mode = e->att_mode;
@@ -293,11 +317,15 @@ static int enqueue_step(gemma_engine *e) {
             mv_args b;
             b.qs = L.o.qs; b.sc = L.o.sc; b.rows = L.o.rows; b.n_rt = L.o.n_rt; b.n_bt = L.o.n_bt; b.nb = L.o.nb;
             b.x = e->attn; b.y = e->sa + r0; b.resid = e->x + r0;
+            if (att_img) { b.x = e->att_act; b.x_da = e->att_da; }
             b.dbg_t = stamp_region(e, il, 2);
-            if (launch_matvec(wt, pick_ks(wt, L.o.n_bt, e->plan[MC_O].ks), PRO_F32, EPI_ADD, b, mv_grid(e, MC_O, L.o.n_rt), s)) return -1;
+            if (launch_matvec(wt, pick_ks(wt, L.o.n_bt, e->plan[MC_O].ks), att_img ? PRO_IMG : PRO_F32, EPI_ADD, b,
+                              mv_grid(e, MC_O, L.o.n_rt), s))
+                return -1;
         }
         if (tp_gather(e, e->sa, e->sh_e)) return -1;
         // K4: rms_norm*ffn_norm + quantize -> gate & up -> gelu(gate)*up  (:724, :446-449)
+        const bool h_img = e->h_act && e->plan[MC_DOWN].img;
         for (int vr = 0; vr < e->n_virtual; ++vr) {
             layer_dev &L = layer_of(e, il, vr);
             mv_args g;
@@ -305,11 +333,20 @@ static int enqueue_step(gemma_engine *e) {
             g.rows = L.gate.rows; g.n_rt = L.gate.n_rt; g.n_bt = L.gate.n_bt; g.nb = L.gate.nb;
             g.x = e->sa; g.norm_w = L.ffn_norm; g.eps = c.eps; g.y = e->h + (size_t)rank_of(e, vr) * e->sh_ff;
             g.gelu_tab = e->gelu_tab; g.gelu_clamp = c.gelu_clamp;
+            if (h_img) {  // this rank's blocks of the image (shard offsets are whole 4-block groups)
+                const size_t b0 = (size_t)rank_of(e, vr) * e->sh_ff / 32;
+                g.out_act = e->h_act + b0 * 8;
+                g.out_da = e->h_da + b0;
+            }
             g.dbg_t = stamp_region(e, il, 3);
             if (launch_matvec(wt, 1, PRO_NORM, EPI_GELU_MUL, g, mv_grid(e, MC_GU, L.gate.n_rt), s))
                 return -1;
         }
-        if (tp_gather(e, e->h, e->sh_ff)) return -1;
+        if (h_img) {
+            if (tp_gather_bytes(e, e->h_act, e->sh_ff, e->h_da, e->sh_ff / 32)) return -1;
+        } else if (tp_gather(e, e->h, e->sh_ff)) {
+            return -1;
+        }
         // K5: quantize(h) -> Wdown, + sa  (:450, :731)
         for (int vr = 0; vr < e->n_virtual; ++vr) {
             layer_dev &L = layer_of(e, il, vr);
@@ -318,8 +355,11 @@ static int enqueue_step(gemma_engine *e) {
             d.qs = L.down.qs; d.sc = L.down.sc; d.rows = L.down.rows; d.n_rt = L.down.n_rt; d.n_bt = L.down.n_bt;
             d.nb = L.down.nb;
             d.x = e->h; d.y = e->x + r0; d.resid = e->sa + r0;
+            if (h_img) { d.x = e->h_act; d.x_da = e->h_da; }
             d.dbg_t = stamp_region(e, il, 4);
-            if (launch_matvec(wt, pick_ks(wt, L.down.n_bt, e->plan[MC_DOWN].ks), PRO_F32, EPI_ADD, d, mv_grid(e, MC_DOWN, L.down.n_rt), s)) return -1;
+            if (launch_matvec(wt, pick_ks(wt, L.down.n_bt, e->plan[MC_DOWN].ks), h_img ? PRO_IMG : PRO_F32, EPI_ADD, d,
+                              mv_grid(e, MC_DOWN, L.down.n_rt), s))
+                return -1;
         }
         if (tp_gather(e, e->x, e->sh_e)) return -1;
         if (e->dbg)
@@ -472,6 +512,14 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     GHIP_FATAL(hipMalloc(&e->attn, (size_t)e->qw * 4));
     GHIP_FATAL(hipMalloc(&e->sa, (size_t)c.n_embd * 4));
     GHIP_FATAL(hipMalloc(&e->h, (size_t)c.n_ff * 4));
+    if (e->qw % 128 == 0) {  // whole 4-block groups
+        GHIP_FATAL(hipMalloc(&e->att_act, (size_t)e->qw));
+        GHIP_FATAL(hipMalloc(&e->att_da, (size_t)e->qw / 32 * 4));
+    }
+    if (e->sh_ff % 128 == 0) {  // every rank's shard is whole 4-block groups
+        GHIP_FATAL(hipMalloc(&e->h_act, (size_t)c.n_ff));
+        GHIP_FATAL(hipMalloc(&e->h_da, (size_t)c.n_ff / 32 * 4));
+    }
     GHIP_FATAL(hipMalloc(&e->logits, (size_t)c.n_vocab * 4));
     GHIP_FATAL(hipMalloc(&e->key, (size_t)e->grid_big * 8));  // per-workgroup argmax keys
     GHIP_FATAL(hipMalloc(&e->pos, 4));
@@ -491,11 +539,11 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     {
         // default launch plan (the shapes of every rank's shards are equal)
         const layer_dev &L0 = e->layers[0];
-        e->plan[MC_QKV] = {pick_ks(wt, L0.qkv.n_bt, e->ks_small), 1};
-        e->plan[MC_O] = {pick_ks(wt, L0.o.n_bt, e->ks_small), 1};
-        e->plan[MC_GU] = {1, 1};
-        e->plan[MC_DOWN] = {pick_ks(wt, L0.down.n_bt, e->ks_down), 1};
-        e->plan[MC_LOGITS] = {1, 1};
+        e->plan[MC_QKV] = {pick_ks(wt, L0.qkv.n_bt, e->ks_small), 1, 0};
+        e->plan[MC_O] = {pick_ks(wt, L0.o.n_bt, e->ks_small), 1, 0};
+        e->plan[MC_GU] = {1, 1, 0};
+        e->plan[MC_DOWN] = {pick_ks(wt, L0.down.n_bt, e->ks_down), 1, 0};
+        e->plan[MC_LOGITS] = {1, 1, 0};
     }
     if (!last_error().empty()) {
         gemma_engine_free(e);
@@ -550,7 +598,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
             (void)hipFree(L.ffn_norm);
         }
     }
-    void *bufs[] = {e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
+    void *bufs[] = {e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
                     e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf.X, e->pf.SA, e->pf.QKV, e->pf.ATT, e->pf.G, e->pf.U,
                     e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.keys};
     for (void *p : bufs)
@@ -717,8 +765,9 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
         case 1:
             set_mat(L.down);
             a.x = e->h; a.y = e->x; a.resid = e->sa; ks = pick_ks(wt, L.down.n_bt, e->plan[MC_DOWN].ks); epi = EPI_ADD;
+            if (e->h_act && e->plan[MC_DOWN].img) { a.x = e->h_act; a.x_da = e->h_da; pro = PRO_IMG; }
             grid = mv_grid(e, MC_DOWN, L.down.n_rt);
-            bytes = (double)L.down.algo_bytes() + c.n_ff * 4.0 + c.n_embd * 8.0;
+            bytes = (double)L.down.algo_bytes() + c.n_ff * (e->h_act ? 36.0 / 32 : 4.0) + c.n_embd * 8.0;
             break;
         case 2:
             set_mat(L.qkv);
@@ -729,8 +778,9 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
         case 3:
             set_mat(L.o);
             a.x = e->attn; a.y = e->sa; a.resid = e->x; ks = pick_ks(wt, L.o.n_bt, e->plan[MC_O].ks); epi = EPI_ADD;
+            if (e->att_act && e->att_mode == ATTN_PER_HEAD && e->plan[MC_O].img) { a.x = e->att_act; a.x_da = e->att_da; pro = PRO_IMG; }
             grid = mv_grid(e, MC_O, L.o.n_rt);
-            bytes = (double)L.o.algo_bytes() + e->qw * 4.0 + c.n_embd * 8.0;
+            bytes = (double)L.o.algo_bytes() + e->qw * (pro == PRO_IMG ? 36.0 / 32 : 4.0) + c.n_embd * 8.0;
             break;
         case 4:
             set_mat(e->embd);
@@ -844,12 +894,12 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
         for (int ks = 1; ks <= (splits ? 8 : 1); ks *= 2) {
             if (pick_ks(wt, nbt[cls], ks) != ks) continue;  // not a divisor, or the LDS image overflows
             const int rmax = cls == MC_LOGITS ? 16 : ks == 1 ? 2 : 4;
-            for (int rpw = 1; rpw <= rmax; rpw *= 2) cands.push_back({ks, rpw});
+            for (int rpw = 1; rpw <= rmax; rpw *= 2) cands.push_back({ks, rpw, e->plan[cls].img});
         }
         const launch_plan keep = e->plan[cls];
         launch_plan win = keep;
         for (const launch_plan &p : cands) {
-            if (p.ks == keep.ks && p.rpw == keep.rpw) continue;
+            if (p.ks == keep.ks && p.rpw == keep.rpw && p.img == keep.img) continue;
             e->plan[cls] = p;
             const double t = trial();
             if (t < 0) {
@@ -862,6 +912,15 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
             }
         }
         e->plan[cls] = win;
+        // the producer-written activation image, at the winning launch shape
+        const bool img_ok = (cls == MC_O && e->att_act && e->att_mode == ATTN_PER_HEAD) || (cls == MC_DOWN && e->h_act);
+        if (img_ok && rc == 0) {
+            e->plan[cls].img ^= 1;
+            const double t = trial();
+            if (t < 0) rc = -1;
+            if (t >= 0 && t < best) best = t;
+            else e->plan[cls].img ^= 1;
+        }
     }
     drop_graph(e);
     (void)hipEventDestroy(t0);
@@ -870,13 +929,14 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
     return rc;
 }
 
-// the current plan: out[2*cls] = K split, out[2*cls+1] = row-tile groups per workgroup
-// (classes qkv, o, gate/up, down, logits); returns the number of ints written
+// the current plan, 3 ints per class (qkv, o, gate/up, down, logits): K split, row-tile groups per
+// workgroup, activation image (o, down); returns the number of ints written
 extern "C" int gemma_engine_plan(gemma_engine *e, int *out, int cap) {
     int n = 0;
-    for (int cls = 0; cls < MC_N && n + 2 <= cap; ++cls) {
+    for (int cls = 0; cls < MC_N && n + 3 <= cap; ++cls) {
         out[n++] = e->plan[cls].ks;
         out[n++] = e->plan[cls].rpw;
+        out[n++] = e->plan[cls].img;
     }
     return n;
 }
@@ -885,14 +945,16 @@ extern "C" int gemma_engine_set_plan(gemma_engine *e, const int *in, int n) {
     const gemma_hip_config &c = e->cfg;
     const layer_dev &L0 = e->layers[0];
     const int64_t nbt[MC_N] = {L0.qkv.n_bt, L0.o.n_bt, L0.gate.n_bt, L0.down.n_bt, e->embd.n_bt};
-    for (int cls = 0; cls < MC_N && 2 * cls + 1 < n; ++cls) {
-        const int ks = in[2 * cls], rpw = in[2 * cls + 1];
+    for (int cls = 0; cls < MC_N && 3 * cls + 2 < n; ++cls) {
+        const int ks = in[3 * cls], rpw = in[3 * cls + 1], img = in[3 * cls + 2];
         const bool splits = cls == MC_QKV || cls == MC_O || cls == MC_DOWN;
-        if (ks < 1 || (!splits && ks != 1) || pick_ks(c.wtype, nbt[cls], ks) != ks || rpw < 1 || rpw > 64) {
+        const bool img_ok = (cls == MC_O && e->att_act) || (cls == MC_DOWN && e->h_act);
+        if (ks < 1 || (!splits && ks != 1) || pick_ks(c.wtype, nbt[cls], ks) != ks || rpw < 1 || rpw > 64 ||
+            (img && !img_ok)) {
             set_error("gemma_engine_set_plan: infeasible plan");
             return -1;
         }
-        e->plan[cls] = {ks, rpw};
+        e->plan[cls] = {ks, rpw, img ? 1 : 0};
     }
     drop_graph(e);
     return 0;

@@ -12,6 +12,8 @@ enum mv_pro : int {
     PRO_NORM = 1,   // x: f32[K] -> rms_norm(x)*norm_w (A.5) -> quantize
     PRO_Q8 = 2,     // x: ggml block_q8_0[K/32] (the C-ABI `wdata`, already converted by ggml INIT)
     PRO_EMBED = 3,  // x: int32 sequence, token = x[*tok_pos]; embedding row (tiled) * emb_scale -> norm
+    PRO_IMG = 4,    // x: the Q8_0 activation image its producer already wrote (act u32 [nb/4][8][4]
+                    //    + x_da f32 [nb]; DESIGN.md §Activation image): a copy into LDS
 };
 enum mv_epi : int {
     EPI_STORE = 0,     // y[r] = dot
@@ -25,6 +27,7 @@ struct mv_args {
     const uint8_t *qs2 = nullptr, *sc2 = nullptr;  // second matrix for EPI_GELU_MUL (ffn_up)
     int64_t rows = 0, n_rt = 0, n_bt = 0, nb = 0;  // nb = K/32
     const void *x = nullptr;                       // activation (see mv_pro)
+    const float *x_da = nullptr;                   // PRO_IMG: the image's block scales
     int64_t x_col_stride = 0;                      // bytes between columns (multi-column launch)
     const float *norm_w = nullptr;
     float eps = 0.f;
@@ -41,6 +44,8 @@ struct mv_args {
     const uint16_t *gelu_tab = nullptr;
     int gelu_clamp = 0;
     unsigned long long *argmax_key = nullptr;      // EPI_ARGMAX: one partial key per workgroup [grid]
+    uint32_t *out_act = nullptr;                   // EPI_GELU_MUL: also write y's Q8_0 image (the
+    float *out_da = nullptr;                       //   next matvec's PRO_IMG input), blocks of y
     int ncols = 1;
     int ablate = 0;  // timing-only ablations (bench): 1 = no prologue, 4 = no carry
     unsigned long long *dbg_t = nullptr;  // diagnostics: 8 s_memrealtime stamps per workgroup
@@ -123,6 +128,8 @@ struct attn_args {
     const uint16_t *exp_tab;
     const int *pos;         // device scalar (position of this token)
     float *out;             // [H*hd]
+    uint32_t *out_act = nullptr;  // per-head mode: also out's Q8_0 image (attn-out's PRO_IMG input)
+    float *out_da = nullptr;
     int H, Hkv, hd, ctx;
     float q_scale;
     float *dbg_w = nullptr;      // optional debug taps: [H][ctx] scores, [H][ctx] fp16 P, [H] inv

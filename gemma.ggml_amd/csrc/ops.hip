@@ -764,7 +764,22 @@ __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
             f16_step8(acc, xv, *(const uint4 *)(P16 + e0));
         }
         const float o = quad_reduce_f16(acc);
-        if (t4 == 0) a.out[(int64_t)h * hd + d] = o;
+        if (t4 == 0) {
+            a.out[(int64_t)h * hd + d] = o;
+            if (a.out_act) ((float *)smem)[d] = o;  // q16|k16 (hd floats) are dead after KQ
+        }
+    }
+    if (a.out_act) {
+        // this head's hd/32 blocks of the Q8_0 activation image of `out` (attn-out's PRO_IMG input;
+        // the same quantize_row_q8_0 the consumer would run, DESIGN.md §Activation image)
+        __syncthreads();
+        if (tid < hd / 8) {
+            const float *o = (const float *)smem + (tid >> 2) * 32 + (tid & 3) * 8;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = o[j];
+            image_put_quad(a.out_act, nullptr, a.out_da, (int64_t)h * (hd / 32) + (tid >> 2), tid & 3, v);
+        }
     }
     AH_STAMP(4);
 }

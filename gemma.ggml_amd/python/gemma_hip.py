@@ -213,14 +213,16 @@ class Engine:
         return self.plan()
 
     def plan(self):
-        buf = (C.c_int * 10)()
-        n = self.L.gemma_engine_plan(self.h, buf, 10)
-        return {k: (buf[2 * i], buf[2 * i + 1]) for i, k in enumerate(self.PLAN_CLASSES[: n // 2])}
+        """{class: (k_split, rows_per_wg, image)}"""
+        buf = (C.c_int * 15)()
+        n = self.L.gemma_engine_plan(self.h, buf, 15)
+        return {k: (buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i, k in enumerate(self.PLAN_CLASSES[: n // 3])}
 
     def set_plan(self, plan):
         flat = []
         for k in self.PLAN_CLASSES:
-            flat += list(plan[k])
+            v = list(plan[k])
+            flat += v + [0] * (3 - len(v))
         arr = (C.c_int * len(flat))(*flat)
         if self.L.gemma_engine_set_plan(self.h, arr, len(flat)) != 0:
             raise RuntimeError("set_plan failed: " + last_error())

@@ -11,9 +11,9 @@ name = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 tpv = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 e = G.Engine(SHAPES[name], n_ctx=256, device=0, tp=(tpv, 0, None) if tpv > 1 else None)
-if os.environ.get("PLAN"):  # e.g. PLAN=1,1,8,1,1,1,8,2,1,16 (qkv, o, gate/up, down, logits: ks,rpw)
+if os.environ.get("PLAN"):  # e.g. PLAN=1,1,0,4,1,0,1,1,0,8,2,0,1,16,0 (qkv, o, gate/up, down, logits: ks,rpw,img)
     v = [int(t) for t in os.environ["PLAN"].split(",")]
-    e.set_plan({k: (v[2 * i], v[2 * i + 1]) for i, k in enumerate(e.PLAN_CLASSES)})
+    e.set_plan({k: (v[3 * i], v[3 * i + 1], v[3 * i + 2]) for i, k in enumerate(e.PLAN_CLASSES)})
 elif os.environ.get("TUNE", "1") == "1":  # (tuning under rocprofv3 crashes the profiler: pass PLAN)
     print("plan", e.tune(6))
 print("plan", e.plan())

@@ -17,9 +17,9 @@ from bench import GEMMA_2B, GEMMA_7B, make_prompt
 layer = int(sys.argv[1]) if len(sys.argv) > 1 else 9
 shape = GEMMA_7B if (len(sys.argv) > 2 and sys.argv[2] == "7b") else GEMMA_2B
 e = G.Engine(shape, n_ctx=512, device=0)
-if os.environ.get("PLAN"):  # qkv, o, gate/up, down, logits: ks,rpw pairs
+if os.environ.get("PLAN"):  # qkv, o, gate/up, down, logits: ks,rpw,img triples
     v = [int(t) for t in os.environ["PLAN"].split(",")]
-    e.set_plan({k: (v[2 * i], v[2 * i + 1]) for i, k in enumerate(e.PLAN_CLASSES)})
+    e.set_plan({k: (v[3 * i], v[3 * i + 1], v[3 * i + 2]) for i, k in enumerate(e.PLAN_CLASSES)})
 print("plan", e.plan())
 e.begin(make_prompt(128, shape["n_vocab"]))
 e.step(140, use_graph=True)

@@ -213,8 +213,9 @@ def test_row_split_virtual_ranks_gemma7b_layers():
 
 @gpu
 def test_tuned_plan_bitexact():
-    """gemma_engine_tune picks (K split, rows per workgroup) per matrix class by timing; every plan
-    must give the oracle's bits.  Also runs every split of the down class explicitly."""
+    """gemma_engine_tune picks (K split, rows per workgroup, activation image) per matrix class by
+    timing; every plan must give the oracle's bits.  Also sweeps the down/attn-out splits and both
+    image settings (f32 prologue vs the producer-written Q8_0 image) explicitly."""
     shape = dict(O.TINY)
     prompt = O.make_prompt(6, shape["n_vocab"])
     m = O.Model(O.make_config(shape, n_ctx=128))
@@ -224,7 +225,8 @@ def test_tuned_plan_bitexact():
     base = dict(plans[0])
     for ks in (1, 2, 4, 8):
         for rpw in (1, 2):
-            p = dict(base, down=(ks, rpw), qkv=(ks if ks <= 4 else 4, rpw), attn_out=(min(ks, 2), 3 - rpw))
+            img = (ks + rpw) % 2  # both image settings of attn-out and down across the sweep
+            p = dict(base, down=(ks, rpw, img), qkv=(ks if ks <= 4 else 4, rpw, 0), attn_out=(min(ks, 2), 3 - rpw, 1 - img))
             try:
                 e.set_plan(p)
             except RuntimeError:
