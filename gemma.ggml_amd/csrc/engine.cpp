@@ -799,6 +799,7 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
     }
     setup(e->layers[0]);
     (void)act_q8;
+    const bool hot = getenv("GHIP_TIME_HOT") != nullptr;
     if (const char *v = getenv("GHIP_ABLATE")) a.ablate = atoi(v);
     hipEvent_t t0, t1;
     GHIP_FATAL(hipEventCreate(&t0));
@@ -811,7 +812,7 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
         }
         if (which < 4) {
             setup(e->layers[layer]);
-            layer = (layer + 1) % c.n_layer;
+            if (!hot) layer = (layer + 1) % c.n_layer;  // hot: the same matrix (Infinity-Cache resident)
         }
         return launch_matvec(wt, ks, pro, epi, a, grid, e->stream);
     };

@@ -305,6 +305,71 @@ __device__ __forceinline__ float mix_hi(uint32_t h2, float y) {
     return d;
 }
 
+// One block tile's activation operands (LDS), loaded once and applied to every weight tile of
+// that block tile the wave holds (gate and up of EPI_GELU_MUL): each ds_read_b128 moves 1 KiB
+// through the LDS pipe even when broadcast, so sharing the operands halves the LDS traffic.
+template <int WT> struct act_tile;
+template <> struct act_tile<T_Q4_0> { uint32_t av[8], nv[8]; float dav[8]; };
+template <> struct act_tile<T_Q8_0> { uint32_t av[4]; float dav[4]; };
+
+template <int WT, bool NSA>
+__device__ __forceinline__ act_tile<WT> load_act(const uint8_t *smem, const lds_map &m, int64_t bt, int l) {
+    act_tile<WT> t;
+    const float *da = (const float *)(smem + m.da);
+    const uint4 *act = (const uint4 *)(smem + m.act);
+    if constexpr (WT == T_Q4_0) {
+        const uint4 A0 = act[(bt * 2) * 8 + l], A1 = act[(bt * 2 + 1) * 8 + l];
+        t.av[0] = A0.x; t.av[1] = A0.y; t.av[2] = A0.z; t.av[3] = A0.w;
+        t.av[4] = A1.x; t.av[5] = A1.y; t.av[6] = A1.z; t.av[7] = A1.w;
+        if (NSA) {
+            const uint4 *ns = (const uint4 *)(smem + m.ns);
+            const uint4 N0 = ns[(bt * 2) * 8 + l], N1 = ns[(bt * 2 + 1) * 8 + l];
+            t.nv[0] = N0.x; t.nv[1] = N0.y; t.nv[2] = N0.z; t.nv[3] = N0.w;
+            t.nv[4] = N1.x; t.nv[5] = N1.y; t.nv[6] = N1.z; t.nv[7] = N1.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) t.nv[j] = (uint32_t)sdot4(t.av[j], 0xF8F8F8F8u, 0);
+        }
+        const float4 DA0 = *(const float4 *)(da + bt * 8), DA1 = *(const float4 *)(da + bt * 8 + 4);
+        t.dav[0] = DA0.x; t.dav[1] = DA0.y; t.dav[2] = DA0.z; t.dav[3] = DA0.w;
+        t.dav[4] = DA1.x; t.dav[5] = DA1.y; t.dav[6] = DA1.z; t.dav[7] = DA1.w;
+    } else {
+        const uint4 A = act[bt * 8 + l];
+        t.av[0] = A.x; t.av[1] = A.y; t.av[2] = A.z; t.av[3] = A.w;
+        const float4 DA = *(const float4 *)(da + bt * 4);
+        t.dav[0] = DA.x; t.dav[1] = DA.y; t.dav[2] = DA.z; t.dav[3] = DA.w;
+    }
+    return t;
+}
+
+// the same arithmetic as tile_dot<WT, false, NSA>, on preloaded operands
+template <int WT>
+__device__ __forceinline__ float tile_dot_a(uint4 q, uint4 scv, const act_tile<WT> &t, float acc) {
+    const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+    if constexpr (WT == T_Q4_0) {
+        const uint32_t sv[4] = {scv.x, scv.y, scv.z, scv.w};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const uint32_t lo = qv[p] & 0x0F0F0F0Fu, hi = (qv[p] >> 4) & 0x0F0F0F0Fu;
+            const int s0 = sdot4(lo, t.av[2 * p], (int)t.nv[2 * p]);
+            const int s1 = sdot4(hi, t.av[2 * p + 1], (int)t.nv[2 * p + 1]);
+            const float d0 = mix_lo(sv[p], t.dav[2 * p]);
+            const float d1 = mix_hi(sv[p], t.dav[2 * p + 1]);
+            acc = __builtin_fmaf(d0, (float)s0, acc);
+            acc = __builtin_fmaf(d1, (float)s1, acc);
+        }
+    } else {
+        const uint32_t sv[2] = {scv.x, scv.y};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int s = sdot4(qv[p], t.av[p], 0);
+            const float d = (p & 1) ? mix_hi(sv[p >> 1], t.dav[p]) : mix_lo(sv[p >> 1], t.dav[p]);
+            acc = __builtin_fmaf(d, (float)s, acc);
+        }
+    }
+    return acc;
+}
+
 // STASH: store the exact (d, (float)isum) terms for the carry instead of accumulating
 template <int WT, bool STASH, bool NSA>
 __device__ __forceinline__ float tile_dot(uint4 q, uint4 scv, const uint8_t *smem, const lds_map &m, int64_t bt, int l,
@@ -674,7 +739,15 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
         }
         ++issued;
         if (issued < n_items) {
-            if (++ic.bt == nbt) {
+            if (NM == 2) {  // gate and up of one block tile back to back (shared act operands)
+                if (++ic.m == 2) {
+                    ic.m = 0;
+                    if (++ic.bt == nbt) {
+                        ic.bt = 0;
+                        ic.rt += rstride;
+                    }
+                }
+            } else if (++ic.bt == nbt) {
                 ic.bt = 0;
                 if (++ic.m == NM) {
                     ic.m = 0;
@@ -705,6 +778,38 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     cursor cc{rt0, 0, 0};
     float acc = 0.0f, va = 0.0f;
     const int64_t n_pad = ONE_SHOT ? U : (n_items + U - 1) / U * U;
+    if constexpr (NM == 2) {
+        // (gate, up) item pairs of the same block tile; two ordered chains (acc: gate, acc2: up)
+        static_assert(KS == 1 && U % 2 == 0, "gate/up pairing");
+        float acc2 = 0.0f;
+        for (int64_t k = 0; k < n_pad; k += U) {
+#pragma unroll
+            for (int u = 0; u < U; u += 2) {
+                const uint4 q0 = qb[u], s0 = sb[u], q1 = qb[u + 1], s1 = sb[u + 1];
+                issue(qb[u], sb[u]);
+                issue(qb[u + 1], sb[u + 1]);
+                if (k + u < n_items) {
+                    const act_tile<WT> at = load_act<WT, NSA>(smem, m, cc.bt, l);
+                    acc = tile_dot_a<WT>(q0, s0, at, acc);
+                    acc2 = tile_dot_a<WT>(q1, s1, at, acc2);
+                    if (cc.bt + 1 == nbt) {
+                        const float vg = fold8(acc), vu = fold8(acc2);
+                        acc = 0.0f;
+                        acc2 = 0.0f;
+                        if ((lane & 7) == 0) {
+                            epilogue<EPI>(a, col, cc.rt * 8 + rr, vg, vu, best);
+                            if (yimg) ((float *)(smem + m.ybuf))[y_it * 32 + wave * 8 + rr] = gelu_tab(a, vg) * vu;
+                        }
+                        ++y_it;
+                        cc.bt = 0;
+                        cc.rt += rstride;
+                    } else {
+                        ++cc.bt;
+                    }
+                }
+            }
+        }
+    } else
     for (int64_t k = 0; k < n_pad; k += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
