@@ -234,7 +234,8 @@ def main():
             "prefill_tok_s": prefill["tok_s"] if prefill else None,
             "prefill": prefill,
             "tp_decode": tp,
-            "launch_plan": {k: {"k_split": v[0], "rows_per_wg": v[1], "image": v[2]} for k, v in plan.items()},
+            "launch_plan": {k: ({"k_split": v[0], "rows_per_wg": v[1], "image": v[2]} if isinstance(v, tuple) else
+                                ("split" if v else "per_head")) for k, v in plan.items()},
             "prefill_serial_tok_s": round(args.prompt / prefill_serial_s, 2),
             "roofline": {"bound": "hbm", "kernel": KERNEL_NAMES[dominant], "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

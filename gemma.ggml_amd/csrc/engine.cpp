@@ -146,6 +146,9 @@ struct layer_dev {
     tiled_mat qkv, o, gate, up, down;
 };
 
+struct gemma_engine;
+static bool att_img_ok(const gemma_engine *e);
+
 // matrix classes of a decode step and their launch plan (K split, row-tile groups per workgroup)
 enum { MC_QKV = 0, MC_O, MC_GU, MC_DOWN, MC_LOGITS, MC_N };
 struct launch_plan {
@@ -212,6 +215,9 @@ static constexpr size_t kStampRegion = 4096 * 16;  // u64 per kernel: <= 4096 wo
 static unsigned long long *stamp_region(gemma_engine *e, int il, int k) {
     return (e->stamp && il == e->stamp_layer) ? e->stamp + (size_t)k * kStampRegion : nullptr;
 }
+
+// attention can hand attn-out the Q8_0 image of its output (per-head form; split form with 32-dim slices)
+static bool att_img_ok(const gemma_engine *e) { return e->att_mode == ATTN_PER_HEAD || e->ag.img; }
 
 // workgroups of a matvec launch: a KS = 1 workgroup runs 4 waves on 4 row tiles at a time, a
 // KS > 1 workgroup its KS waves on one row tile; each workgroup repeats for rpw row-tile groups
@@ -298,7 +304,7 @@ static int enqueue_step(gemma_engine *e) {
         t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
         t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.rope_cur = e->rope_cur; t.exp_tab = e->exp_tab;
         t.pos = e->pos; t.out = e->attn;
-        const bool att_img = e->att_act && e->att_mode == ATTN_PER_HEAD && e->plan[MC_O].img;
+        const bool att_img = e->att_act && att_img_ok(e) && e->plan[MC_O].img;
         if (att_img) { t.out_act = e->att_act; t.out_da = e->att_da; }
         t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
         t.q_scale = 1.0f / sqrtf((float)c.head_dim);
@@ -778,7 +784,7 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
         case 3:
             set_mat(L.o);
             a.x = e->attn; a.y = e->sa; a.resid = e->x; ks = pick_ks(wt, L.o.n_bt, e->plan[MC_O].ks); epi = EPI_ADD;
-            if (e->att_act && e->att_mode == ATTN_PER_HEAD && e->plan[MC_O].img) { a.x = e->att_act; a.x_da = e->att_da; pro = PRO_IMG; }
+            if (e->att_act && att_img_ok(e) && e->plan[MC_O].img) { a.x = e->att_act; a.x_da = e->att_da; pro = PRO_IMG; }
             grid = mv_grid(e, MC_O, L.o.n_rt);
             bytes = (double)L.o.algo_bytes() + e->qw * (pro == PRO_IMG ? 36.0 / 32 : 4.0) + c.n_embd * 8.0;
             break;
@@ -913,8 +919,16 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
             }
         }
         e->plan[cls] = win;
+        if (cls == MC_O && rc == 0 && e->ag.nwg && e->cfg.n_ctx <= 2048 && e->cfg.head_dim <= 256) {
+            // attention form (feeds attn-out): one workgroup per head vs the XCD-colocated split
+            e->att_mode ^= 1;
+            const double t = trial();
+            if (t < 0) rc = -1;
+            if (t >= 0 && t < best) best = t;
+            else e->att_mode ^= 1;
+        }
         // the producer-written activation image, at the winning launch shape
-        const bool img_ok = (cls == MC_O && e->att_act && e->att_mode == ATTN_PER_HEAD) || (cls == MC_DOWN && e->h_act);
+        const bool img_ok = (cls == MC_O && e->att_act && att_img_ok(e)) || (cls == MC_DOWN && e->h_act);
         if (img_ok && rc == 0) {
             e->plan[cls].img ^= 1;
             const double t = trial();
@@ -939,6 +953,7 @@ extern "C" int gemma_engine_plan(gemma_engine *e, int *out, int cap) {
         out[n++] = e->plan[cls].rpw;
         out[n++] = e->plan[cls].img;
     }
+    if (n < cap) out[n++] = e->att_mode;  // attention form: 0 per head, 1 split
     return n;
 }
 
@@ -956,6 +971,15 @@ extern "C" int gemma_engine_set_plan(gemma_engine *e, const int *in, int n) {
             return -1;
         }
         e->plan[cls] = {ks, rpw, img ? 1 : 0};
+    }
+    if (n > 3 * MC_N) {
+        const int mode = in[3 * MC_N];
+        if ((mode != ATTN_PER_HEAD && mode != ATTN_SPLIT) || (mode == ATTN_SPLIT && !e->ag.nwg) ||
+            (mode == ATTN_PER_HEAD && (c.head_dim > 256 || c.n_ctx > 2048))) {
+            set_error("gemma_engine_set_plan: infeasible attention form");
+            return -1;
+        }
+        e->att_mode = mode;
     }
     drop_graph(e);
     return 0;

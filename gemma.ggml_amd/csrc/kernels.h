@@ -146,6 +146,7 @@ struct attn_args {
 };
 struct attn_geom {
     int nwg = 0, grid = 0;
+    int img = 0;  // the split form can write the output's Q8_0 image (32-dim KQV slices)
     size_t lds = 0, sbuf_floats = 0, sync_ints = 0;
 };
 attn_geom attn_geometry(int H, int Hkv, int hd, int ctx);

@@ -233,8 +233,11 @@ __device__ __forceinline__ void f16_step(float acc[4][8], const uint4 *x4, const
     }
 }
 
-constexpr int ATT_THREADS = 256;
-constexpr int ATT_QUADS = ATT_THREADS / 4;  // 64 quads: one KQ (position, head) or KQV (dim, head) each
+#ifndef GHIP_ATT_THREADS
+#define GHIP_ATT_THREADS 1024
+#endif
+constexpr int ATT_THREADS = GHIP_ATT_THREADS;
+constexpr int ATT_QUADS = ATT_THREADS / 4;  // one KQ (position, head) or KQV (dim, head) pair per quad
 constexpr int ATT_VW = 256;                 // V positions staged in LDS per dimension row (n_kv <= 256)
 constexpr int ATT_STG = 2;                  // staging uint4 per thread for each of K and V
 constexpr int ATT_MAXWG = 256;              // co-resident workgroups (in-kernel hand-off)
@@ -279,7 +282,8 @@ struct attn_split {
     int ps, ds;
 };
 __host__ __device__ inline attn_split attn_split_of(int G, int hd) {
-    int ps = ATT_QUADS / G, ds = ATT_QUADS / G;
+    // KQV slices of at most 32 dims: one Q8_0 block of each head's output per workgroup (image)
+    int ps = ATT_QUADS / G, ds = ATT_QUADS / G < 32 ? ATT_QUADS / G : 32;
     const int cap = ATT_STG * ATT_THREADS * 8;  // halfs
     if (ps * hd > cap) ps = cap / hd;
     if (ds * ATT_VW > cap) ds = cap / ATT_VW;
@@ -304,7 +308,7 @@ __device__ __forceinline__ int ld_sc1_i(const int *p) {
 
 #define ATT_STAMP(i)                                                                                        \
     do {                                                                                                    \
-        if (a.dbg_t && tid == 0) a.dbg_t[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (a.dbg_t && tid == 0) a.dbg_t[(int64_t)(kvh * a.nwg + wg) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
 // One token's attention for the G = H/Hkv query heads of kv head kvh = blockIdx.x / nwg, split over
@@ -321,7 +325,11 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int hd = a.hd, half = hd / 2, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
     const int lane = tid & 63, wave = tid >> 6;
-    const int G = a.H / a.Hkv, nwg = a.nwg, kvh = blockIdx.x / nwg, wg = blockIdx.x % nwg;
+    // a kv group's nwg workgroups share blockIdx % 8 (one XCD under round-robin placement: the
+    // hand-off stays in one L2 — speed only, the protocol is placement-independent)
+    const int G = a.H / a.Hkv, nwg = a.nwg;
+    const int slot = blockIdx.x >> 3, kvh = (slot / nwg) * 8 + (int)(blockIdx.x & 7), wg = slot % nwg;
+    if (kvh >= a.Hkv) return;
     const attn_split sp = attn_split_of(G, hd);
     const int PS = sp.ps, DS = sp.ds;
     const int nb = (hd + DS - 1) / DS;  // workgroups with KQV work
@@ -334,21 +342,27 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
     const float *cs = a.rope_cur, *sn = a.rope_cur + half;  // row of *pos (k_advance keeps it)
     // q: thread t takes 4 consecutive pairs (h, e..e+3) of the G*half pairs (npair % 4 == 0)
     const int npair = G * half, nq4 = npair / 4;
-    float4 qa[2], qb[2], ca[2], sa[2];
+    // (only waves holding pairs issue these loads: wave-uniform branches)
+    float4 qa[2] = {}, qb[2] = {}, ca[2] = {}, sa[2] = {};
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const int i4 = tid + r * ATT_THREADS;
-        const int i = (i4 < nq4 ? i4 : 0) * 4;
-        const int h = i / half, e = i % half;
-        qa[r] = *(const float4 *)(qg + h * hd + e);
-        qb[r] = *(const float4 *)(qg + h * hd + e + half);
-        ca[r] = *(const float4 *)(cs + e);
-        sa[r] = *(const float4 *)(sn + e);
+        if (i4 - lane < nq4) {
+            const int i = (i4 < nq4 ? i4 : 0) * 4;
+            const int h = i / half, e = i % half;
+            qa[r] = *(const float4 *)(qg + h * hd + e);
+            qb[r] = *(const float4 *)(qg + h * hd + e + half);
+            ca[r] = *(const float4 *)(cs + e);
+            sa[r] = *(const float4 *)(sn + e);
+        }
     }
     const int kq4 = half / 4;  // k: 4 pairs per thread for tid < half/4
     const int ik = (tid < kq4 ? tid : 0) * 4;
-    const float4 ka = *(const float4 *)(kh + ik), kb = *(const float4 *)(kh + ik + half);
-    const float4 kc4 = *(const float4 *)(cs + ik), ks4 = *(const float4 *)(sn + ik);
+    float4 ka{}, kb{}, kc4{}, ks4{};
+    if (wave * 64 < kq4) {
+        ka = *(const float4 *)(kh + ik); kb = *(const float4 *)(kh + ik + half);
+        kc4 = *(const float4 *)(cs + ik); ks4 = *(const float4 *)(sn + ik);
+    }
     // phase A, first position block of this workgroup: its PS K rows, one coalesced uint4 each
     const int kcw = hd / 8;  // uint4 per K row
     uint4 kst[ATT_STG];
@@ -577,14 +591,32 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
             f16_step8(acc, xv, *(const uint4 *)(prow + e0));
         }
         const float o = quad_reduce_f16(acc);
-        if (t4 == 0) a.out[(int64_t)(kvh * G + hb) * hd + db] = o;
+        if (t4 == 0) {
+            a.out[(int64_t)(kvh * G + hb) * hd + db] = o;
+            if (a.out_act) ((float *)smem)[hb * DS + (db - wg * DS)] = o;  // q16 is dead after KQ
+        }
+    }
+    if (a.out_act) {
+        // this slice's Q8_0 blocks of each head's output (DS == 32, aligned: one block per head)
+        __syncthreads();
+        if (tid < G * 4) {
+            const int h = tid >> 2, q = tid & 3;
+            const float *o = (const float *)smem + h * DS + q * 8;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = o[j];
+            image_put_quad(a.out_act, nullptr, a.out_da, (int64_t)(kvh * G + h) * (hd / 32) + wg, q, v);
+        }
     }
     ATT_STAMP(5);
 }
 
 constexpr int AH_THREADS = 1024;  // per-head form: 256 quads = 256 KQ positions / KQV dims per pass
-constexpr int AH_KPF = 8;         // K steps (of 32 elements) prefetched per lane: hd <= 256
-constexpr int AH_VPF = 8;         // V steps (of 32 positions) prefetched per lane: n_kv <= 256
+#ifndef GHIP_AH_PF
+#define GHIP_AH_PF 4
+#endif
+constexpr int AH_KPF = GHIP_AH_PF;  // K steps (of 32 elements) prefetched per lane: hd <= 256
+constexpr int AH_VPF = GHIP_AH_PF;  // V steps (of 32 positions) prefetched per lane: n_kv <= 256
 
 #define AH_STAMP(i)                                                                                         \
     do {                                                                                                    \
@@ -608,10 +640,15 @@ __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
     const float *vh = a.qkv + (int64_t)a.H * hd + kvw + (int64_t)kvh * hd;
     const float *cs = a.rope_cur, *sn = a.rope_cur + half;
     // ---- early loads (issue order = wait order): RoPE inputs + pos, then K rows, then V rows
+    // RoPE inputs: only the waves holding a pair load them (every load instruction costs the CU's
+    // load path ~16 clk whatever its addresses; a wave-uniform branch skips the others)
     const int n4 = half / 4, i4 = (tid < n4 ? tid : 0) * 4;
-    const float4 qa = *(const float4 *)(qh + i4), qb = *(const float4 *)(qh + i4 + half);
-    const float4 ka = *(const float4 *)(kh + i4), kb = *(const float4 *)(kh + i4 + half);
-    const float4 ca = *(const float4 *)(cs + i4), sa = *(const float4 *)(sn + i4);
+    float4 qa{}, qb{}, ka{}, kb{}, ca{}, sa{};
+    if (wave * 64 < n4) {
+        qa = *(const float4 *)(qh + i4); qb = *(const float4 *)(qh + i4 + half);
+        ka = *(const float4 *)(kh + i4); kb = *(const float4 *)(kh + i4 + half);
+        ca = *(const float4 *)(cs + i4); sa = *(const float4 *)(sn + i4);
+    }
     const int pos_v = ((const int *)a.rope_cur)[hd];  // published with the row (k_advance / begin)
     uint4 kpre[AH_KPF];
     {
@@ -948,10 +985,11 @@ attn_geom attn_geometry(int H, int Hkv, int hd, int ctx) {
     if (nb * Hkv > ATT_MAXWG) return g;
     const int na = (ctx + PS - 1) / PS;
     g.nwg = std::max(nb, std::min(na, std::min(32, ATT_MAXWG / Hkv)));
-    g.grid = g.nwg * Hkv;
+    g.grid = 8 * g.nwg * ((Hkv + 7) / 8);  // XCD-colocated groups (idle slots exit at once)
     g.lds = (size_t)G * hd * 2 + (size_t)hd * 2 + (size_t)PS * hd * 2 + (size_t)DS * ATT_VW * 2 + (size_t)G * ctx * 2;
     g.sbuf_floats = (size_t)Hkv * ctx * G;
     g.sync_ints = (size_t)Hkv * 2;
+    g.img = DS == 32 && hd % 32 == 0;
     return g;
 }
 
@@ -973,12 +1011,13 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
         return 0;
     }
     const attn_geom g = attn_geometry(a.H, a.Hkv, a.hd, a.ctx);
-    if (a.hd % 32 != 0 || a.hd > 512 || a.ctx % 32 != 0 || g.nwg == 0 || a.nwg != g.nwg || !a.sbuf || !a.sync) {
+    if (a.hd % 32 != 0 || a.hd > 512 || a.ctx % 32 != 0 || g.nwg == 0 || a.nwg != g.nwg || !a.sbuf || !a.sync ||
+        (a.out_act && attn_split_of(a.H / a.Hkv, a.hd).ds != 32)) {
         set_error("attn_decode: unsupported shape or missing scratch");
         return -1;
     }
     // every workgroup of a kv group must be resident at once (in-kernel hand-off)
-    if (g.grid > ATT_MAXWG) {
+    if (g.nwg * a.Hkv > ATT_MAXWG) {
         set_error("attn_decode: too many workgroups for the in-kernel hand-off");
         return -1;
     }

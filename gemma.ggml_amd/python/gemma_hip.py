@@ -213,16 +213,21 @@ class Engine:
         return self.plan()
 
     def plan(self):
-        """{class: (k_split, rows_per_wg, image)}"""
-        buf = (C.c_int * 15)()
-        n = self.L.gemma_engine_plan(self.h, buf, 15)
-        return {k: (buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i, k in enumerate(self.PLAN_CLASSES[: n // 3])}
+        """{class: (k_split, rows_per_wg, image)} plus "attention": form (0 per head, 1 split)"""
+        buf = (C.c_int * 16)()
+        n = self.L.gemma_engine_plan(self.h, buf, 16)
+        p = {k: (buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i, k in enumerate(self.PLAN_CLASSES[: n // 3])}
+        if n > 15:
+            p["attention"] = buf[15]
+        return p
 
     def set_plan(self, plan):
         flat = []
         for k in self.PLAN_CLASSES:
             v = list(plan[k])
             flat += v + [0] * (3 - len(v))
+        if "attention" in plan:
+            flat.append(int(plan["attention"]))
         arr = (C.c_int * len(flat))(*flat)
         if self.L.gemma_engine_set_plan(self.h, arr, len(flat)) != 0:
             raise RuntimeError("set_plan failed: " + last_error())

@@ -60,6 +60,28 @@ def test_decode_tiny_gqa_bitexact():
 
 
 @gpu
+@pytest.mark.parametrize("attention", [0, 1])
+def test_decode_gemma2b_attention_forms_bitexact(attention):
+    """both attention forms (one workgroup per head; XCD-colocated position/dim split with one
+    in-kernel hand-off), each with its Q8_0 output image feeding attn-out"""
+    O.lib().orc_set_threads(16)
+    shape = O.GEMMA_2B
+    m = O.Model(O.make_config(shape, n_ctx=256))
+    prompt = O.make_prompt(6, shape["n_vocab"])
+    seq_ref, lg_ref = m.generate(prompt, 3)
+    e = _engine(shape, n_ctx=256)
+    p = e.plan()
+    p["attention"] = attention
+    p["attn_out"] = (p["attn_out"][0], p["attn_out"][1], 1)
+    e.set_plan(p)
+    e.begin(prompt)
+    lg = e.step(len(prompt) + 3, want_logits=True, use_graph=True)
+    assert list(e.tokens()[: len(seq_ref)]) == list(seq_ref)
+    assert np.array_equal(lg[len(prompt) - 1:].view(np.uint32), lg_ref.view(np.uint32))
+    e.close()
+
+
+@gpu
 def test_decode_gemma2b_bitexact():
     O.lib().orc_set_threads(16)
     _check_decode(O.GEMMA_2B, n_prompt=6, n_decode=4, n_ctx=256)
@@ -232,6 +254,7 @@ def test_tuned_plan_bitexact():
             except RuntimeError:
                 continue  # infeasible split for this shape
             plans.append(p)
+    plans += [dict(plans[0], attention=0), dict(plans[0], attention=1), dict(plans[1], attention=1)]
     for p in plans:
         e.set_plan(p)
         e.begin(prompt)
