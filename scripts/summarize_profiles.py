@@ -49,6 +49,20 @@ if stats:
                     f"{float(r['AverageNs'])/1e3:.3f} | {float(r['MinNs'])/1e3:.3f} | {float(r['MaxNs'])/1e3:.3f} | "
                     f"{float(r['Percentage']):.2f} |\n")
     os.system(f"cp '{stats[0]}' '{out}/kernel_stats.csv'")
+trace = glob.glob(os.path.join(src, "prof", "**", "*kernel_trace.csv"), recursive=True)
+if trace:
+    # the same trace split by launch shape: the bench's Gemma-2B launches are separated from the
+    # tuning sweep and the Gemma-7B TP leg that share a template instance
+    groups = {}
+    for r in csv.DictReader(open(trace[0])):
+        key = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))
+        groups.setdefault(key, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    with open(os.path.join(out, "kernel_trace_by_shape.md"), "w") as f:
+        f.write("# rocprofv3 --kernel-trace, grouped by (kernel, grid, workgroup)\n\n")
+        f.write("| kernel | grid threads | WG | calls | avg us | median us |\n|---|---|---|---|---|---|\n")
+        for key, v in sorted(groups.items(), key=lambda kv: -sum(kv[1]))[:40]:
+            v.sort()
+            f.write(f"| `{key[0]}` | {key[1]} | {key[2]} | {len(v)} | {sum(v)/len(v)/1e3:.2f} | {v[len(v)//2]/1e3:.2f} |\n")
 
 per = {}
 for cnt in ("FETCH_SIZE", "WRITE_SIZE"):
