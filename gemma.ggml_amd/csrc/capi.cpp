@@ -231,8 +231,8 @@ extern "C" void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, 
 // W: ggml row-major blocks [rows][K/32] of `type`; X: [T][K] f32.  Quantizes X like ggml's INIT
 // (Q8_0, AVX2 semantics) and runs the int8 MFMA GEMM: Y[T][rows].  xq/da (optional) return the
 // activation image for a bit-exact check of the quantizer.
-extern "C" int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X, float *Y,
-                               int8_t *xq_out, float *da_out) {
+static int test_gemm(bool exact, int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X, float *Y,
+                     int8_t *xq_out, float *da_out) {
     set_error("");
     if ((type != T_Q4_0 && type != T_Q8_0) || K % 32 || rows <= 0 || T <= 0) {
         set_error("gemma_test_gemm: bad arguments");
@@ -258,7 +258,7 @@ extern "C" int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, con
     gemm_args g;
     g.qs = m.qs; g.sc = m.sc; g.rows = rows; g.n_rt = m.n_rt; g.n_bt = m.n_bt; g.nb = m.nb;
     g.xq = d_q; g.ldq = ldq; g.da = d_da; g.ldd = ldd; g.T = T; g.y = d_y; g.ldy = rows;
-    if (r == 0) r = launch_gemm_q(type, EPI_STORE, g, nullptr);
+    if (r == 0) r = exact ? launch_gemm_exact(type, EPI_STORE, g, nullptr) : launch_gemm_q(type, EPI_STORE, g, nullptr);
     if (r == 0) GHIP_CHECK(hipDeviceSynchronize());
     if (r == 0) {
         GHIP_CHECK(hipMemcpy(Y, d_y, (size_t)(T * rows * 4), hipMemcpyDeviceToHost));
@@ -272,4 +272,14 @@ extern "C" int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, con
     void *bufs[] = {d_rows, d_x, d_y, d_q, d_da};
     for (void *p : bufs) (void)hipFree(p);
     return r;
+}
+
+extern "C" int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X, float *Y,
+                               int8_t *xq_out, float *da_out) {
+    return test_gemm(false, type, rows, K, T, W, X, Y, xq_out, da_out);
+}
+
+extern "C" int gemma_test_gemm_exact(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X,
+                                     float *Y, int8_t *xq_out, float *da_out) {
+    return test_gemm(true, type, rows, K, T, W, X, Y, xq_out, da_out);
 }

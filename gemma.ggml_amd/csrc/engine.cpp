@@ -1010,7 +1010,7 @@ static int prefill_alloc(gemma_engine *e, int T) {
     return 0;
 }
 
-static int enqueue_prefill(gemma_engine *e, int T, float *taps = nullptr) {
+static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nullptr) {
     const gemma_hip_config &c = e->cfg;
     hipStream_t s = e->stream;
     auto &p = e->pf;
@@ -1020,7 +1020,7 @@ static int enqueue_prefill(gemma_engine *e, int T, float *taps = nullptr) {
         gemm_args g;
         g.qs = m.qs; g.sc = m.sc; g.rows = m.rows; g.n_rt = m.n_rt; g.n_bt = m.n_bt; g.nb = m.nb;
         g.xq = p.XQ; g.ldq = p.ldq; g.da = p.DA; g.ldd = p.ldd; g.T = T; g.y = y; g.resid = resid; g.ldy = ldy;
-        return launch_gemm_q(wt, epi, g, s);
+        return exact ? launch_gemm_exact(wt, epi, g, s) : launch_gemm_q(wt, epi, g, s);
     };
     auto quant = [&](int mode, const float *x, const float *x2, int64_t K, const float *norm_w) {
         qrow_args a;
@@ -1048,7 +1048,7 @@ static int enqueue_prefill(gemma_engine *e, int T, float *taps = nullptr) {
         attnp_args at;
         at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
         at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
-        if (launch_attn_prefill(at, s)) return -1;
+        if (exact ? launch_attn_rows(at, s) : launch_attn_prefill(at, s)) return -1;
         if (quant(QR_F32, p.ATT, nullptr, e->qw, nullptr)) return -1;
         if (gemm(L.o, EPI_ADD, p.X, p.SA, E)) return -1;
         if (quant(QR_NORM, p.SA, nullptr, E, L.ffn_norm)) return -1;
@@ -1069,13 +1069,13 @@ static int enqueue_prefill(gemma_engine *e, int T, float *taps = nullptr) {
     return launch_advance((const unsigned long long *)p.keys, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
 }
 
-// MFMA prefill of the prompt given to gemma_engine_begin: all prompt
-// positions in one pass (int8 MFMA GEMMs, f16 MFMA causal attention), KV cache filled, logits for
-// every row as the reference computes them (src/gemma_model.cpp:740); returns the greedy token
-// and leaves the engine at position T, ready for gemma_engine_step.  Logits match the CPU path
-// within fp32 reordering; the token-by-token path remains the bit-exact one.
-extern "C" int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *logits_all) {
-    set_error("");
+// Batched prefill of the prompt given to gemma_engine_begin: all prompt
+// positions in one pass, KV cache filled, logits for every row as the reference computes them
+// (src/gemma_model.cpp:740); returns the greedy token and leaves the engine at position T, ready
+// for gemma_engine_step.  exact: ggml-lane-order GEMMs + per-row decode-arithmetic attention,
+// bit-identical to the CPU path; otherwise int8 MFMA GEMMs + f16 MFMA attention, which differ from
+// it in fp32 summation order.
+static int prefill_run(gemma_engine *e, bool exact, float *logits_last, float *logits_all) {
     (void)hipSetDevice(e->device);
     const gemma_hip_config &c = e->cfg;
     const int T = e->n_prompt;
@@ -1088,7 +1088,7 @@ extern "C" int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *
         return -1;
     }
     if (prefill_alloc(e, T)) return -1;
-    if (enqueue_prefill(e, T)) return -1;
+    if (enqueue_prefill(e, T, exact)) return -1;
     GHIP_CHECK(hipStreamSynchronize(e->stream));
     if (logits_last)
         GHIP_CHECK(hipMemcpy(logits_last, e->pf.LG + (size_t)(T - 1) * c.n_vocab, (size_t)c.n_vocab * 4,
@@ -1098,6 +1098,16 @@ extern "C" int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *
     GHIP_CHECK(hipMemcpy(&tok, e->token, 4, hipMemcpyDeviceToHost));
     e->host_pos = T;
     return tok;
+}
+
+extern "C" int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *logits_all) {
+    set_error("");
+    return prefill_run(e, true, logits_last, logits_all);
+}
+
+extern "C" int gemma_engine_prefill_fast(gemma_engine *e, float *logits_last, float *logits_all) {
+    set_error("");
+    return prefill_run(e, false, logits_last, logits_all);
 }
 
 // one eager step with per-layer taps copied to host: [L][qkv | attn | x_out]
@@ -1270,9 +1280,9 @@ extern "C" double gemma_hbm_read_gbs(int device, size_t bytes, int iters) {
     return gbs;
 }
 
-// diagnostics: the MFMA prefill with the residual stream after every layer copied to host_taps
+// diagnostics: the prefill (exact or MFMA) with the residual stream after every layer copied to host_taps
 // [n_layer][T][n_embd] (compare with the oracle's per-layer hidden states)
-extern "C" int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps) {
+extern "C" int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps, int exact) {
     set_error("");
     (void)hipSetDevice(e->device);
     const gemma_hip_config &c = e->cfg;
@@ -1285,7 +1295,7 @@ extern "C" int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps) {
     float *d = nullptr;
     const size_t n = (size_t)c.n_layer * T * c.n_embd;
     GHIP_CHECK(hipMalloc(&d, n * 4));
-    int r = enqueue_prefill(e, T, d);
+    int r = enqueue_prefill(e, T, exact != 0, d);
     if (r == 0) GHIP_CHECK(hipStreamSynchronize(e->stream));
     if (r == 0) GHIP_CHECK(hipMemcpy(host_taps, d, n * 4, hipMemcpyDeviceToHost));
     (void)hipFree(d);

@@ -89,6 +89,8 @@ struct gemm_args {  // Y[t][r] (stride ldy) = W (tiled) x Xq[t] (+ resid), t < T
     int64_t ldy = 0;
 };
 int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s);
+// the same product in ggml's AVX2 lane order (bit-identical to mul_mat)
+int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s);
 
 struct ropekv_args {  // RoPE q (-> f16, x q_scale) and k, store k/v of positions p0.. in the layer caches
     const float *qkv = nullptr;  // [T][ldqkv] = q | k | v
@@ -108,6 +110,8 @@ struct attnp_args {  // causal attention of T prompt tokens against the layer ca
     int T = 0, H = 0, Hkv = 0, hd = 0, ctx = 0, n_kv = 0;
 };
 int launch_attn_prefill(const attnp_args &a, hipStream_t s);
+// exact rows: each prompt row with the decode attention's arithmetic (ops.hip)
+int launch_attn_rows(const attnp_args &a, hipStream_t s);
 int launch_row_argmax(const float *row, int64_t n, unsigned long long *keys, int parts, hipStream_t s);
 
 // ---- weights (ops.hip) ------------------------------------------------------------------------

@@ -821,6 +821,84 @@ __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
     AH_STAMP(4);
 }
 
+// ---- exact causal attention for T prompt rows (the reference's prefill graph) -----------------
+// Row i of the prefill KQ / soft_max_ext / KQV (src/gemma_model.cpp:467-489 with T tokens) is the
+// decode computation at position i: positions j > i are masked to -inf (e = 0), and the KQV terms
+// past the row's own padded n_kv multiply exact zeros, so each row runs k_attn_head's arithmetic
+// (vec_dot_f16 lane order via v_fma_mix, fp16 exp, integer-exact sum, (float)(1/sum)) over
+// n_kv(i) = 32*((i+1)/32+1) positions.  One 1024-thread workgroup per (row, kv head) serves the
+// G query heads of that kv head, so every K/V row leaves L2 once per row for all of them:
+// quad q -> head q % G, KQ position q / G (+ 256/G per pass), KQV dim q / G (+ 256/G).  Rows are
+// issued longest first.  q16 / caches come from k_rope_kv_prefill (same RoPE/f16 arithmetic).
+constexpr int AR_THREADS = 1024;
+
+__global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2, lane = tid & 63, wave = tid >> 6;
+    const int G = a.H / a.Hkv, hd = a.hd, kvw = a.Hkv * hd, nkp = a.n_kv;
+    const int kvh = blockIdx.x % a.Hkv, i = a.T - 1 - (int)(blockIdx.x / a.Hkv);
+    const int g = quad % G, qo = quad / G, QP = (AR_THREADS / 4) / G, h = kvh * G + g;
+    float *S = (float *)smem;                      // [G][nkp]
+    uint16_t *P16 = (uint16_t *)(S + (size_t)G * nkp);  // [G][nkp]
+    int n_kv = 32 * ((i + 1) / 32 + 1);
+    if (n_kv > nkp) n_kv = nkp;
+    uint4 qv[8];
+    const uint16_t *qrow = a.q16 + ((int64_t)i * a.H + h) * hd;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qv[s] = s * 32 < hd ? *(const uint4 *)(qrow + s * 32 + t4 * 8) : make_uint4(0, 0, 0, 0);
+    // KQ + mask (scale 1.0, mask 0 / -inf)
+    for (int j0 = 0; j0 < n_kv; j0 += QP) {
+        const int j = j0 + qo;
+        if (j >= n_kv) continue;
+        float kq = 0.0f;
+        if (j <= i) {
+            float acc[8];
+#pragma unroll
+            for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+            const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s * 32 < hd) f16_step8(acc, *(const uint4 *)(krow + s * 32), qv[s]);
+            kq = quad_reduce_f16(acc);
+        }
+        if (t4 == 0) S[g * nkp + j] = (j > i) ? -INFINITY : kq * 1.0f + 0.0f;
+    }
+    __syncthreads();
+    // soft_max_ext per head row: wave w takes heads w, w+16, ...
+    for (int gg = wave; gg < G; gg += AR_THREADS / 64) {
+        const float *Sr = S + gg * nkp;
+        float mx = -INFINITY;
+        for (int j = lane; j < n_kv; j += 64) mx = fmaxf(mx, Sr[j]);
+        mx = wave_max(mx);
+        unsigned long long isum = 0;
+        for (int j = lane; j < n_kv; j += 64) {
+            const float w = Sr[j];
+            const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
+            isum += (unsigned long long)(e * 16777216.0f);
+        }
+        const unsigned long long tot = wave_sum_u64(isum);
+        const double sum = (double)tot * (1.0 / 16777216.0);
+        const float inv = (float)(1.0 / sum);
+        for (int j = lane; j < n_kv; j += 64) {
+            const float w = Sr[j];
+            const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
+            P16[gg * nkp + j] = (uint16_t)f2h(e * inv);
+        }
+    }
+    __syncthreads();
+    // KQV: out[i][h][d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16[h])
+    for (int d = qo; d < hd; d += QP) {
+        float acc[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+        const uint16_t *vr = a.vc + ((int64_t)kvh * hd + d) * a.ctx + t4 * 8;
+        const uint16_t *pr = P16 + g * nkp + t4 * 8;
+        for (int st = 0; st < n_kv; st += 32) f16_step8(acc, *(const uint4 *)(vr + st), *(const uint4 *)(pr + st));
+        const float o = quad_reduce_f16(acc);
+        if (t4 == 0) a.out[(int64_t)i * a.ldo + (int64_t)h * hd + d] = o;
+    }
+}
+
 // streaming read for the measured HBM roofline: 8 x 16 B in flight per lane, grid-stride
 typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) k_stream_read(const uint4 *src_, uint64_t n16, unsigned *sink) {
@@ -991,6 +1069,20 @@ attn_geom attn_geometry(int H, int Hkv, int hd, int ctx) {
     g.sync_ints = (size_t)Hkv * 2;
     g.img = DS == 32 && hd % 32 == 0;
     return g;
+}
+
+int launch_attn_rows(const attnp_args &a, hipStream_t s) {
+    const int G = a.Hkv > 0 ? a.H / a.Hkv : 0;
+    const size_t lds = (size_t)G * a.n_kv * 6;
+    if (G <= 0 || a.H % a.Hkv || (AR_THREADS / 4) % G || a.hd % 32 || a.hd > 256 || a.ctx % 32 || a.n_kv % 32 ||
+        a.n_kv > a.ctx || a.T <= 0 || a.T > a.n_kv || lds > 160 * 1024) {
+        set_error("attn_rows: unsupported shape (head_dim <= 256, 256 % G == 0, G*n_kv*6 B of LDS <= 160 KiB)");
+        return -1;
+    }
+    GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_attn_rows, dim3((unsigned)(a.T * a.Hkv)), dim3(AR_THREADS), lds, s, a);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 int launch_attn_decode(const attn_args &a, hipStream_t s) {

@@ -256,6 +256,179 @@ __global__ void __launch_bounds__(256) k_gemm_q(gemm_args g) {
     }
 }
 
+// ---- exact GEMM: ggml's AVX2 lane order for every (row, token) pair ------------------------------
+// The reference computes each prompt row's MUL_MAT with the same vec_dot as decode:
+// eight fp32 lane chains acc_l = fmaf(d_w*d_a, isum_l, acc_l) in block order, isum_l = the exact
+// int32 dot of elements 4l..4l+3, then hsum ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7)).  Here one thread
+// runs lanes lp and lp+4 (lp = tid & 3) for XR rows x XT tokens: per block and (row, token) one
+// product d = d_w*d_a (exact: two fp16 significands) and per lane one v_dot4_i32_i8 + cvt + fmaf —
+// the identical operation sequence, so Y is bit-identical to mul_mat.  The fold is local
+// (a_lp + a_lp+4) then quad xor-2 / xor-1 DPP adds.  VALU-bound: 3.5 VALU ops per (row, token,
+// block, lane); the MFMA GEMM above cannot keep the lane chains.
+// Workgroup tile XM rows x XN tokens; K staged XKB = 8 blocks at a time, lane-major in LDS
+// (Ws[b][l][row], Xs[b][l][token] dwords) with the next stage's global loads in flight during
+// the current stage's compute.  blockIdx.x walks tokens so the token tiles of one weight tile run
+// together and the weights leave HBM about once per XCD.
+constexpr int XM = 32, XN = 64, XKB = 8, XR = 4, XT = 8;
+
+template <int WT, int EPI>
+__global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
+    __shared__ __attribute__((aligned(16))) uint32_t Ws[XKB][8][XM];
+    __shared__ __attribute__((aligned(16))) uint32_t Xs[XKB][8][XN];
+    __shared__ __attribute__((aligned(16))) float dws[XKB][XM];
+    __shared__ __attribute__((aligned(16))) float das[XKB][XN];
+    constexpr int BT = wfmt<WT>::BT;
+    constexpr int WREC = (WT == T_Q4_0) ? 1 : 2;  // 16-B weight records per thread per stage
+    const int tid = threadIdx.x, lp = tid & 3, gi = tid >> 2;
+    const int rg = gi & 7, tg = gi >> 3;
+    const int64_t t0 = (int64_t)blockIdx.x * XN, r0 = (int64_t)blockIdx.y * XM;
+    const int64_t n_rt = g.n_rt, n_bt = g.n_bt, nb = g.nb;
+
+    float acc[2][XR][XT];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int i = 0; i < XR; ++i)
+#pragma unroll
+            for (int j = 0; j < XT; ++j) acc[a][i][j] = 0.0f;
+
+    // staging registers: weight records + their row's scales, 4 token records, 2 token scales
+    uint4 wq[WREC], ws[WREC], xr[4];
+    float xd[2];
+    auto gload = [&](int64_t kb0) {
+#pragma unroll
+        for (int k = 0; k < WREC; ++k) {
+            const int rec = tid + 256 * k, tile_i = rec >> 6, ln = rec & 63, rr = ln >> 3;
+            const int rti = (WT == T_Q4_0) ? tile_i : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
+            int64_t rt = r0 / 8 + rti, bt = kb0 / BT + bti;
+            const bool ok = rt < n_rt && bt < n_bt;
+            rt = ok ? rt : 0;
+            bt = ok ? bt : 0;
+            wq[k] = *(const uint4 *)(g.qs + (rt * n_bt + bt) * 1024 + ln * 16);
+            const uint8_t *sp = g.sc + ((rt * n_bt + bt) * 8 + rr) * wfmt<WT>::SCALE_BYTES;
+            if (WT == T_Q4_0) ws[k] = *(const uint4 *)sp;
+            else { const uint2 s2 = *(const uint2 *)sp; ws[k] = make_uint4(s2.x, s2.y, 0u, 0u); }
+            if (!ok) { wq[k] = make_uint4(0u, 0u, 0u, 0u); ws[k] = make_uint4(0u, 0u, 0u, 0u); }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rec = tid + 256 * k, tok = rec >> 4, seg = rec & 15;
+            const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
+            xr[k] = *(const uint4 *)(g.xq + t * g.ldq + kb0 * 32 + seg * 16);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = tid + 256 * k, tok = c >> 3, b = c & 7;
+            const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
+            xd[k] = (kb0 + b < nb) ? g.da[t * g.ldd + kb0 + b] : 0.0f;
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int k = 0; k < WREC; ++k) {
+            const int rec = tid + 256 * k, tile_i = rec >> 6, ln = rec & 63, rr = ln >> 3, l = ln & 7;
+            const int rti = (WT == T_Q4_0) ? tile_i : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
+            const int row = rti * 8 + rr;
+            const uint32_t qd[4] = {wq[k].x, wq[k].y, wq[k].z, wq[k].w};
+            const uint32_t sd[4] = {ws[k].x, ws[k].y, ws[k].z, ws[k].w};
+            if (WT == T_Q4_0) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    // byte k of dword p: low nibble = block 2p elem 4l+k, high = block 2p+1; n -> n - 8
+                    const uint32_t vlo = (qd[p] & 0x0F0F0F0Fu) ^ 0x08080808u;
+                    const uint32_t vhi = ((qd[p] >> 4) & 0x0F0F0F0Fu) ^ 0x08080808u;
+                    Ws[2 * p][l][row] = vlo | ((vlo & 0x08080808u) * 0x1Eu);
+                    Ws[2 * p + 1][l][row] = vhi | ((vhi & 0x08080808u) * 0x1Eu);
+                }
+                if (l == 0) {
+#pragma unroll
+                    for (int b = 0; b < 8; ++b) dws[b][row] = h2f(sd[b >> 1] >> (16 * (b & 1)));
+                }
+            } else {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) Ws[bti * 4 + p][l][row] = qd[p];
+                if (l == 0) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) dws[bti * 4 + b][row] = h2f(sd[b >> 1] >> (16 * (b & 1)));
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int rec = tid + 256 * k, tok = rec >> 4, seg = rec & 15, b = seg >> 1, l0 = (seg & 1) * 4;
+            Xs[b][l0 + 0][tok] = xr[k].x;
+            Xs[b][l0 + 1][tok] = xr[k].y;
+            Xs[b][l0 + 2][tok] = xr[k].z;
+            Xs[b][l0 + 3][tok] = xr[k].w;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = tid + 256 * k;
+            das[c & 7][c >> 3] = xd[k];
+        }
+    };
+
+    gload(0);
+    for (int64_t kb0 = 0; kb0 < nb; kb0 += XKB) {
+        lstore();
+        __syncthreads();
+        if (kb0 + XKB < nb) gload(kb0 + XKB);
+        const int nbs = (int)(nb - kb0 < XKB ? nb - kb0 : XKB);
+        for (int b = 0; b < nbs; ++b) {
+            const uint4 w0 = *(const uint4 *)&Ws[b][lp][rg * XR], w1 = *(const uint4 *)&Ws[b][lp + 4][rg * XR];
+            const uint4 x0a = *(const uint4 *)&Xs[b][lp][tg * XT], x0b = *(const uint4 *)&Xs[b][lp][tg * XT + 4];
+            const uint4 x1a = *(const uint4 *)&Xs[b][lp + 4][tg * XT], x1b = *(const uint4 *)&Xs[b][lp + 4][tg * XT + 4];
+            const float4 dw4 = *(const float4 *)&dws[b][rg * XR];
+            const float4 da0 = *(const float4 *)&das[b][tg * XT], da1 = *(const float4 *)&das[b][tg * XT + 4];
+            const uint32_t wv[2][4] = {{w0.x, w0.y, w0.z, w0.w}, {w1.x, w1.y, w1.z, w1.w}};
+            const uint32_t xv[2][8] = {{x0a.x, x0a.y, x0a.z, x0a.w, x0b.x, x0b.y, x0b.z, x0b.w},
+                                       {x1a.x, x1a.y, x1a.z, x1a.w, x1b.x, x1b.y, x1b.z, x1b.w}};
+            const float dwv[4] = {dw4.x, dw4.y, dw4.z, dw4.w};
+            const float dav[8] = {da0.x, da0.y, da0.z, da0.w, da1.x, da1.y, da1.z, da1.w};
+#pragma unroll
+            for (int i = 0; i < XR; ++i)
+#pragma unroll
+                for (int j = 0; j < XT; ++j) {
+                    const float d = dwv[i] * dav[j];
+#pragma unroll
+                    for (int a = 0; a < 2; ++a) {
+                        const int s = __builtin_amdgcn_sdot4((int)wv[a][i], (int)xv[a][j], 0, false);
+                        acc[a][i][j] = __builtin_fmaf(d, (float)s, acc[a][i][j]);
+                    }
+                }
+        }
+        __syncthreads();
+    }
+    // hsum: (a_lp + a_lp+4), then quad xor 2, xor 1; thread lp stores tokens 2lp, 2lp+1
+#pragma unroll
+    for (int j = 0; j < XT; ++j) {
+        float o[XR];
+#pragma unroll
+        for (int i = 0; i < XR; ++i) {
+            float v = acc[0][i][j] + acc[1][i][j];
+            v = v + dpp_f<0x4E>(v);
+            v = v + dpp_f<0xB1>(v);
+            o[i] = v;
+        }
+        const int64_t t = t0 + tg * XT + j, r = r0 + rg * XR;
+        if ((j >> 1) != lp || t >= g.T) continue;
+        float *y = g.y + t * g.ldy + r;
+        if (EPI == EPI_ADD) {
+            const float *rs = g.resid + t * g.ldy + r;
+#pragma unroll
+            for (int i = 0; i < XR; ++i)
+                if (r + i < g.rows) o[i] = o[i] + rs[i];
+        }
+        if (r + XR <= g.rows && (g.ldy & 3) == 0) {
+            *(float4 *)y = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < XR; ++i)
+                if (r + i < g.rows) y[i] = o[i];
+        }
+    }
+}
+
 // ---- RoPE + q scale + KV store for T prompt tokens (positions p0 .. p0+T-1) --------------------
 // Same per-element arithmetic as the decode attention (src/gemma_model.cpp:698-718, 499-518).
 __global__ void __launch_bounds__(256) k_rope_kv_prefill(ropekv_args a) {
@@ -493,6 +666,29 @@ int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s) {
     else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_q<T_Q8_0, EPI_ADD>), grid, dim3(256), 0, s, g);
     else {
         set_error("gemm_q: unsupported (type, epilogue)");
+        return -1;
+    }
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
+    if (g.ldq % 256 || g.nb * 32 > g.ldq || g.T <= 0 || g.rows <= 0) {
+        set_error("gemm_exact: activation image must be padded to 256 elements");
+        return -1;
+    }
+    const int64_t gy = (g.rows + XM - 1) / XM;
+    if (gy > 65535) {
+        set_error("gemm_exact: too many rows");
+        return -1;
+    }
+    const dim3 grid((unsigned)((g.T + XN - 1) / XN), (unsigned)gy);
+    if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_STORE>), grid, dim3(256), 0, s, g);
+    else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_ADD>), grid, dim3(256), 0, s, g);
+    else if (wtype == T_Q8_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_STORE>), grid, dim3(256), 0, s, g);
+    else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_ADD>), grid, dim3(256), 0, s, g);
+    else {
+        set_error("gemm_exact: unsupported (type, epilogue)");
         return -1;
     }
     GHIP_CHECK(hipGetLastError());

@@ -19,6 +19,7 @@ GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
 EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
            "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
            "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
+           "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
            "gemma_engine_plan", "gemma_engine_set_plan", "gemma_hbm_read_gbs",
            "gemma_tp_unique_id", "gemma_engine_create_tp"]
@@ -88,6 +89,10 @@ def lib():
     L.gemma_engine_pos.argtypes = [vp]
     L.gemma_engine_prefill.restype = C.c_int
     L.gemma_engine_prefill.argtypes = [vp, vp, vp]
+    L.gemma_engine_prefill_fast.restype = C.c_int
+    L.gemma_engine_prefill_fast.argtypes = [vp, vp, vp]
+    L.gemma_engine_prefill_taps.restype = C.c_int
+    L.gemma_engine_prefill_taps.argtypes = [vp, vp, C.c_int]
     L.gemma_engine_tensor.restype = C.c_int64
     L.gemma_engine_tensor.argtypes = [vp, C.c_int, vp, i64]
     L.gemma_engine_tune.argtypes = [vp, C.c_int]
@@ -182,11 +187,13 @@ class Engine:
         n = self.L.gemma_engine_tokens(self.h, _p(out), len(out))
         return out[:n]
 
-    def prefill(self, n_prompt=None, want_all=False):
-        """MFMA prefill of the prompt given to begin(); returns (token, last-row logits[, all rows])."""
+    def prefill(self, n_prompt=None, want_all=False, exact=True):
+        """Batched prefill of the prompt given to begin(); returns (token, last-row logits[, all rows]).
+        exact=True: bit-identical to the CPU path; False: the MFMA tolerance path."""
         last = np.zeros(self.cfg.n_vocab, dtype=np.float32)
         allv = np.zeros((n_prompt, self.cfg.n_vocab), dtype=np.float32) if want_all else None
-        tok = self.L.gemma_engine_prefill(self.h, _p(last), _p(allv) if want_all else None)
+        fn = self.L.gemma_engine_prefill if exact else self.L.gemma_engine_prefill_fast
+        tok = fn(self.h, _p(last), _p(allv) if want_all else None)
         if tok < 0:
             raise RuntimeError("prefill failed: " + last_error())
         return (tok, last, allv) if want_all else (tok, last)

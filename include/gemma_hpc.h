@@ -74,9 +74,12 @@ int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_prompt);
 int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_graph);
 int gemma_engine_tokens(gemma_engine *e, int32_t *out, int cap); /* sequence so far; returns len */
 int gemma_engine_pos(gemma_engine *e);
-/* batched prefill on MFMA (tolerance path): processes the whole prompt,
- * writes the last row's logits (and all rows if logits_all), returns the greedy token */
+/* batched prefill (the reference's T-token graph, src/gemma_model.cpp:665-747): processes the
+ * whole prompt in one pass, writes the last row's logits (and all rows if logits_all), returns
+ * the greedy token.  Bit-identical to the CPU path (ggml lane order). */
 int gemma_engine_prefill(gemma_engine *e, float *logits_last, float *logits_all);
+/* the same on int8/f16 MFMA: fp32 summation order differs from the CPU path (tolerance path) */
+int gemma_engine_prefill_fast(gemma_engine *e, float *logits_last, float *logits_all);
 /* weights back in ggml row-major layout (tests); tid as in DESIGN.md §Synthetic weights */
 int64_t gemma_engine_tensor(gemma_engine *e, int tid, void *dst, int64_t cap);
 /* time `iters` launches of one hot kernel with hipEvents on the engine stream; returns avg µs and
@@ -93,8 +96,9 @@ int gemma_engine_plan(gemma_engine *e, int *out, int cap);
 int gemma_engine_set_plan(gemma_engine *e, const int *in, int n);
 /* debugging: one eager step with per-layer taps [n_layer][qkv | attn_out | layer_out] */
 int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
-/* diagnostics: MFMA prefill with the residual stream after each layer -> [n_layer][T][n_embd] */
-int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps);
+/* diagnostics: prefill (exact != 0: the exact path) with the residual stream after each layer
+ * -> [n_layer][T][n_embd] */
+int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps, int exact);
 /* diagnostics: one eager step with s_memrealtime phase stamps (100 MHz) of layer `layer`'s five
  * kernels (regions 0..4: qkv, attention, attn-out, gate/up, down) and the logits kernel (region 5);
  * out = 6 * 4096 * 16 u64, slot [region][workgroup][phase], unused slots 0 */
@@ -108,6 +112,9 @@ int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos
 /* per-op test entry: the prefill path's Q8_0 row quantization + int8 MFMA GEMM on host buffers */
 int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X, float *Y,
                     int8_t *xq_out, float *da_out);
+/* the same with the exact (ggml AVX2 lane order) GEMM of the exact prefill */
+int gemma_test_gemm_exact(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X, float *Y,
+                          int8_t *xq_out, float *da_out);
 /* measured HBM read roofline: streaming read of `bytes` on `device`, `iters` passes; GB/s */
 double gemma_hbm_read_gbs(int device, size_t bytes, int iters);
 /* per-op test entry: the softmax's exp(f16) for all 65536 codes (compared with ggml's table) */

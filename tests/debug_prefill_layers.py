@@ -16,12 +16,12 @@ m = O.Model(O.make_config(shape, n_ctx=256))
 m.inference(prompt, 0, want_all=True)
 L = G.lib()
 L.gemma_engine_prefill_taps.restype = C.c_int
-L.gemma_engine_prefill_taps.argtypes = [C.c_void_p, C.c_void_p]
+L.gemma_engine_prefill_taps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
 e = G.Engine(shape, n_ctx=256, device=0)
 e.begin(prompt)
 E = shape["n_embd"]
 taps = np.zeros((shape["n_layer"], n, E), np.float32)
-assert L.gemma_engine_prefill_taps(e.h, taps.ctypes.data) == 0, G.last_error()
+assert L.gemma_engine_prefill_taps(e.h, taps.ctypes.data, 0) == 0, G.last_error()
 for il in range(shape["n_layer"]):
     ref = m.hidden(il, n)
     err = np.abs(taps[il] - ref).max(axis=1) / np.abs(ref).max(axis=1)

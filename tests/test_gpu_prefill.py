@@ -1,8 +1,12 @@
-"""GPU parity of the prefill path (int8 MFMA GEMMs) against the CPU oracle.
+"""GPU parity of the two batched prefill paths against the CPU oracle.
 
-The activation Q8_0 image must be bit-identical to ggml's INIT quantizer (AVX2 semantics); the GEMM
-result differs from ggml's AVX2 lane-order accumulation only by fp32 rounding order, so it is
-checked at 1e-4 of the row maximum (the north star's logit tolerance is 1e-3 relative)."""
+EXACT path (gemma_engine_prefill): ggml-lane-order GEMMs + per-row decode-arithmetic attention —
+every logit of every prompt row, the greedy token and the KV cache left for decode must be
+bit-identical to the oracle (the CPU path's T-token graph, src/gemma_model.cpp:665-747).
+
+FAST path (gemma_engine_prefill_fast, int8/f16 MFMA): the activation Q8_0 image must be
+bit-identical to ggml's INIT quantizer (AVX2 semantics); the GEMM result differs from ggml's AVX2
+lane-order accumulation only by fp32 rounding order, so it is checked at 1e-4 of the row maximum."""
 import ctypes as C
 
 import numpy as np
@@ -14,13 +18,36 @@ gpu = pytest.mark.gpu
 GEMM_TOL = 1e-4
 
 
-def _gemm(L, wtype, W, X, rows, K, T):
+def _gemm(L, wtype, W, X, rows, K, T, exact=False):
     Y = np.zeros((T, rows), np.float32)
     xq = np.zeros((T, K), np.int8)
     da = np.zeros((T, K // 32), np.float32)
-    r = L.gemma_test_gemm(wtype, rows, K, T, W.ctypes.data, X.ctypes.data, Y.ctypes.data, xq.ctypes.data,
-                          da.ctypes.data)
+    fn = L.gemma_test_gemm_exact if exact else L.gemma_test_gemm
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_int64] + [C.c_void_p] * 5
+    r = fn(wtype, rows, K, T, W.ctypes.data, X.ctypes.data, Y.ctypes.data, xq.ctypes.data, da.ctypes.data)
     return r, Y, xq, da
+
+
+@gpu
+@pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0], ids=["q4_0", "q8_0"])
+@pytest.mark.parametrize("rows,K,T", [(64, 256, 64), (100, 512, 37), (72, 2048, 130), (2560, 2048, 96),
+                                      (256, 16384, 70), (40, 96, 3), (8, 32, 1), (96, 1312, 65)])
+def test_gemm_exact_bit_identical(wtype, rows, K, T):
+    """Exact GEMM == mul_mat (AVX2 lane order) bit for bit, incl. ragged rows/tokens/blocks and a
+    zero block."""
+    import gemma_hip as G
+    L = G.lib()
+    rng = np.random.default_rng(rows * 13 + K + T)
+    Wf = (rng.standard_normal((rows, K)) * 0.05).astype(np.float32)
+    W = O.quantize(Wf, "q4_0_ref" if wtype == O.Q4_0 else "q8_0_ref")
+    X = (rng.standard_normal((T, K)) * rng.uniform(0.1, 3.0, (T, 1))).astype(np.float32)
+    X[0, :min(37, K)] = 0.0
+    r, Y, xq, da = _gemm(L, wtype, W, X, rows, K, T, exact=True)
+    assert r == 0, G.last_error()
+    wdata, rs = O.mul_mat_init(wtype, X)
+    ref = O.mul_mat(W, wtype, rows, W.shape[1], K, wdata, rs, T)
+    assert np.array_equal(Y.view(np.uint32), ref.view(np.uint32)), np.abs(Y - ref).max()
 
 
 @gpu
@@ -80,7 +107,7 @@ def _prefill_case(shape, n_prompt, n_ctx, wtype=O.Q4_0, n_decode=6, deep=False):
     tok_ref, last_ref, all_ref = m.inference(prompt, 0, want_all=True)
     e = G.Engine(shape, n_ctx=n_ctx, wtype=wtype, device=0)
     e.begin(prompt)
-    tok, last, allv = e.prefill(n_prompt, want_all=True)
+    tok, last, allv = e.prefill(n_prompt, want_all=True, exact=False)
     err = _check_rows(allv, all_ref, deep)
     srt = np.sort(last_ref)
     if srt[-1] - srt[-2] > 2 * FLIP_TOL * np.abs(last_ref).max():  # a clear winner must be reproduced
@@ -122,3 +149,50 @@ def test_prefill_tiny_q8_0_gqa():
 def test_prefill_gemma2b_shapes():
     err, same = _prefill_case(dict(O.GEMMA_2B), 96, 256, n_decode=3, deep=True)
     assert same
+
+
+# ---- exact batched prefill: bit-identical logits for every row ---------------------------------
+def _prefill_exact_case(shape, n_prompt, n_ctx, wtype=O.Q4_0, n_decode=4):
+    import gemma_hip as G
+    prompt = O.make_prompt(n_prompt, shape["n_vocab"])
+    m = O.Model(O.make_config(shape, n_ctx=n_ctx, wtype=wtype))
+    tok_ref, last_ref, all_ref = m.inference(prompt, 0, want_all=True)
+    e = G.Engine(shape, n_ctx=n_ctx, wtype=wtype, device=0)
+    e.begin(prompt)
+    tok, last, allv = e.prefill(n_prompt, want_all=True, exact=True)
+    bad = np.nonzero((allv.view(np.uint32) != all_ref.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, (bad[:8], np.abs(allv - all_ref).max())
+    assert tok == tok_ref, (tok, tok_ref)
+    # decode continues bit-exactly from the KV cache the prefill wrote
+    seq = list(prompt) + [tok]
+    m.reset()
+    m.inference(list(prompt), 0)
+    lg = e.step(n_decode, want_logits=True, use_graph=True)
+    for i in range(n_decode):
+        _, l_ref, _ = m.inference(seq, 1)
+        assert np.array_equal(lg[i].view(np.uint32), l_ref.view(np.uint32)), i
+        seq.append(int(l_ref.argmax()))
+    assert list(e.tokens())[:len(seq)] == seq
+    e.close()
+    m.close()
+
+
+@gpu
+@pytest.mark.parametrize("n_prompt", [1, 31, 32, 100])
+def test_prefill_exact_tiny(n_prompt):
+    _prefill_exact_case(dict(O.TINY), n_prompt, 256)
+
+
+@gpu
+def test_prefill_exact_q8_0_gqa():
+    _prefill_exact_case(dict(O.TINY, n_head=4, n_head_kv=2), 70, 256, wtype=O.Q8_0)
+
+
+@gpu
+def test_prefill_exact_mha():
+    _prefill_exact_case(dict(O.TINY, n_head=4, n_head_kv=4), 45, 128)
+
+
+@gpu
+def test_prefill_exact_gemma2b_shapes():
+    _prefill_exact_case(dict(O.GEMMA_2B), 96, 256, n_decode=2)
