@@ -243,21 +243,23 @@ static int test_gemm(bool exact, int type, int64_t rows, int64_t K, int64_t T, c
     uint8_t *d_rows = nullptr;
     float *d_x = nullptr, *d_y = nullptr, *d_da = nullptr;
     int8_t *d_q = nullptr;
+    uint16_t *d_h = nullptr;
     GHIP_CHECK(hipMalloc(&d_rows, (size_t)(row_bytes * rows)));
     GHIP_CHECK(hipMalloc(&d_x, (size_t)(T * K * 4)));
     GHIP_CHECK(hipMalloc(&d_y, (size_t)(T * rows * 4)));
     GHIP_CHECK(hipMalloc(&d_q, (size_t)(T * ldq)));
     GHIP_CHECK(hipMalloc(&d_da, (size_t)(T * ldd * 4)));
+    GHIP_CHECK(hipMalloc(&d_h, (size_t)(T * ldq * 2)));
     GHIP_CHECK(hipMemcpy(d_rows, W, (size_t)(row_bytes * rows), hipMemcpyHostToDevice));
     GHIP_CHECK(hipMemcpy(d_x, X, (size_t)(T * K * 4), hipMemcpyHostToDevice));
     tiled_mat m = alloc_tiled(type, rows, K, nullptr);
     int r = launch_repack(m, d_rows, row_bytes, nullptr);
     qrow_args qa;
-    qa.x = d_x; qa.ldx = K; qa.K = K; qa.q = d_q; qa.ldq = ldq; qa.da = d_da; qa.ldd = ldd;
+    qa.x = d_x; qa.ldx = K; qa.K = K; qa.q = d_q; qa.qh = exact ? d_h : nullptr; qa.ldq = ldq; qa.da = d_da; qa.ldd = ldd;
     if (r == 0) r = launch_quant_rows(QR_F32, qa, (int)T, nullptr);
     gemm_args g;
     g.qs = m.qs; g.sc = m.sc; g.rows = rows; g.n_rt = m.n_rt; g.n_bt = m.n_bt; g.nb = m.nb;
-    g.xq = d_q; g.ldq = ldq; g.da = d_da; g.ldd = ldd; g.T = T; g.y = d_y; g.ldy = rows;
+    g.xq = d_q; g.xh = d_h; g.ldq = ldq; g.da = d_da; g.ldd = ldd; g.T = T; g.y = d_y; g.ldy = rows;
     if (r == 0) r = exact ? launch_gemm_exact(type, EPI_STORE, g, nullptr) : launch_gemm_q(type, EPI_STORE, g, nullptr);
     if (r == 0) GHIP_CHECK(hipDeviceSynchronize());
     if (r == 0) {
@@ -269,7 +271,7 @@ static int test_gemm(bool exact, int type, int64_t rows, int64_t K, int64_t T, c
                                    hipMemcpyDeviceToHost));
     }
     free_tiled(m);
-    void *bufs[] = {d_rows, d_x, d_y, d_q, d_da};
+    void *bufs[] = {d_rows, d_x, d_y, d_q, d_da, d_h};
     for (void *p : bufs) (void)hipFree(p);
     return r;
 }

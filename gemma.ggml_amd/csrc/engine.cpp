@@ -204,6 +204,7 @@ struct gemma_engine {
         float *DA = nullptr;
         uint16_t *Q16 = nullptr;
         int8_t *XQ = nullptr;
+        uint16_t *XH = nullptr;  // f16 image of the quantized activations (exact GEMM operand)
         void *keys = nullptr;
     } pf;
     float *dbg = nullptr;  // per-layer taps [L][qkv_rows + qw + E] (debug steps only)
@@ -606,7 +607,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     }
     void *bufs[] = {e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
                     e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf.X, e->pf.SA, e->pf.QKV, e->pf.ATT, e->pf.G, e->pf.U,
-                    e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.keys};
+                    e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.XH, e->pf.keys};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     (void)hipStreamDestroy(e->stream);
@@ -988,7 +989,7 @@ extern "C" int gemma_engine_set_plan(gemma_engine *e, const int *in, int n) {
 static int prefill_alloc(gemma_engine *e, int T) {
     auto &p = e->pf;
     if (p.T >= T) return 0;
-    void *bufs[] = {p.X, p.SA, p.QKV, p.ATT, p.G, p.U, p.LG, p.DA, p.Q16, p.XQ, p.keys};
+    void *bufs[] = {p.X, p.SA, p.QKV, p.ATT, p.G, p.U, p.LG, p.DA, p.Q16, p.XQ, p.XH, p.keys};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     const gemma_hip_config &c = e->cfg;
@@ -1005,6 +1006,7 @@ static int prefill_alloc(gemma_engine *e, int T) {
     GHIP_CHECK(hipMalloc(&p.DA, (size_t)T * p.ldd * 4));
     GHIP_CHECK(hipMalloc(&p.Q16, (size_t)T * e->qw * 2));
     GHIP_CHECK(hipMalloc(&p.XQ, (size_t)T * p.ldq));
+    GHIP_CHECK(hipMalloc(&p.XH, (size_t)T * p.ldq * 2));
     GHIP_CHECK(hipMalloc(&p.keys, 256 * 8));
     p.T = T;
     return 0;
@@ -1019,13 +1021,13 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
     auto gemm = [&](const tiled_mat &m, int epi, const float *resid, float *y, int64_t ldy) {
         gemm_args g;
         g.qs = m.qs; g.sc = m.sc; g.rows = m.rows; g.n_rt = m.n_rt; g.n_bt = m.n_bt; g.nb = m.nb;
-        g.xq = p.XQ; g.ldq = p.ldq; g.da = p.DA; g.ldd = p.ldd; g.T = T; g.y = y; g.resid = resid; g.ldy = ldy;
+        g.xq = p.XQ; g.xh = p.XH; g.ldq = p.ldq; g.da = p.DA; g.ldd = p.ldd; g.T = T; g.y = y; g.resid = resid; g.ldy = ldy;
         return exact ? launch_gemm_exact(wt, epi, g, s) : launch_gemm_q(wt, epi, g, s);
     };
     auto quant = [&](int mode, const float *x, const float *x2, int64_t K, const float *norm_w) {
         qrow_args a;
         a.x = x; a.x2 = x2; a.ldx = K; a.K = K; a.norm_w = norm_w; a.eps = c.eps;
-        a.q = p.XQ; a.ldq = p.ldq; a.da = p.DA; a.ldd = p.ldd;
+        a.q = exact ? nullptr : p.XQ; a.qh = exact ? p.XH : nullptr; a.ldq = p.ldq; a.da = p.DA; a.ldd = p.ldd;
         a.gelu_tab = e->gelu_tab; a.gelu_clamp = c.gelu_clamp;
         if (mode == QR_EMBED_NORM) {
             a.tokens = e->hist; a.emb_qs = e->embd.qs; a.emb_sc = e->embd.sc; a.emb_type = wt;

@@ -70,7 +70,8 @@ struct qrow_args {  // T rows of K floats -> Q8_0 image q [T][ldq] int8 + da [T]
     float *emb_out = nullptr;                 // scaled embedding rows (the residual stream), stride ldx
     const uint16_t *gelu_tab = nullptr;
     int gelu_clamp = 0;
-    int8_t *q = nullptr;
+    int8_t *q = nullptr;                      // int8 image (nullptr: not written)
+    uint16_t *qh = nullptr;                   // optional f16 image of the same values (exact GEMM)
     int64_t ldq = 0;                          // multiple of 256 (zero padded)
     float *da = nullptr;
     int64_t ldd = 0;                          // >= ldq / 32
@@ -80,6 +81,7 @@ struct gemm_args {  // Y[t][r] (stride ldy) = W (tiled) x Xq[t] (+ resid), t < T
     const uint8_t *qs = nullptr, *sc = nullptr;
     int64_t rows = 0, n_rt = 0, n_bt = 0, nb = 0;
     const int8_t *xq = nullptr;
+    const uint16_t *xh = nullptr;  // f16 image of xq (the exact GEMM's MFMA operand), same stride
     int64_t ldq = 0;
     const float *da = nullptr;
     int64_t ldd = 0;

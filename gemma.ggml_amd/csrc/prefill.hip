@@ -119,11 +119,23 @@ __global__ void __launch_bounds__(256) k_quant_rows(qrow_args a) {
             pk[h] = (uint32_t)(qi[0] & 0xFF) | ((uint32_t)(qi[1] & 0xFF) << 8) | ((uint32_t)(qi[2] & 0xFF) << 16) |
                     ((uint32_t)(qi[3] & 0xFF) << 24);
         }
-        *(uint2 *)(qo + b * 32 + q * 8) = make_uint2(pk[0], pk[1]);
+        if (a.q) *(uint2 *)(qo + b * 32 + q * 8) = make_uint2(pk[0], pk[1]);
+        if (a.qh) {  // the same integers as f16 (exact): the exact GEMM's MFMA operand
+            uint32_t hv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int q0 = (int8_t)(pk[k >> 1] >> (16 * (k & 1))), q1 = (int8_t)(pk[k >> 1] >> (16 * (k & 1) + 8));
+                hv[k] = f2h((float)q0) | (f2h((float)q1) << 16);
+            }
+            *(uint4 *)(a.qh + (int64_t)t * a.ldq + b * 32 + q * 8) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+        }
         if (q == 0) dout[b] = h2f(d16);
     }
-    // zero the K padding of the int8 image (the GEMM stages whole 256-element chunks)
-    for (int64_t i = K + tid * 4; i < a.ldq; i += 256 * 4) *(uint32_t *)(qo + i) = 0;
+    // zero the K padding of the images (the GEMMs stage whole 256-element chunks)
+    if (a.q)
+        for (int64_t i = K + tid * 4; i < a.ldq; i += 256 * 4) *(uint32_t *)(qo + i) = 0;
+    if (a.qh)
+        for (int64_t i = K + tid * 2; i < a.ldq; i += 256 * 2) *(uint32_t *)(a.qh + (int64_t)t * a.ldq + i) = 0;
     for (int64_t b = nb + tid; b < a.ldd; b += 256) dout[b] = 0.0f;
 }
 
@@ -259,42 +271,78 @@ __global__ void __launch_bounds__(256) k_gemm_q(gemm_args g) {
 // ---- exact GEMM: ggml's AVX2 lane order for every (row, token) pair ------------------------------
 // The reference computes each prompt row's MUL_MAT with the same vec_dot as decode:
 // eight fp32 lane chains acc_l = fmaf(d_w*d_a, isum_l, acc_l) in block order, isum_l = the exact
-// int32 dot of elements 4l..4l+3, then hsum ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7)).  Here one thread
-// runs lanes lp and lp+4 (lp = tid & 3) for XR rows x XT tokens: per block and (row, token) one
-// product d = d_w*d_a (exact: two fp16 significands) and per lane one v_dot4_i32_i8 + cvt + fmaf —
-// the identical operation sequence, so Y is bit-identical to mul_mat.  The fold is local
-// (a_lp + a_lp+4) then quad xor-2 / xor-1 DPP adds.  VALU-bound: 3.5 VALU ops per (row, token,
-// block, lane); the MFMA GEMM above cannot keep the lane chains.
-// Workgroup tile XM rows x XN tokens; K staged XKB = 8 blocks at a time, lane-major in LDS
-// (Ws[b][l][row], Xs[b][l][token] dwords) with the next stage's global loads in flight during
-// the current stage's compute.  blockIdx.x walks tokens so the token tiles of one weight tile run
+// int32 dot of elements 4l..4l+3, then hsum ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7)).
+// The lane sums come from f16 MFMA with the lane structure in the M dimension: MFMA row m = 8*rr
+// + l is weight row rr's lane l, its A row holds only elements 4l..4l+3 of the block (zeros
+// elsewhere), so D[m][token] = isum_l exactly (products and sums of small integers are exact in
+// f32) and arrives as f32 — no conversion.  A lane's D registers are 4 consecutive m = 4 lanes of
+// one (row, token), so one d = d_w*d_a (exact: two fp16 significands) serves 4 fmaf; the chain
+// continues block after block in the same register: the identical operation sequence, so Y is
+// bit-identical to mul_mat.  Fold: lanes 0-3 / 4-7 of a pair sit in lanes j / j^16.
+// Workgroup tile XM rows x XN tokens, 4 waves of 16 rows x 32 tokens (8 x 2 MFMA 16x16x32 per
+// block).  K is staged XKB = 8 blocks at a time: weights as pre-masked 16-B A fragments per
+// (block, row, lane) (Q4_0 nibbles / Q8_0 int8 -> f16 by the 0x6400 exponent trick), tokens as
+// f16 rows (the quantizer's f16 image); the next stage's global loads are in flight during the
+// current stage's MFMAs.  blockIdx.x walks tokens so the token tiles of one weight tile run
 // together and the weights leave HBM about once per XCD.
-constexpr int XM = 32, XN = 64, XKB = 8, XR = 4, XT = 8;
+typedef _Float16 xh8 __attribute__((ext_vector_type(8)));
+typedef float xf4 __attribute__((ext_vector_type(4)));
+
+// four small integers (bytes of v, biased so they are in [0, 1024)) -> 2 dwords of f16 pairs
+// f16(1024 + u) has bits 0x6400 | u; subtracting the bias (1024 + b) in f16 is exact
+__device__ __forceinline__ uint2 bytes_to_f16x4(uint32_t v, uint32_t bias_pair) {
+    const uint32_t lo = __builtin_amdgcn_perm(0u, v, 0x0c010c00u) | 0x64006400u;  // bytes 0,1
+    const uint32_t hi = __builtin_amdgcn_perm(0u, v, 0x0c030c02u) | 0x64006400u;  // bytes 2,3
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 b = __builtin_bit_cast(h2, bias_pair);
+    const h2 l2 = __builtin_bit_cast(h2, lo) - b, h2v = __builtin_bit_cast(h2, hi) - b;
+    return make_uint2(__builtin_bit_cast(uint32_t, l2), __builtin_bit_cast(uint32_t, h2v));
+}
+
+#ifndef GHIP_XCT
+#define GHIP_XCT 1
+#endif
+#ifndef GHIP_XPF
+#define GHIP_XPF 0
+#endif
+constexpr int XCT = GHIP_XCT;             // 16-token MFMA column tiles per wave
+constexpr int XM = 32, XN = 32 * XCT, XKB = 8;
+constexpr int XS_ROW = XKB * 32 * 2 + 16;  // bytes per staged token row (f16, padded)
+constexpr int XREC = XN * XKB * 64 / 16 / 256;  // 16-B token records per thread per stage
+constexpr int XDA = XN * XKB / 256;             // token scales per thread per stage
 
 template <int WT, int EPI>
 __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
-    __shared__ __attribute__((aligned(16))) uint32_t Ws[XKB][8][XM];
-    __shared__ __attribute__((aligned(16))) uint32_t Xs[XKB][8][XN];
-    __shared__ __attribute__((aligned(16))) float dws[XKB][XM];
+    // A fragments: [b][row][lane] 16 B (lane l's 4 f16 in half l&1 of the fragment)
+    // + a zero region the inactive lanes read at the same strides (no per-lane select)
+    __shared__ __attribute__((aligned(16))) uint4 Wf[XKB * XM * 8 + 7 * 16 + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t Xs[XN * XS_ROW];
+    __shared__ __attribute__((aligned(16))) float dws[XKB][2][XM / 2];  // [b][row & 1][row >> 1]
     __shared__ __attribute__((aligned(16))) float das[XKB][XN];
     constexpr int BT = wfmt<WT>::BT;
     constexpr int WREC = (WT == T_Q4_0) ? 1 : 2;  // 16-B weight records per thread per stage
-    const int tid = threadIdx.x, lp = tid & 3, gi = tid >> 2;
-    const int rg = gi & 7, tg = gi >> 3;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, kg = lane >> 4;
+    const int wr = (wave & 1) * 16, wt = (wave >> 1) * 16 * XCT;  // wave tile: rows wr.., tokens wt..
     const int64_t t0 = (int64_t)blockIdx.x * XN, r0 = (int64_t)blockIdx.y * XM;
     const int64_t n_rt = g.n_rt, n_bt = g.n_bt, nb = g.nb;
+    // this lane's A fragment: MFMA row l16 = (weight row wr + 2*rt + (l16 >> 3), lane l16 & 7);
+    // nonzero only when the lane's 4 elements fall in the lane's k range 8*kg .. 8*kg+7
+    const bool a_act = ((l16 & 7) >> 1) == kg;
+    const uint4 *a_ptr = a_act ? &Wf[(wr + (l16 >> 3)) * 8 + (l16 & 7)] : &Wf[XKB * XM * 8];
+    const int a_bstride = a_act ? XM * 8 : 0;
+    for (int i = tid; i < 7 * 16 + 1; i += 256) Wf[XKB * XM * 8 + i] = make_uint4(0u, 0u, 0u, 0u);
 
-    float acc[2][XR][XT];
+    float acc[8][XCT][4];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int i = 0; i < XR; ++i)
+        for (int j = 0; j < XCT; ++j)
 #pragma unroll
-            for (int j = 0; j < XT; ++j) acc[a][i][j] = 0.0f;
+            for (int v = 0; v < 4; ++v) acc[i][j][v] = 0.0f;
 
-    // staging registers: weight records + their row's scales, 4 token records, 2 token scales
-    uint4 wq[WREC], ws[WREC], xr[4];
-    float xd[2];
+    uint4 wq[WREC], ws[WREC], xr[XREC];
+    float xd[XDA];
     auto gload = [&](int64_t kb0) {
 #pragma unroll
         for (int k = 0; k < WREC; ++k) {
@@ -311,13 +359,13 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
             if (!ok) { wq[k] = make_uint4(0u, 0u, 0u, 0u); ws[k] = make_uint4(0u, 0u, 0u, 0u); }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int rec = tid + 256 * k, tok = rec >> 4, seg = rec & 15;
+        for (int k = 0; k < XREC; ++k) {  // XN tokens x 512 B in 16-B records
+            const int rec = tid + 256 * k, tok = rec >> 5, seg = rec & 31;
             const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
-            xr[k] = *(const uint4 *)(g.xq + t * g.ldq + kb0 * 32 + seg * 16);
+            xr[k] = *(const uint4 *)(g.xh + t * g.ldq + kb0 * 32 + seg * 8);
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < XDA; ++k) {
             const int c = tid + 256 * k, tok = c >> 3, b = c & 7;
             const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
             xd[k] = (kb0 + b < nb) ? g.da[t * g.ldd + kb0 + b] : 0.0f;
@@ -331,41 +379,71 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
             const int row = rti * 8 + rr;
             const uint32_t qd[4] = {wq[k].x, wq[k].y, wq[k].z, wq[k].w};
             const uint32_t sd[4] = {ws[k].x, ws[k].y, ws[k].z, ws[k].w};
+            auto put = [&](int b, uint2 f) {
+                Wf[(b * XM + row) * 8 + l] = (l & 1) ? make_uint4(0u, 0u, f.x, f.y) : make_uint4(f.x, f.y, 0u, 0u);
+            };
             if (WT == T_Q4_0) {
 #pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    // byte k of dword p: low nibble = block 2p elem 4l+k, high = block 2p+1; n -> n - 8
-                    const uint32_t vlo = (qd[p] & 0x0F0F0F0Fu) ^ 0x08080808u;
-                    const uint32_t vhi = ((qd[p] >> 4) & 0x0F0F0F0Fu) ^ 0x08080808u;
-                    Ws[2 * p][l][row] = vlo | ((vlo & 0x08080808u) * 0x1Eu);
-                    Ws[2 * p + 1][l][row] = vhi | ((vhi & 0x08080808u) * 0x1Eu);
-                }
-                if (l == 0) {
-#pragma unroll
-                    for (int b = 0; b < 8; ++b) dws[b][row] = h2f(sd[b >> 1] >> (16 * (b & 1)));
+                for (int p = 0; p < 4; ++p) {  // nibble n -> f16(n - 8): bias 1032
+                    put(2 * p, bytes_to_f16x4(qd[p] & 0x0F0F0F0Fu, 0x64086408u));
+                    put(2 * p + 1, bytes_to_f16x4((qd[p] >> 4) & 0x0F0F0F0Fu, 0x64086408u));
                 }
             } else {
 #pragma unroll
-                for (int p = 0; p < 4; ++p) Ws[bti * 4 + p][l][row] = qd[p];
-                if (l == 0) {
+                for (int p = 0; p < 4; ++p)  // int8 q -> f16(q): byte q ^ 0x80 = q + 128, bias 1152
+                    put(bti * 4 + p, bytes_to_f16x4(qd[p] ^ 0x80808080u, 0x64806480u));
+            }
+            if (l == 0) {
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) dws[bti * 4 + b][row] = h2f(sd[b >> 1] >> (16 * (b & 1)));
-                }
+                for (int b = 0; b < BT; ++b) dws[(WT == T_Q4_0 ? 0 : bti * 4) + b][row & 1][row >> 1] = h2f(sd[b >> 1] >> (16 * (b & 1)));
             }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int rec = tid + 256 * k, tok = rec >> 4, seg = rec & 15, b = seg >> 1, l0 = (seg & 1) * 4;
-            Xs[b][l0 + 0][tok] = xr[k].x;
-            Xs[b][l0 + 1][tok] = xr[k].y;
-            Xs[b][l0 + 2][tok] = xr[k].z;
-            Xs[b][l0 + 3][tok] = xr[k].w;
+        for (int k = 0; k < XREC; ++k) {
+            const int rec = tid + 256 * k, tok = rec >> 5, seg = rec & 31;
+            *(uint4 *)(Xs + tok * XS_ROW + seg * 16) = xr[k];
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < XDA; ++k) {
             const int c = tid + 256 * k;
             das[c & 7][c >> 3] = xd[k];
         }
+    };
+    // one block's operands from LDS: A fragments (8 row pairs), B fragments, d_w (rows wr + 2*rt +
+    // (kg >> 1)) and d_a (tokens wt + 16*ct + l16)
+    struct frag { xh8 a[8]; xh8 b[XCT]; float dw[8]; float da[XCT]; };
+    auto ldfrag = [&](int b, frag &f) {
+        const uint4 *ab = a_ptr + b * a_bstride;
+#pragma unroll
+        for (int rt = 0; rt < 8; ++rt) f.a[rt] = *(const xh8 *)(ab + rt * 16);
+#pragma unroll
+        for (int ct = 0; ct < XCT; ++ct) {
+            f.b[ct] = *(const xh8 *)(Xs + (wt + ct * 16 + l16) * XS_ROW + b * 64 + kg * 16);
+            f.da[ct] = das[b][wt + ct * 16 + l16];
+        }
+        const float4 dwa = *(const float4 *)&dws[b][kg >> 1][wr / 2];
+        const float4 dwb = *(const float4 *)&dws[b][kg >> 1][wr / 2 + 4];
+        f.dw[0] = dwa.x; f.dw[1] = dwa.y; f.dw[2] = dwa.z; f.dw[3] = dwa.w;
+        f.dw[4] = dwb.x; f.dw[5] = dwb.y; f.dw[6] = dwb.z; f.dw[7] = dwb.w;
+    };
+    // all MFMAs of the block first (back-to-back on the matrix pipe), then the lane-chain fmafs
+    auto block = [&](const frag &f) {
+        xf4 dd[8][XCT];
+#pragma unroll
+        for (int rt = 0; rt < 8; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < XCT; ++ct) {
+                const xf4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+                dd[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.a[rt], f.b[ct], z, 0, 0, 0);
+            }
+#pragma unroll
+        for (int rt = 0; rt < 8; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < XCT; ++ct) {
+                const float d = f.dw[rt] * f.da[ct];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[rt][ct][v] = __builtin_fmaf(d, dd[rt][ct][v], acc[rt][ct][v]);
+            }
     };
 
     gload(0);
@@ -374,59 +452,38 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
         __syncthreads();
         if (kb0 + XKB < nb) gload(kb0 + XKB);
         const int nbs = (int)(nb - kb0 < XKB ? nb - kb0 : XKB);
+#if GHIP_XPF
+        frag cur;
+        ldfrag(0, cur);
         for (int b = 0; b < nbs; ++b) {
-            const uint4 w0 = *(const uint4 *)&Ws[b][lp][rg * XR], w1 = *(const uint4 *)&Ws[b][lp + 4][rg * XR];
-            const uint4 x0a = *(const uint4 *)&Xs[b][lp][tg * XT], x0b = *(const uint4 *)&Xs[b][lp][tg * XT + 4];
-            const uint4 x1a = *(const uint4 *)&Xs[b][lp + 4][tg * XT], x1b = *(const uint4 *)&Xs[b][lp + 4][tg * XT + 4];
-            const float4 dw4 = *(const float4 *)&dws[b][rg * XR];
-            const float4 da0 = *(const float4 *)&das[b][tg * XT], da1 = *(const float4 *)&das[b][tg * XT + 4];
-            const uint32_t wv[2][4] = {{w0.x, w0.y, w0.z, w0.w}, {w1.x, w1.y, w1.z, w1.w}};
-            const uint32_t xv[2][8] = {{x0a.x, x0a.y, x0a.z, x0a.w, x0b.x, x0b.y, x0b.z, x0b.w},
-                                       {x1a.x, x1a.y, x1a.z, x1a.w, x1b.x, x1b.y, x1b.z, x1b.w}};
-            const float dwv[4] = {dw4.x, dw4.y, dw4.z, dw4.w};
-            const float dav[8] = {da0.x, da0.y, da0.z, da0.w, da1.x, da1.y, da1.z, da1.w};
-#pragma unroll
-            for (int i = 0; i < XR; ++i)
-#pragma unroll
-                for (int j = 0; j < XT; ++j) {
-                    const float d = dwv[i] * dav[j];
-#pragma unroll
-                    for (int a = 0; a < 2; ++a) {
-                        const int s = __builtin_amdgcn_sdot4((int)wv[a][i], (int)xv[a][j], 0, false);
-                        acc[a][i][j] = __builtin_fmaf(d, (float)s, acc[a][i][j]);
-                    }
-                }
+            frag nxt;
+            ldfrag(b + 1 < nbs ? b + 1 : b, nxt);  // next block's operands in flight
+            block(cur);
+            cur = nxt;
         }
+#else
+        for (int b = 0; b < nbs; ++b) {
+            frag cur;
+            ldfrag(b, cur);
+            block(cur);
+        }
+#endif
         __syncthreads();
     }
-    // hsum: (a_lp + a_lp+4), then quad xor 2, xor 1; thread lp stores tokens 2lp, 2lp+1
+    // hsum: lane kg even holds lanes 0-3 of (row, token), lane^16 lanes 4-7
 #pragma unroll
-    for (int j = 0; j < XT; ++j) {
-        float o[XR];
+    for (int rt = 0; rt < 8; ++rt)
 #pragma unroll
-        for (int i = 0; i < XR; ++i) {
-            float v = acc[0][i][j] + acc[1][i][j];
-            v = v + dpp_f<0x4E>(v);
-            v = v + dpp_f<0xB1>(v);
-            o[i] = v;
+        for (int ct = 0; ct < XCT; ++ct) {
+            float p[4];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) p[v] = acc[rt][ct][v] + __shfl_xor(acc[rt][ct][v], 16);
+            float o = (p[0] + p[2]) + (p[1] + p[3]);
+            const int64_t t = t0 + wt + ct * 16 + l16, r = r0 + wr + 2 * rt + (kg >> 1);
+            if ((kg & 1) || t >= g.T || r >= g.rows) continue;
+            if (EPI == EPI_ADD) o = o + g.resid[t * g.ldy + r];
+            g.y[t * g.ldy + r] = o;
         }
-        const int64_t t = t0 + tg * XT + j, r = r0 + rg * XR;
-        if ((j >> 1) != lp || t >= g.T) continue;
-        float *y = g.y + t * g.ldy + r;
-        if (EPI == EPI_ADD) {
-            const float *rs = g.resid + t * g.ldy + r;
-#pragma unroll
-            for (int i = 0; i < XR; ++i)
-                if (r + i < g.rows) o[i] = o[i] + rs[i];
-        }
-        if (r + XR <= g.rows && (g.ldy & 3) == 0) {
-            *(float4 *)y = make_float4(o[0], o[1], o[2], o[3]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < XR; ++i)
-                if (r + i < g.rows) y[i] = o[i];
-        }
-    }
 }
 
 // ---- RoPE + q scale + KV store for T prompt tokens (positions p0 .. p0+T-1) --------------------
@@ -673,8 +730,8 @@ int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s) {
 }
 
 int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
-    if (g.ldq % 256 || g.nb * 32 > g.ldq || g.T <= 0 || g.rows <= 0) {
-        set_error("gemm_exact: activation image must be padded to 256 elements");
+    if (g.ldq % 256 || g.nb * 32 > g.ldq || g.T <= 0 || g.rows <= 0 || !g.xh) {
+        set_error("gemm_exact: needs the f16 activation image, padded to 256 elements");
         return -1;
     }
     const int64_t gy = (g.rows + XM - 1) / XM;
