@@ -691,6 +691,9 @@ __device__ __forceinline__ float carry_chain(const void *st_s, const float *st_d
     return carry_run<2, false>(ps, pd, total, acc);
 }
 
+#ifndef GHIP_UPRE
+#define GHIP_UPRE 4
+#endif
 // ONE_SHOT: every wave's items fit the register ring (n_items <= U): no refills in the stream loop
 template <int WT, int KS, int PRO, int EPI, int U, int R, bool NSA, bool ONE_SHOT>
 __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
@@ -769,12 +772,17 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
             }
         }
     };
+    // UPRE ring slots go out before the prologue, the rest after it: a full ring from every wave at
+    // once oversubscribes the CU's load queue and would hold the prologue behind the issue
+    constexpr int UP = GHIP_UPRE < U ? GHIP_UPRE : U;
 #pragma unroll
-    for (int u = 0; u < U; ++u) issue(qb[u], sb[u]);
+    for (int u = 0; u < UP; ++u) issue(qb[u], sb[u]);
     if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 1] = __builtin_amdgcn_s_memrealtime();
 
     // 2) activation image in LDS
     if (!(a.ablate & 1)) build_activation<WT, PRO, R, NSA>(a, col, smem, m, ar);
+#pragma unroll
+    for (int u = UP; u < U; ++u) issue(qb[u], sb[u]);
     if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 2] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
     if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 3] = __builtin_amdgcn_s_memrealtime();
