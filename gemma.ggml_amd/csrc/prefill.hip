@@ -279,8 +279,9 @@ __global__ void __launch_bounds__(256) k_gemm_q(gemm_args g) {
 // one (row, token), so one d = d_w*d_a (exact: two fp16 significands) serves 4 fmaf; the chain
 // continues block after block in the same register: the identical operation sequence, so Y is
 // bit-identical to mul_mat.  Fold: lanes 0-3 / 4-7 of a pair sit in lanes j / j^16.
-// Workgroup tile XM rows x XN tokens, 4 waves of 16 rows x 32 tokens (8 x 2 MFMA 16x16x32 per
-// block).  K is staged XKB = 8 blocks at a time: weights as pre-masked 16-B A fragments per
+// Workgroup tile XM = 32 rows x XN tokens: waves of 2*XRT rows x 16*XCT tokens (XRT x XCT MFMA
+// 16x16x32 per block; 4 x 2 measured best: the LDS fragment reads, not the MFMAs or the fmafs,
+// bound this loop).  K is staged XKB = 8 blocks at a time: weights as pre-masked 16-B A fragments per
 // (block, row, lane) (Q4_0 nibbles / Q8_0 int8 -> f16 by the 0x6400 exponent trick), tokens as
 // f16 rows (the quantizer's f16 image); the next stage's global loads are in flight during the
 // current stage's MFMAs.  blockIdx.x walks tokens so the token tiles of one weight tile run
@@ -300,19 +301,37 @@ __device__ __forceinline__ uint2 bytes_to_f16x4(uint32_t v, uint32_t bias_pair) 
 }
 
 #ifndef GHIP_XCT
-#define GHIP_XCT 1
+#define GHIP_XCT 2
 #endif
 #ifndef GHIP_XPF
 #define GHIP_XPF 0
 #endif
+#ifndef GHIP_XWAVES
+#define GHIP_XWAVES 4
+#endif
+#ifndef GHIP_XRT
+#define GHIP_XRT 4
+#endif
 constexpr int XCT = GHIP_XCT;             // 16-token MFMA column tiles per wave
-constexpr int XM = 32, XN = 32 * XCT, XKB = 8;
+constexpr int XRT = GHIP_XRT;             // 2-row MFMA row tiles per wave
+constexpr int XW = GHIP_XWAVES;           // waves per workgroup: XWR row groups x XWC token groups
+constexpr int XNT = 64 * XW;
+constexpr int XM = 32, XWR = XM / (2 * XRT), XWC = XW / XWR, XN = XWC * 16 * XCT, XKB = 8;
+static_assert(XWR * XWC == XW && XWR * 2 * XRT == XM, "wave grid");
 constexpr int XS_ROW = XKB * 32 * 2 + 16;  // bytes per staged token row (f16, padded)
-constexpr int XREC = XN * XKB * 64 / 16 / 256;  // 16-B token records per thread per stage
-constexpr int XDA = XN * XKB / 256;             // token scales per thread per stage
+constexpr int XREC = XN * XKB * 64 / 16 / XNT;  // 16-B token records per thread per stage
+constexpr int XDA = (XN * XKB + XNT - 1) / XNT;  // token scales per thread per stage
+static_assert(XN * XKB * 64 / 16 % XNT == 0, "token records");
 
+#ifndef GHIP_XWPE
+#define GHIP_XWPE 0
+#endif
 template <int WT, int EPI>
-__global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
+__global__ void __launch_bounds__(XNT)
+#if GHIP_XWPE
+__attribute__((amdgpu_waves_per_eu(GHIP_XWPE, GHIP_XWPE)))
+#endif
+k_gemm_x(gemm_args g) {
     // A fragments: [b][row][lane] 16 B (lane l's 4 f16 in half l&1 of the fragment)
     // + a zero region the inactive lanes read at the same strides (no per-lane select)
     __shared__ __attribute__((aligned(16))) uint4 Wf[XKB * XM * 8 + 7 * 16 + 1];
@@ -320,10 +339,12 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
     __shared__ __attribute__((aligned(16))) float dws[XKB][2][XM / 2];  // [b][row & 1][row >> 1]
     __shared__ __attribute__((aligned(16))) float das[XKB][XN];
     constexpr int BT = wfmt<WT>::BT;
-    constexpr int WREC = (WT == T_Q4_0) ? 1 : 2;  // 16-B weight records per thread per stage
+    constexpr int WRECS = (WT == T_Q4_0) ? 256 : 512;  // 16-B weight records per stage
+    constexpr int WREC = (WRECS + XNT - 1) / XNT;      // per thread
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, kg = lane >> 4;
-    const int wr = (wave & 1) * 16, wt = (wave >> 1) * 16 * XCT;  // wave tile: rows wr.., tokens wt..
+    const int wr = (wave % XWR) * 2 * XRT, wt = (wave / XWR) * 16 * XCT;  // wave tile: rows wr.., tokens wt..
+    static_assert(XNT % 64 == 0, "waves");
     const int64_t t0 = (int64_t)blockIdx.x * XN, r0 = (int64_t)blockIdx.y * XM;
     const int64_t n_rt = g.n_rt, n_bt = g.n_bt, nb = g.nb;
     // this lane's A fragment: MFMA row l16 = (weight row wr + 2*rt + (l16 >> 3), lane l16 & 7);
@@ -331,9 +352,9 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
     const bool a_act = ((l16 & 7) >> 1) == kg;
     const uint4 *a_ptr = a_act ? &Wf[(wr + (l16 >> 3)) * 8 + (l16 & 7)] : &Wf[XKB * XM * 8];
     const int a_bstride = a_act ? XM * 8 : 0;
-    for (int i = tid; i < 7 * 16 + 1; i += 256) Wf[XKB * XM * 8 + i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = tid; i < 7 * 16 + 1; i += XNT) Wf[XKB * XM * 8 + i] = make_uint4(0u, 0u, 0u, 0u);
 
-    float acc[8][XCT][4];
+    float acc[XRT][XCT][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -341,32 +362,34 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
 #pragma unroll
             for (int v = 0; v < 4; ++v) acc[i][j][v] = 0.0f;
 
-    uint4 wq[WREC], ws[WREC], xr[XREC];
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    u4v wq[WREC], ws[WREC], xr[XREC];
     float xd[XDA];
     auto gload = [&](int64_t kb0) {
 #pragma unroll
         for (int k = 0; k < WREC; ++k) {
-            const int rec = tid + 256 * k, tile_i = rec >> 6, ln = rec & 63, rr = ln >> 3;
-            const int rti = (WT == T_Q4_0) ? tile_i : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
+            const int rec = tid + XNT * k, tile_i = (rec >> 6) & 7, ln = rec & 63, rr = ln >> 3;
+            if (rec >= WRECS) break;  // wave-uniform
+            const int rti = (WT == T_Q4_0) ? (tile_i & 3) : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
             int64_t rt = r0 / 8 + rti, bt = kb0 / BT + bti;
             const bool ok = rt < n_rt && bt < n_bt;
             rt = ok ? rt : 0;
             bt = ok ? bt : 0;
-            wq[k] = *(const uint4 *)(g.qs + (rt * n_bt + bt) * 1024 + ln * 16);
+            wq[k] = *(const u4v *)(g.qs + (rt * n_bt + bt) * 1024 + ln * 16);
             const uint8_t *sp = g.sc + ((rt * n_bt + bt) * 8 + rr) * wfmt<WT>::SCALE_BYTES;
-            if (WT == T_Q4_0) ws[k] = *(const uint4 *)sp;
-            else { const uint2 s2 = *(const uint2 *)sp; ws[k] = make_uint4(s2.x, s2.y, 0u, 0u); }
-            if (!ok) { wq[k] = make_uint4(0u, 0u, 0u, 0u); ws[k] = make_uint4(0u, 0u, 0u, 0u); }
+            if (WT == T_Q4_0) ws[k] = *(const u4v *)sp;
+            else { const uint2 s2 = *(const uint2 *)sp; ws[k] = u4v{s2.x, s2.y, 0u, 0u}; }
+            if (!ok) { wq[k] = u4v{0u, 0u, 0u, 0u}; ws[k] = u4v{0u, 0u, 0u, 0u}; }
         }
 #pragma unroll
         for (int k = 0; k < XREC; ++k) {  // XN tokens x 512 B in 16-B records
-            const int rec = tid + 256 * k, tok = rec >> 5, seg = rec & 31;
+            const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
             const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
-            xr[k] = *(const uint4 *)(g.xh + t * g.ldq + kb0 * 32 + seg * 8);
+            xr[k] = *(const u4v *)(g.xh + t * g.ldq + kb0 * 32 + seg * 8);
         }
 #pragma unroll
         for (int k = 0; k < XDA; ++k) {
-            const int c = tid + 256 * k, tok = c >> 3, b = c & 7;
+            const int c = (tid + XNT * k) % (XN * 8), tok = c >> 3, b = c & 7;
             const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
             xd[k] = (kb0 + b < nb) ? g.da[t * g.ldd + kb0 + b] : 0.0f;
         }
@@ -374,8 +397,9 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
     auto lstore = [&]() {
 #pragma unroll
         for (int k = 0; k < WREC; ++k) {
-            const int rec = tid + 256 * k, tile_i = rec >> 6, ln = rec & 63, rr = ln >> 3, l = ln & 7;
-            const int rti = (WT == T_Q4_0) ? tile_i : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
+            const int rec = tid + XNT * k, tile_i = (rec >> 6) & 7, ln = rec & 63, rr = ln >> 3, l = ln & 7;
+            if (rec >= WRECS) break;  // wave-uniform
+            const int rti = (WT == T_Q4_0) ? (tile_i & 3) : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
             const int row = rti * 8 + rr;
             const uint32_t qd[4] = {wq[k].x, wq[k].y, wq[k].z, wq[k].w};
             const uint32_t sd[4] = {ws[k].x, ws[k].y, ws[k].z, ws[k].w};
@@ -400,44 +424,45 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
         }
 #pragma unroll
         for (int k = 0; k < XREC; ++k) {
-            const int rec = tid + 256 * k, tok = rec >> 5, seg = rec & 31;
-            *(uint4 *)(Xs + tok * XS_ROW + seg * 16) = xr[k];
+            const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
+            *(u4v *)(Xs + tok * XS_ROW + seg * 16) = xr[k];
         }
 #pragma unroll
         for (int k = 0; k < XDA; ++k) {
-            const int c = tid + 256 * k;
-            das[c & 7][c >> 3] = xd[k];
+            const int c = tid + XNT * k;
+            if (c < XN * 8) das[c & 7][c >> 3] = xd[k];
         }
     };
     // one block's operands from LDS: A fragments (8 row pairs), B fragments, d_w (rows wr + 2*rt +
     // (kg >> 1)) and d_a (tokens wt + 16*ct + l16)
-    struct frag { xh8 a[8]; xh8 b[XCT]; float dw[8]; float da[XCT]; };
+    struct frag { xh8 a[XRT]; xh8 b[XCT]; float dw[XRT]; float da[XCT]; };
     auto ldfrag = [&](int b, frag &f) {
         const uint4 *ab = a_ptr + b * a_bstride;
 #pragma unroll
-        for (int rt = 0; rt < 8; ++rt) f.a[rt] = *(const xh8 *)(ab + rt * 16);
+        for (int rt = 0; rt < XRT; ++rt) f.a[rt] = *(const xh8 *)(ab + rt * 16);
 #pragma unroll
         for (int ct = 0; ct < XCT; ++ct) {
             f.b[ct] = *(const xh8 *)(Xs + (wt + ct * 16 + l16) * XS_ROW + b * 64 + kg * 16);
             f.da[ct] = das[b][wt + ct * 16 + l16];
         }
-        const float4 dwa = *(const float4 *)&dws[b][kg >> 1][wr / 2];
-        const float4 dwb = *(const float4 *)&dws[b][kg >> 1][wr / 2 + 4];
-        f.dw[0] = dwa.x; f.dw[1] = dwa.y; f.dw[2] = dwa.z; f.dw[3] = dwa.w;
-        f.dw[4] = dwb.x; f.dw[5] = dwb.y; f.dw[6] = dwb.z; f.dw[7] = dwb.w;
+#pragma unroll
+        for (int q = 0; q < XRT; q += 4) {
+            const float4 dwq = *(const float4 *)&dws[b][kg >> 1][wr / 2 + q];
+            f.dw[q] = dwq.x; f.dw[q + 1] = dwq.y; f.dw[q + 2] = dwq.z; f.dw[q + 3] = dwq.w;
+        }
     };
     // all MFMAs of the block first (back-to-back on the matrix pipe), then the lane-chain fmafs
     auto block = [&](const frag &f) {
-        xf4 dd[8][XCT];
+        xf4 dd[XRT][XCT];
 #pragma unroll
-        for (int rt = 0; rt < 8; ++rt)
+        for (int rt = 0; rt < XRT; ++rt)
 #pragma unroll
             for (int ct = 0; ct < XCT; ++ct) {
                 const xf4 z = {0.0f, 0.0f, 0.0f, 0.0f};
                 dd[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.a[rt], f.b[ct], z, 0, 0, 0);
             }
 #pragma unroll
-        for (int rt = 0; rt < 8; ++rt)
+        for (int rt = 0; rt < XRT; ++rt)
 #pragma unroll
             for (int ct = 0; ct < XCT; ++ct) {
                 const float d = f.dw[rt] * f.da[ct];
@@ -472,7 +497,7 @@ __global__ void __launch_bounds__(256) k_gemm_x(gemm_args g) {
     }
     // hsum: lane kg even holds lanes 0-3 of (row, token), lane^16 lanes 4-7
 #pragma unroll
-    for (int rt = 0; rt < 8; ++rt)
+    for (int rt = 0; rt < XRT; ++rt)
 #pragma unroll
         for (int ct = 0; ct < XCT; ++ct) {
             float p[4];
@@ -740,10 +765,10 @@ int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
         return -1;
     }
     const dim3 grid((unsigned)((g.T + XN - 1) / XN), (unsigned)gy);
-    if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_STORE>), grid, dim3(256), 0, s, g);
-    else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_ADD>), grid, dim3(256), 0, s, g);
-    else if (wtype == T_Q8_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_STORE>), grid, dim3(256), 0, s, g);
-    else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_ADD>), grid, dim3(256), 0, s, g);
+    if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_STORE>), grid, dim3(XNT), 0, s, g);
+    else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_ADD>), grid, dim3(XNT), 0, s, g);
+    else if (wtype == T_Q8_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_STORE>), grid, dim3(XNT), 0, s, g);
+    else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_ADD>), grid, dim3(XNT), 0, s, g);
     else {
         set_error("gemm_exact: unsupported (type, epilogue)");
         return -1;
