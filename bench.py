@@ -14,6 +14,7 @@ Gemma-2B decode stream per GPU (weak scaling: tokens over all ranks / max-over-r
 the N GPUs and RCCL all-gathers (strong scaling of one stream).  Rank 0 prints ONE JSON line.
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -200,6 +201,15 @@ def main():
         prefill["tok_s"] = prefill["exact"]["tok_s"]
         prefill["ms"] = prefill["exact"]["ms"]
 
+    # K-quant leg: Q4_K / Q6_K x Q8_K matvec alone at Gemma-2B shapes, cold weights
+    kquant = {}
+    for t, name in ((G.GGML_TYPE_Q4_K, "q4_K"), (G.GGML_TYPE_Q6_K, "q6_K")):
+        for rows, K, nm in ((16384, 2048, "gate"), (2048, 16384, "down"), (256000, 2048, "output")):
+            ab = C.c_double()
+            us = G.lib().gemma_kq_time(t, rows, K, 30, C.byref(ab))
+            if us > 0:
+                kquant[f"{name}_{nm}"] = {"us": round(us, 3), "GB/s": round(ab.value / us / 1e3, 1)}
+
     # roofline leg: each hot matvec timed alone with hipEvents on the engine stream
     kern = {}
     for k in (0, 1, 2, 3, 4):
@@ -241,6 +251,7 @@ def main():
             "decode_tok_s": round(n_tok / dt, 2),
             "prefill_tok_s": prefill["tok_s"] if prefill else None,
             "prefill": prefill,
+            "kquant_matvec": kquant,
             "tp_decode": tp,
             "launch_plan": {k: ({"k_split": v[0], "rows_per_wg": v[1], "image": v[2]} if isinstance(v, tuple) else
                                 ("split" if v else "per_head")) for k, v in plan.items()},

@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -42,6 +43,7 @@ struct hpc_state {
     int device = 0;
     hipStream_t stream = nullptr;
     std::map<weight_key, tiled_mat> weights;
+    std::map<weight_key, uint8_t *> raw_weights;  // K-quants: ggml row-major super-blocks, packed rows
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
     void *host_stage = nullptr;
@@ -101,6 +103,27 @@ const tiled_mat *get_weight(const weight_key &k) {
     return &(s.weights[k] = m);
 }
 
+// K-quant rows (Q4_K 144 B / Q6_K 210 B per 256 values) stay in ggml layout, rows packed
+int64_t kq_row_bytes(int type, int64_t ne00) { return ne00 / 256 * (type == T_Q4_K ? 144 : 210); }
+
+const uint8_t *get_raw_weight(const weight_key &k) {
+    hpc_state &s = st();
+    auto it = s.raw_weights.find(k);
+    if (it != s.raw_weights.end()) return it->second;
+    const int64_t row_bytes = kq_row_bytes(k.type, k.ne00);
+    uint8_t *dev = nullptr;
+    if (hipMalloc(&dev, (size_t)(row_bytes * k.ne01)) != hipSuccess) {
+        set_error("mul_mat: weight upload alloc failed");
+        return nullptr;
+    }
+    if (hipMemcpy2D(dev, row_bytes, k.host, k.nb01, row_bytes, k.ne01, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(dev);
+        set_error("mul_mat: weight upload failed");
+        return nullptr;
+    }
+    return s.raw_weights[k] = dev;
+}
+
 }  // namespace
 
 extern "C" int hpc_init(int device) {
@@ -121,6 +144,8 @@ extern "C" void hpc_shutdown(void) {
     if (!s.inited) return;
     for (auto &kv : s.weights) free_tiled(kv.second);
     s.weights.clear();
+    for (auto &kv : s.raw_weights) (void)hipFree(kv.second);
+    s.raw_weights.clear();
     if (s.scratch) (void)hipFree(s.scratch);
     if (s.host_stage) (void)hipHostFree(s.host_stage);
     s.scratch = s.host_stage = nullptr;
@@ -142,7 +167,7 @@ extern "C" int hpc_last_error(char *buf, size_t len) {
 
 extern "C" void hpc_set_error_mode(int exit_on_error) { st().exit_on_error = exit_on_error; }
 
-extern "C" int hpc_weight_cache_entries(void) { return (int)st().weights.size(); }
+extern "C" int hpc_weight_cache_entries(void) { return (int)(st().weights.size() + st().raw_weights.size()); }
 
 extern "C" void hpc_set_matvec_ks(int ks) { st().ks = ks > 0 ? ks : 1; }
 
@@ -150,6 +175,13 @@ extern "C" int hpc_register_weight(const void *host, int type, int64_t ne00, int
     hpc_state &s = st();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (hpc_init(s.device)) return -1;
+    if (type == T_Q4_K || type == T_Q6_K) {
+        if (ne00 % 256) {
+            set_error("hpc_register_weight: K-quant rows need ne00 % 256 == 0");
+            return -1;
+        }
+        return get_raw_weight({host, type, ne00, ne01, nb01}) ? 0 : -1;
+    }
     if ((type != T_Q4_0 && type != T_Q8_0) || ne00 % 32) {
         set_error("hpc_register_weight: unsupported type/shape");
         return -1;
@@ -192,6 +224,22 @@ extern "C" void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, 
         while (ks > 1 && (W->n_bt % ks || matvec_lds_bytes(type, ks, W->n_bt, W->n_bt / ks) > 160 * 1024)) ks >>= 1;
         const int grid = ks > 1 ? (int)std::min<int64_t>(W->n_rt, 1024) : (int)std::min<int64_t>((W->n_rt + 3) / 4, 1024);
         if (launch_matvec(type, ks, PRO_Q8, EPI_STORE, a, grid, s.stream)) return fail(last_error());
+    } else if (type == T_Q4_K || type == T_Q6_K) {
+        // vec_dot_type Q8_K: wdata holds col_num Q8_K rows (row_size = K/256 * 292 bytes)
+        if (shared_edge % 256 || row_size != (size_t)(shared_edge / 256 * 292))
+            return fail("K-quant mul_mat needs shared_edge % 256 == 0 and Q8_K wdata rows");
+        const uint8_t *W = get_raw_weight({src0->data, type, shared_edge, ne01, (size_t)nb01});
+        if (!W) return fail(last_error());
+        if (ensure_scratch(dst_bytes + w_bytes + 256)) return fail(last_error());
+        dev_dst = (float *)s.scratch;
+        dev_w = (const char *)s.scratch + ((dst_bytes + 255) & ~(size_t)255);
+        if (hipMemcpyAsync((void *)dev_w, wdata, w_bytes, hipMemcpyHostToDevice, s.stream) != hipSuccess)
+            return fail("mul_mat: wdata upload failed");
+        kq_args a;
+        a.w = W; a.row_bytes = kq_row_bytes(type, shared_edge); a.rows = ne01; a.nsb = (int)(shared_edge / 256);
+        a.x = (const uint8_t *)dev_w; a.x_col_stride = (int64_t)row_size;
+        a.y = dev_dst; a.y_col_stride = ne01; a.ncols = (int)col_num;
+        if (launch_matvec_kq(type, a, s.stream)) return fail(last_error());
     } else if (type == T_F16) {
         // src0 (e.g. a KV-cache view) changes between calls: upload the ne01 rows every time
         const size_t K = (size_t)shared_edge;
@@ -284,4 +332,55 @@ extern "C" int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, con
 extern "C" int gemma_test_gemm_exact(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X,
                                      float *Y, int8_t *xq_out, float *da_out) {
     return test_gemm(true, type, rows, K, T, W, X, Y, xq_out, da_out);
+}
+
+// ---- K-quant matvec timing (bench.py): random bytes of the right shape, `iters` launches timed
+// with hipEvents on one stream; returns avg µs and the algorithmic bytes per launch
+extern "C" double gemma_kq_time(int type, int64_t rows, int64_t K, int iters, double *algo_bytes) {
+    set_error("");
+    if ((type != T_Q4_K && type != T_Q6_K) || K % 256 || rows <= 0 || iters <= 0) {
+        set_error("gemma_kq_time: bad arguments");
+        return -1.0;
+    }
+    const int64_t rb = kq_row_bytes(type, K), nsb = K / 256;
+    const size_t wbytes = (size_t)(rb * rows);
+    // rotate over enough copies that each launch reads cold weights (> the 256 MiB Infinity Cache)
+    const int copies = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)(768ull << 20) / (int64_t)wbytes));
+    uint8_t *w = nullptr, *x = nullptr;
+    float *y = nullptr;
+    if (hipMalloc(&w, wbytes * copies) != hipSuccess || hipMalloc(&x, (size_t)nsb * 292) != hipSuccess ||
+        hipMalloc(&y, (size_t)rows * 4) != hipSuccess) {
+        set_error("gemma_kq_time: alloc failed");
+        return -1.0;
+    }
+    // valid-looking data: bytes 0x11 with small fp16 scales (value does not change the timing)
+    (void)hipMemset(w, 0x11, wbytes * copies);
+    (void)hipMemset(x, 0x01, (size_t)nsb * 292);
+    hipStream_t s;
+    (void)hipStreamCreate(&s);
+    kq_args a;
+    a.row_bytes = rb; a.rows = rows; a.nsb = (int)nsb; a.x = x; a.x_col_stride = nsb * 292; a.y = y; a.y_col_stride = rows;
+    int r = 0;
+    for (int i = 0; i < 3 && !r; ++i) { a.w = w + (size_t)(i % copies) * wbytes; r = launch_matvec_kq(type, a, s); }
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, s);
+    for (int i = 0; i < iters && !r; ++i) {
+        a.w = w + (size_t)(i % copies) * wbytes;
+        r = launch_matvec_kq(type, a, s);
+    }
+    (void)hipEventRecord(e1, s);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(s);
+    (void)hipFree(w);
+    (void)hipFree(x);
+    (void)hipFree(y);
+    if (r) return -1.0;
+    if (algo_bytes) *algo_bytes = (double)wbytes + (double)nsb * 292 + (double)rows * 4;
+    return (double)ms * 1e3 / iters;
 }

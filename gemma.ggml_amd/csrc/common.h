@@ -15,7 +15,7 @@
 namespace ghip {
 
 // ggml type ids (GGUF numbering)
-enum : int { T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q8_0 = 8 };
+enum : int { T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q8_0 = 8, T_Q4_K = 12, T_Q6_K = 14, T_Q8_K = 15 };
 
 // ggml on-disk/host block formats
 struct block_q4_0 { uint16_t d; uint8_t qs[16]; };

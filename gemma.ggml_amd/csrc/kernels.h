@@ -55,6 +55,19 @@ struct mv_args {
 int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int grid_x, hipStream_t s);
 size_t matvec_lds_bytes(int wtype, int ks, int64_t n_bt, int64_t segment_tiles);
 
+// ---- K-quant matvec (kquant.hip) -----------------------------------------------------------------
+struct kq_args {  // y[c][r] = vec_dot_{q4_K,q6_K}_q8_K(row r of w, column c of x), ggml AVX2 lane order
+    const uint8_t *w = nullptr;   // ggml row-major super-blocks, row_bytes per row
+    int64_t row_bytes = 0, rows = 0;
+    int nsb = 0;                  // super-blocks per row (K / 256)
+    const uint8_t *x = nullptr;   // Q8_K columns (292 B per super-block), x_col_stride bytes apart
+    int64_t x_col_stride = 0;
+    float *y = nullptr;
+    int64_t y_col_stride = 0;     // floats between output columns
+    int ncols = 1;
+};
+int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s);
+
 // ---- prefill (prefill.hip) ----------------------------------------------------------------------
 enum qrow_mode { QR_F32 = 0, QR_NORM = 1, QR_EMBED_NORM = 2, QR_GELU = 3 };
 struct qrow_args {  // T rows of K floats -> Q8_0 image q [T][ldq] int8 + da [T][ldd] (f32 of fp16 d)

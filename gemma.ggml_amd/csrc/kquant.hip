@@ -1,0 +1,201 @@
+// kquant.hip — K-quant matvec on gfx950: Q4_K / Q6_K weights
+// (ggml row-major super-blocks, 144 / 210 B per 256 values; src/kernals.cl:13-34) against a Q8_K
+// activation column (ggml's INIT for K-quant src0: 292 B per 256 values).
+//
+// Numerics = ggml's AVX2 vec_dot_q4_K_q8_K / vec_dot_q6_K_q8_K lane order (restated in
+// oracle/kquants_cpu.cpp): one thread is one AVX2 lane l of one row; per super-block it forms the
+// lane's exact int32 sum over bytes 4l..4l+3 of every 32-value chunk (v_dot4_i32_i8 per chunk,
+// times the chunk's integer scale), then acc = fmaf(y.d*f16(x.d), (float)isum, acc).  Q4_K adds
+// the mins term in lanes 0..3 (fmaf(-y.d*f16(x.dmin), (float)(m·S), accm)); the result is
+// hsum_float_8(acc) + ((m0+m2)+(m1+m3)), folded with DPP like the Q4_0 path.
+// Bound: HBM (weights read once); 8 rows x 8 lanes per wave, the Q8_K column staged in LDS.
+#include <algorithm>
+
+#include "device_util.h"
+#include "kernels.h"
+
+namespace ghip {
+namespace {
+
+constexpr int KQ_THREADS = 256;
+
+__device__ __forceinline__ int sdot4k(uint32_t a, uint32_t b) { return __builtin_amdgcn_sdot4((int)a, (int)b, 0, false); }
+
+// a dword at a 2-byte aligned address (Q6_K blocks are 210 B: odd blocks start 2 mod 4)
+__device__ __forceinline__ uint32_t ld_u32_a2(const uint8_t *p) {
+    const uint16_t *h = (const uint16_t *)p;
+    return (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+}
+
+// one super-block s of row `wrow` for AVX2 lane l: the lane's exact int32 sum and the fp32 scale
+// d = y.d*f16(x.d); Q4_K also the mins lane k = l & 3 (meaningful in lanes 0..3): prod and dmin
+struct kq_term { int sumi; float d; int prod; float dmin; };
+
+template <int WT>
+__device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *xs, int s, int l) {
+    kq_term t;
+    const uint8_t *xb = xs + s * 292;
+    const float yd = *(const float *)xb;
+    const int8_t *q8 = (const int8_t *)(xb + 4);
+    if (WT == T_Q4_K) {
+        const uint8_t *blk = wrow + (int64_t)s * 144;
+        const uint4 h = *(const uint4 *)blk;  // d, dmin, scales[12]
+        uint32_t q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = *(const uint32_t *)(blk + 16 + 32 * j + 4 * l);
+        // six-bit scales / mins (src/kernals.cl:79-84)
+        const uint32_t u0 = h.y, u1 = h.z, u2 = h.w;
+        const uint32_t s03 = u0 & 0x3f3f3f3fu;                                      // sc 0..3
+        const uint32_t s47 = (u2 & 0x0f0f0f0fu) | (((u0 >> 6) & 0x03030303u) << 4);  // sc 4..7
+        const uint32_t m03 = u1 & 0x3f3f3f3fu;                                      // mins 0..3
+        const uint32_t m47 = ((u2 >> 4) & 0x0f0f0f0fu) | (((u1 >> 6) & 0x03030303u) << 4);
+        int sumi = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t scw = j < 2 ? s03 : s47;
+            const int sc_lo = (scw >> (16 * (j & 1))) & 0xFF, sc_hi = (scw >> (16 * (j & 1) + 8)) & 0xFF;
+            const uint32_t alo = *(const uint32_t *)(q8 + 64 * j + 4 * l);
+            const uint32_t ahi = *(const uint32_t *)(q8 + 64 * j + 32 + 4 * l);
+            sumi += sc_lo * sdot4k(q[j] & 0x0F0F0F0Fu, alo) + sc_hi * sdot4k((q[j] >> 4) & 0x0F0F0F0Fu, ahi);
+        }
+        t.sumi = sumi;
+        t.d = yd * pin(h2f(h.x));
+        t.dmin = -yd * pin(h2f(h.x >> 16));
+        const int16_t *bs = (const int16_t *)(xb + 260);
+        const int k = l & 3;
+        const int S0 = (int)bs[4 * k] + (int)bs[4 * k + 1], S1 = (int)bs[4 * k + 2] + (int)bs[4 * k + 3];
+        const uint32_t mw = k < 2 ? m03 : m47;
+        const int mn0 = (mw >> (16 * (k & 1))) & 0xFF, mn1 = (mw >> (16 * (k & 1) + 8)) & 0xFF;
+        t.prod = mn0 * S0 + mn1 * S1;
+    } else {
+        const uint8_t *blk = wrow + (int64_t)s * 210;
+        int sumi = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t qla = ld_u32_a2(blk + 64 * j + 4 * l);
+            const uint32_t qlb = ld_u32_a2(blk + 64 * j + 32 + 4 * l);
+            const uint32_t qh = ld_u32_a2(blk + 128 + 32 * j + 4 * l);
+            const uint32_t q6[4] = {(qla & 0x0F0F0F0Fu) | ((qh & 0x03030303u) << 4),
+                                    (qlb & 0x0F0F0F0Fu) | (((qh >> 2) & 0x03030303u) << 4),
+                                    ((qla >> 4) & 0x0F0F0F0Fu) | (((qh >> 4) & 0x03030303u) << 4),
+                                    ((qlb >> 4) & 0x0F0F0F0Fu) | (((qh >> 6) & 0x03030303u) << 4)};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t av = *(const uint32_t *)(q8 + 128 * j + 32 * i + 4 * l);
+                const int p = sdot4k(q6[i], av) - sdot4k(0x20202020u, av);
+                const int sc = (int)(int8_t)blk[192 + 8 * j + 2 * i + (l >> 2)];
+                sumi += sc * p;
+            }
+        }
+        t.sumi = sumi;
+        t.d = yd * pin(h2f(*(const uint16_t *)(blk + 208)));
+        t.prod = 0;
+        t.dmin = 0.0f;
+    }
+    return t;
+}
+
+__device__ __forceinline__ void stage_q8k(const kq_args &a, uint8_t *xs, int col, int tid, int nth) {
+    const uint32_t *src = (const uint32_t *)(a.x + (int64_t)col * a.x_col_stride);
+    uint32_t *dst = (uint32_t *)xs;
+    for (int i = tid; i < a.nsb * 73; i += nth) dst[i] = src[i];
+}
+
+// fold the 8 lanes (and the 4 mins lanes) of each row; lane 0 of the 8-group stores
+template <int WT>
+__device__ __forceinline__ void kq_store(const kq_args &a, int col, int64_t row_raw, int l, float acc, float accm) {
+    float v = fold8_dpp(acc);  // ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7)) in lane 0 of the 8-group
+    if (WT == T_Q4_K) v = v + quad_fold_dpp(accm);  // (m0+m2)+(m1+m3) in lane 0
+    if (l == 0 && row_raw < a.rows) a.y[(int64_t)col * a.y_col_stride + row_raw] = v;
+}
+
+template <int WT>
+__global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xs[];  // the column's Q8_K blocks
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
+    const int col = blockIdx.y;
+    stage_q8k(a, xs, col, tid, KQ_THREADS);
+    __syncthreads();
+    const int64_t n_groups = (a.rows + 7) / 8;
+    for (int64_t g = (int64_t)blockIdx.x * (KQ_THREADS / 64) + wave; g < n_groups; g += (int64_t)gridDim.x * (KQ_THREADS / 64)) {
+        const int64_t row_raw = g * 8 + rr;
+        const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;  // all lanes stay active for the folds
+        const uint8_t *wrow = a.w + row * a.row_bytes;
+        float acc = 0.0f, accm = 0.0f;
+        for (int s = 0; s < a.nsb; ++s) {
+            const kq_term t = kq_block<WT>(wrow, xs, s, l);
+            acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
+            if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
+        }
+        kq_store<WT>(a, col, row_raw, l, acc, accm);
+    }
+}
+
+// K split for tall-K / few-row shapes (e.g. ffn_down, 2048 x 16384): one row group per workgroup,
+// KS waves each take nsb/KS super-blocks.  Waves 1..KS-1 stash their exact terms (sumi, d[, prod,
+// dmin]) in LDS; wave 0 runs its own segment, then continues ITS chain through the stash in
+// super-block order — the identical fmaf sequence (the Q4_0 path's ordered carry).
+template <int WT, int KS>
+__global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
+    const int col = blockIdx.y, nsb = a.nsb, seg = nsb / KS;
+    int *st_i = (int *)(xs + nsb * 292);        // [nsb][64] lane sums
+    float *st_d = (float *)(st_i + nsb * 64);   // [nsb][8]  per-row d
+    int *st_p = (int *)(st_d + nsb * 8);        // [nsb][64] mins products (Q4_K)
+    float *st_m = (float *)(st_p + nsb * 64);   // [nsb][8]  per-row dmin (Q4_K)
+    stage_q8k(a, xs, col, tid, 64 * KS);
+    __syncthreads();
+    const int64_t row_raw = (int64_t)blockIdx.x * 8 + rr;
+    const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
+    const uint8_t *wrow = a.w + row * a.row_bytes;
+    float acc = 0.0f, accm = 0.0f;
+    for (int s = wave * seg; s < (wave + 1) * seg; ++s) {
+        const kq_term t = kq_block<WT>(wrow, xs, s, l);
+        if (wave == 0) {
+            acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
+            if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
+        } else {
+            st_i[s * 64 + lane] = t.sumi;
+            if (l == 0) st_d[s * 8 + rr] = t.d;
+            if (WT == T_Q4_K) {
+                st_p[s * 64 + lane] = t.prod;
+                if (l == 0) st_m[s * 8 + rr] = t.dmin;
+            }
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    for (int s = seg; s < nsb; ++s) {
+        acc = __builtin_fmaf(st_d[s * 8 + rr], (float)st_i[s * 64 + lane], acc);
+        if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(st_m[s * 8 + rr], (float)st_p[s * 64 + lane], accm);
+    }
+    kq_store<WT>(a, col, row_raw, l, acc, accm);
+}
+
+}  // namespace
+
+int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
+    if ((wtype != T_Q4_K && wtype != T_Q6_K) || a.nsb <= 0 || a.rows <= 0 || a.ncols <= 0 || a.x_col_stride % 4 ||
+        a.nsb * 292 > 64 * 1024) {
+        set_error("matvec_kq: unsupported type or shape");
+        return -1;
+    }
+    const int64_t groups = (a.rows + 7) / 8;
+    // few row groups and a long K: split K over 8 waves (the ordered carry keeps the fmaf chain)
+    const size_t lds_ks = (size_t)a.nsb * (292 + 64 * 4 * 2 + 8 * 4 * 2);
+    if (groups < 2048 && a.nsb % 8 == 0 && a.nsb >= 16 && lds_ks <= 64 * 1024) {
+        if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8>), dim3((unsigned)groups, a.ncols), dim3(512), lds_ks, s, a);
+        else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8>), dim3((unsigned)groups, a.ncols), dim3(512), lds_ks, s, a);
+        GHIP_CHECK(hipGetLastError());
+        return 0;
+    }
+    const unsigned grid_x = (unsigned)std::min<int64_t>((groups + 3) / 4, 4096);
+    const size_t lds = (size_t)a.nsb * 292;
+    if (wtype == T_Q4_K) hipLaunchKernelGGL(k_matvec_kq<T_Q4_K>, dim3(grid_x, a.ncols), dim3(KQ_THREADS), lds, s, a);
+    else hipLaunchKernelGGL(k_matvec_kq<T_Q6_K>, dim3(grid_x, a.ncols), dim3(KQ_THREADS), lds, s, a);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace ghip

@@ -14,12 +14,13 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GHIP_LIB") or os.path.join(PKG_DIR, "lib", "libgemma_hip.so")
 
 GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
+GGML_TYPE_Q4_K, GGML_TYPE_Q6_K, GGML_TYPE_Q8_K = 12, 14, 15
 
 # exported symbols (checked against include/gemma_hpc.h by tests/test_capi_symbols.py)
 EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
            "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
            "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
-           "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact",
+           "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact", "gemma_kq_time",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
            "gemma_engine_plan", "gemma_engine_set_plan", "gemma_hbm_read_gbs",
            "gemma_tp_unique_id", "gemma_engine_create_tp"]
@@ -100,6 +101,8 @@ def lib():
     L.gemma_engine_set_plan.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     L.gemma_engine_time.restype = C.c_double
     L.gemma_engine_time.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    L.gemma_kq_time.restype = C.c_double
+    L.gemma_kq_time.argtypes = [C.c_int, i64, i64, C.c_int, C.POINTER(C.c_double)]
     L.gemma_hbm_read_gbs.restype = C.c_double
     L.gemma_hbm_read_gbs.argtypes = [C.c_int, C.c_size_t, C.c_int]
     L.gemma_engine_sync.restype = C.c_int

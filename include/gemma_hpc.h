@@ -22,7 +22,8 @@ extern "C" {
  * Same signature and argument meaning.  dst[(c % ne1)*nb1 + (c / ne1)*nb2 + r*4] =
  * vec_dot(shared_edge, src0 + r*nb01, wdata + c*row_size) for r < ne01, c < ne11*ne12, with the
  * dot computed on the GPU in ggml's AVX2 lane order (bit-identical to the CPU path).
- * src0_type: GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 (wdata = block_q8_0 rows) or GGML_TYPE_F16
+ * src0_type: GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 (wdata = block_q8_0 rows), GGML_TYPE_Q4_K /
+ * GGML_TYPE_Q6_K (wdata = block_q8_K rows; ggml's AVX2 K-quant lane order) or GGML_TYPE_F16
  * (wdata = fp16 rows).  `vec_dot` is accepted for link compatibility and not called.
  * Quantized src0 is uploaded + re-tiled once and cached by (src0->data, shape) — weights are
  * immutable for the program's lifetime (src/gemma_model.cpp:24-27); F16 src0 (KV-cache views)
@@ -115,6 +116,9 @@ int gemma_test_gemm(int type, int64_t rows, int64_t K, int64_t T, const void *W,
 /* the same with the exact (ggml AVX2 lane order) GEMM of the exact prefill */
 int gemma_test_gemm_exact(int type, int64_t rows, int64_t K, int64_t T, const void *W, const float *X, float *Y,
                           int8_t *xq_out, float *da_out);
+/* K-quant matvec (Q4_K / Q6_K x Q8_K) timed alone: avg µs per launch over
+ * `iters` launches rotating over cold weight copies; *algo_bytes = weights + Q8_K column + y */
+double gemma_kq_time(int type, int64_t rows, int64_t K, int iters, double *algo_bytes);
 /* measured HBM read roofline: streaming read of `bytes` on `device`, `iters` passes; GB/s */
 double gemma_hbm_read_gbs(int device, size_t bytes, int iters);
 /* per-op test entry: the softmax's exp(f16) for all 65536 codes (compared with ggml's table) */

@@ -180,6 +180,9 @@ extern "C" size_t orc_row_size(int type, int64_t ne) {
         case ORC_F16: return (size_t)ne * 2;
         case ORC_Q4_0: return (size_t)(ne / 32) * 18;
         case ORC_Q8_0: return (size_t)(ne / 32) * 34;
+        case ORC_Q4_K: return (size_t)(ne / 256) * 144;
+        case ORC_Q6_K: return (size_t)(ne / 256) * 210;
+        case ORC_Q8_K: return (size_t)(ne / 256) * 292;
     }
     return 0;
 }

@@ -98,6 +98,8 @@ vec_dot_fn pick_vec_dot(int type, int avx2) {
         case ORC_Q4_0: return avx2 ? orc_vec_dot_q4_0_q8_0_avx2 : orc_vec_dot_q4_0_q8_0;
         case ORC_Q8_0: return avx2 ? orc_vec_dot_q8_0_q8_0_avx2 : orc_vec_dot_q8_0_q8_0;
         case ORC_F16: return avx2 ? f16_dot_avx2 : f16_dot_ordered;
+        case ORC_Q4_K: return avx2 ? orc_vec_dot_q4_K_q8_K_avx2 : orc_vec_dot_q4_K_q8_K;
+        case ORC_Q6_K: return avx2 ? orc_vec_dot_q6_K_q8_K_avx2 : orc_vec_dot_q6_K_q8_K;
     }
     return nullptr;
 }
@@ -154,6 +156,9 @@ extern "C" void orc_mul_mat_init(int src0_type, const float *src1, int64_t k, in
             uint16_t *o = (uint16_t *)(w + c * k * 2);
             for (int64_t i = 0; i < k; ++i) o[i] = orc_fp32_to_fp16(src1[c * col_stride_f + i]);
         }
+    } else if (src0_type == ORC_Q4_K || src0_type == ORC_Q6_K) {  // vec_dot_type Q8_K
+        const size_t rs = orc_row_size(ORC_Q8_K, k);
+        for (int64_t c = 0; c < n_cols; ++c) orc_quantize_row_q8_K(src1 + c * col_stride_f, w + c * rs, (int)k);
     } else {
         const size_t rs = orc_row_size(ORC_Q8_0, k);
         for (int64_t c = 0; c < n_cols; ++c) orc_quantize_row_q8_0(src1 + c * col_stride_f, w + c * rs, (int)k);

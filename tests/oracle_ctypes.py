@@ -14,6 +14,7 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "lib", "liboracle.so")
 
 F32, F16, Q4_0, Q8_0 = 0, 1, 2, 8
+Q4_K, Q6_K, Q8_K = 12, 14, 15
 
 
 def build():
@@ -55,6 +56,11 @@ def lib():
                "orc_vec_dot_q4_0_q8_0_avx2", "orc_vec_dot_q8_0_q8_0_avx2", "orc_vec_dot_f16_avx2"):
         getattr(L, fn).argtypes = [C.c_int, f32p, vp, vp]
     L.orc_block_lane_sums.argtypes = [C.c_int, vp, vp, vp]
+    L.orc_quantize_row_q8_K.argtypes = [vp, vp, C.c_int]
+    for fn in ("orc_vec_dot_q4_K_q8_K", "orc_vec_dot_q6_K_q8_K", "orc_vec_dot_q4_K_q8_K_avx2",
+               "orc_vec_dot_q6_K_q8_K_avx2", "orc_vec_dot_q4_K_q8_K_generic", "orc_vec_dot_q6_K_q8_K_generic"):
+        getattr(L, fn).argtypes = [C.c_int, f32p, vp, vp]
+    L.orc_synth_kquant.argtypes = [C.c_int, C.c_uint64, i64, i64, vp]
     L.orc_rms_norm.argtypes = [vp, vp, C.c_int, C.c_float]
     L.orc_soft_max_row.argtypes = [vp, vp, vp, C.c_int, C.c_float]
     L.orc_rope_neox.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_float]
@@ -106,6 +112,35 @@ def quantize(x, kind):
     return out
 
 
+KQ_BLOCK = {12: 144, 14: 210}   # Q4_K, Q6_K bytes per 256 values
+
+
+def synth_kquant(wtype, seed, rows, k):
+    """Random valid Q4_K / Q6_K blocks, [rows, k/256*bpb] bytes (ggml layout)."""
+    out = np.zeros((rows, k // 256 * KQ_BLOCK[wtype]), dtype=np.uint8)
+    lib().orc_synth_kquant(wtype, seed, rows, k, ptr(out))
+    return out
+
+
+def quantize_q8_K(x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    rows, k = x.shape
+    out = np.zeros((rows, k // 256 * 292), dtype=np.uint8)
+    for r in range(rows):
+        lib().orc_quantize_row_q8_K(ptr(x[r]), ptr(out[r]), k)
+    return out
+
+
+def vec_dot_k(wtype, wrow, arow, k, form="ordered"):
+    """form: 'ordered' (AVX2-order emulation), 'avx2', 'generic'."""
+    L = lib()
+    name = {12: "q4_K", 14: "q6_K"}[wtype]
+    sfx = {"ordered": "", "avx2": "_avx2", "generic": "_generic"}[form]
+    s = C.c_float()
+    getattr(L, f"orc_vec_dot_{name}_q8_K{sfx}")(k, C.byref(s), ptr(wrow), ptr(arow))
+    return s.value
+
+
 def vec_dot(wtype, wrow, arow, k, avx2=False):
     L = lib()
     s = C.c_float()
@@ -132,7 +167,7 @@ def mul_mat_init(src0_type, x):
     L = lib()
     x = np.ascontiguousarray(x, dtype=np.float32)
     ncols, k = x.shape
-    rs = k * 2 if src0_type == F16 else k // 32 * 34
+    rs = k * 2 if src0_type == F16 else (k // 256 * 292 if src0_type in (Q4_K, Q6_K) else k // 32 * 34)
     out = np.zeros((ncols, rs), dtype=np.uint8)
     L.orc_mul_mat_init(src0_type, ptr(x), k, ncols, k, ptr(out))
     return out, rs
