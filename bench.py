@@ -194,7 +194,7 @@ def main():
             best = min(times[1:])
             prefill[name] = {"tok_s": round(args.prefill / best, 1), "ms": round(best * 1e3, 3)}
         pe.close()
-        prefill["exact"]["path"] = ("ggml-lane-order sdot4 GEMMs + per-row exact attention; bit-identical "
+        prefill["exact"]["path"] = ("ggml AVX2 lane order: lane-masked f16 MFMA GEMMs + fmaf lane chains, per-row exact attention; bit-identical "
                                     "logits to the CPU path")
         prefill["fast"]["path"] = ("int8 MFMA GEMMs + f16 MFMA attention; fp32 order differs from the CPU "
                                    "path (DESIGN.md Prefill)")

@@ -173,7 +173,7 @@ def test_unsupported_type_reports_error():
     G.lib().hpc_set_error_mode(0)
     src = np.zeros(1024, dtype=np.uint8)
     w = np.zeros(1024, dtype=np.uint8)
-    G.mul_mat(src, 12, 4, 144, 256, w, 292, 1)  # GGML_TYPE_Q4_K: not on this path yet
+    G.mul_mat(src, 13, 4, 176, 256, w, 292, 1)  # GGML_TYPE_Q5_K: no kernel (src/hpc.cpp:132-143)
     assert "kernel is null" in G.last_error()
 
 
