@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--prefill", type=int, default=2048, help="prefill leg prompt length (0 = skip)")
     ap.add_argument("--no-tune", action="store_true", help="default launch plan instead of the measured one")
     ap.add_argument("--tp-steps", type=int, default=48, help="Gemma-7B row-split decode leg steps (0 = skip)")
+    ap.add_argument("--q8-steps", type=int, default=48, help="Gemma-2B Q8_0 decode leg steps (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,6 +176,29 @@ def main():
         except Exception as ex:  # reported, never fatal to the headline line
             tp = {"error": str(ex)[:300]}
 
+    # second quant format (BASELINE config 5): the same decode with Q8_0 weights (2.66 GB/token)
+    q8 = None
+    if args.wtype == "q4_0" and args.q8_steps > 0:
+        try:
+            qe = G.Engine(GEMMA_2B, n_ctx=args.ctx, wtype=G.GGML_TYPE_Q8_0, device=local_rank)
+            qplan = qe.tune(6) if not args.no_tune else qe.plan()
+            qe.begin(prompt)
+            qe.step(args.prompt + args.warmup, use_graph=True)
+            qe.L.gemma_engine_sync(qe.h)
+            t0 = time.perf_counter()
+            qe.step(args.q8_steps, use_graph=True)
+            qe.L.gemma_engine_sync(qe.h)
+            qdt = time.perf_counter() - t0
+            qus, qalgo = qe.time_kernel(0, args.kernel_iters)
+            qe.close()
+            q8 = {"model": "Gemma-2B Q8_0", "tok_s": round(args.q8_steps / qdt, 2),
+                  "ms_per_token": round(qdt / args.q8_steps * 1e3, 4), "steps": args.q8_steps,
+                  "token_weight_bytes": 2662727680,
+                  "gate_up_matvec": {"avg_us": round(qus, 3), "GB/s": round(qalgo / (qus * 1e-6) / 1e9, 1)},
+                  "launch_plan": qplan}
+        except Exception as ex:  # reported, never fatal to the headline line
+            q8 = {"error": str(ex)[:300]}
+
     # prefill leg (BASELINE config 3): batched prefill of a 2048-token synthetic prompt, logits for
     # every row as the reference computes them.  "exact": bit-identical to the CPU path (the
     # headline prefill_tok_s); "fast": int8/f16 MFMA, fp32 summation order differs
@@ -252,6 +276,7 @@ def main():
             "prefill_tok_s": prefill["tok_s"] if prefill else None,
             "prefill": prefill,
             "kquant_matvec": kquant,
+            "q8_0_decode": q8,
             "tp_decode": tp,
             "launch_plan": {k: ({"k_split": v[0], "rows_per_wg": v[1], "image": v[2]} if isinstance(v, tuple) else
                                 ("split" if v else "per_head")) for k, v in plan.items()},

@@ -196,3 +196,36 @@ def test_prefill_exact_mha():
 @gpu
 def test_prefill_exact_gemma2b_shapes():
     _prefill_exact_case(dict(O.GEMMA_2B), 96, 256, n_decode=2)
+
+
+@gpu
+def test_prefill_exact_full_size_equals_token_by_token():
+    """BASELINE config 3 at full size (Gemma-2B shapes, T = 2048): the batched exact prefill's
+    last-row logits, greedy token and KV cache equal the token-by-token decode path's bit for bit
+    (both are bit-exact restatements of the CPU path; a size-independent property, no oracle)."""
+    import gemma_hip as G
+    T = 2048
+    shape = dict(O.GEMMA_2B)
+    prompt = O.make_prompt(T, shape["n_vocab"])
+    a = G.Engine(shape, n_ctx=T + 64, device=0)
+    a.begin(prompt)
+    tok_a, last_a = a.prefill(T)
+    nxt_a = a.step(2, want_logits=True, use_graph=True)
+    toks_a = list(a.tokens())
+    a.close()
+    b = G.Engine(shape, n_ctx=T + 64, device=0)
+    b.begin(prompt)
+    b.step(T - 1, use_graph=True)
+    lg = b.step(1 + 2, want_logits=True, use_graph=True)  # position T-1 (prompt's last), then 2 decodes
+    toks_b = list(b.tokens())
+    b.close()
+    assert np.array_equal(last_a.view(np.uint32), lg[0].view(np.uint32))
+    assert np.array_equal(nxt_a.view(np.uint32), lg[1:].view(np.uint32))
+    assert toks_a == toks_b and toks_a[T] == tok_a
+
+
+@gpu
+def test_prefill_exact_gemma7b_layers():
+    """Gemma-7B layer shapes (E 3072, 16 q / 16 kv heads, F 24576), 3 layers, Q4_0: every row."""
+    _prefill_exact_case(dict(n_layer=3, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, n_ff=24576,
+                             n_vocab=8192), 37, 128, n_decode=2)
