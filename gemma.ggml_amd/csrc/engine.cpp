@@ -62,7 +62,7 @@ float host_f16_to_f32(uint16_t h) {
 }
 
 // ggml_init tables: exp and gelu over every fp16 pattern
-static void build_f16_tables(std::vector<uint16_t> &exp_t, std::vector<uint16_t> &gelu_t) {
+void build_f16_tables(std::vector<uint16_t> &exp_t, std::vector<uint16_t> &gelu_t) {
     exp_t.resize(65536);
     gelu_t.resize(65536);
     for (int i = 0; i < 65536; ++i) {
@@ -75,7 +75,7 @@ static void build_f16_tables(std::vector<uint16_t> &exp_t, std::vector<uint16_t>
 }
 
 // rope NEOX cos/sin: theta = (float)p, theta *= powf(base, -2/n_dims) per pair
-static void build_rope(int ctx, int hd, float base, std::vector<float> &c, std::vector<float> &s) {
+void build_rope(int ctx, int hd, float base, std::vector<float> &c, std::vector<float> &s) {
     const int half = hd / 2;
     c.resize((size_t)ctx * half);
     s.resize((size_t)ctx * half);

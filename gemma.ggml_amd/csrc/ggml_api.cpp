@@ -1,0 +1,819 @@
+// ggml_api.cpp — the ggml context / tensor / graph / op surface that src/gemma_model.cpp is written
+// against (SURVEY §8(b) "wide op surface"), implemented for MI355X so the reference's driver code
+// can build its graphs unchanged and run them on the GPU.
+//
+// Host side (this file) follows ggml's conventions: tensors carry host `data` pointers into a
+// context arena or a "CPU" backend buffer; views alias their source (view_src = the root tensor,
+// view_offs cumulative); ggml_build_forward_expand orders nodes depth-first by their sources.
+// ggml_graph_compute_with_ctx is the device executor (the hpc_graph_compute role of SURVEY §8(b)):
+//   * leaves get device mirrors: weights (tensors outside backend buffers) uploaded once per data
+//     pointer (immutable for the program, src/gemma_model.cpp:24-27); backend-buffer leaves the
+//     graph writes into (the KV cache, via ggml_cpy) are device-authoritative after their first
+//     upload; other backend-buffer leaves (tokens, positions, the mask the host writes through
+//     ->data, src/gemma_model.cpp:318-335) are re-uploaded every compute;
+//   * every node runs on the GPU in graph order (csrc/ggml_ops.hip; quantized MUL_MAT on the hot
+//     path's k_matvec for <= 4 columns and k_gemm_x otherwise, both in ggml's AVX2 lane order);
+//   * the LAST node's data is copied back to its host tensor (the one src/gemma_model.cpp:280
+//     samples from).
+// Not provided: GGUF, ops outside the Gemma graph (they fail with an error), K-quant src0 in graphs.
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/gemma_hpc.h"
+#include "kernels.h"
+
+using namespace ghip;
+
+struct ggml_context {
+    char *mem = nullptr;
+    size_t mem_size = 0, used = 0;
+    bool owns_mem = false, no_alloc = false;
+    std::vector<ggml_tensor *> tensors;
+    std::vector<ggml_cgraph *> graphs;
+};
+
+struct ggml_backend_buffer_type {
+    const char *name;
+};
+struct ggml_backend_buffer {
+    char *mem = nullptr;
+    size_t size = 0;
+    std::vector<ggml_tensor *> tensors;
+};
+
+namespace {
+
+constexpr size_t kAlign = 32;
+constexpr int kGraphSize = 8192;
+
+size_t type_size(int t) {
+    switch (t) {
+        case GGML_TYPE_F32: case GGML_TYPE_I32: return 4;
+        case GGML_TYPE_F16: case GGML_TYPE_I16: return 2;
+        case GGML_TYPE_I8: return 1;
+        case GGML_TYPE_Q4_0: return 18;
+        case GGML_TYPE_Q8_0: return 34;
+        case GGML_TYPE_Q4_K: return 144;
+        case GGML_TYPE_Q6_K: return 210;
+        case GGML_TYPE_Q8_K: return 292;
+        default: return 0;
+    }
+}
+int64_t blck_size(int t) {
+    switch (t) {
+        case GGML_TYPE_Q4_0: case GGML_TYPE_Q8_0: return 32;
+        case GGML_TYPE_Q4_K: case GGML_TYPE_Q6_K: case GGML_TYPE_Q8_K: return 256;
+        default: return 1;
+    }
+}
+
+ggml_tensor *new_tensor_impl(ggml_context *ctx, ggml_type type, int n_dims, const int64_t *ne, ggml_tensor *view_src,
+                             size_t view_offs) {
+    ggml_tensor *t = new ggml_tensor();
+    memset(t, 0, sizeof(*t));
+    t->type = type;
+    for (int i = 0; i < GGML_MAX_DIMS; ++i) t->ne[i] = i < n_dims ? ne[i] : 1;
+    t->nb[0] = type_size(type);
+    t->nb[1] = t->nb[0] * (t->ne[0] / blck_size(type));
+    for (int i = 2; i < GGML_MAX_DIMS; ++i) t->nb[i] = t->nb[i - 1] * t->ne[i - 1];
+    if (view_src && view_src->view_src) {  // views always point at the root tensor
+        view_offs += view_src->view_offs;
+        view_src = view_src->view_src;
+    }
+    t->view_src = view_src;
+    t->view_offs = view_offs;
+    if (view_src) {
+        t->data = view_src->data ? (char *)view_src->data + view_offs : nullptr;
+    } else if (!ctx->no_alloc) {
+        const size_t nbytes = ggml_nbytes(t);
+        const size_t off = (ctx->used + kAlign - 1) & ~(kAlign - 1);
+        if (off + nbytes > ctx->mem_size) {
+            fprintf(stderr, "[gemma_hip] ggml: context out of memory (%zu + %zu > %zu)\n", off, nbytes, ctx->mem_size);
+            abort();
+        }
+        t->data = ctx->mem + off;
+        ctx->used = off + nbytes;
+    }
+    ctx->tensors.push_back(t);
+    return t;
+}
+
+ggml_tensor *view_of(ggml_context *ctx, ggml_tensor *a, int n_dims, const int64_t *ne, size_t offset) {
+    return new_tensor_impl(ctx, a->type, n_dims, ne, a, offset);
+}
+
+ggml_tensor *op_result(ggml_context *ctx, ggml_tensor *like, ggml_op op, ggml_tensor *s0, ggml_tensor *s1 = nullptr,
+                       ggml_tensor *s2 = nullptr) {
+    ggml_tensor *t = new_tensor_impl(ctx, GGML_TYPE_F32, 4, like->ne, nullptr, 0);
+    t->op = op;
+    t->src[0] = s0;
+    t->src[1] = s1;
+    t->src[2] = s2;
+    return t;
+}
+
+void set_f32(ggml_tensor *t, int i, float v) { memcpy(&t->op_params[i], &v, 4); }
+float get_f32(const ggml_tensor *t, int i) {
+    float v;
+    memcpy(&v, &t->op_params[i], 4);
+    return v;
+}
+
+bool is_contiguous(const ggml_tensor *t) {
+    return t->nb[0] == type_size(t->type) && t->nb[1] == t->nb[0] * (t->ne[0] / blck_size(t->type)) &&
+           t->nb[2] == t->nb[1] * t->ne[1] && t->nb[3] == t->nb[2] * t->ne[2];
+}
+
+// ---- device executor state ------------------------------------------------------------------------
+struct leaf_mirror {
+    void *dev = nullptr;
+    size_t bytes = 0;
+    bool valid = false;  // device copy current (for device-authoritative leaves)
+};
+
+struct executor {
+    std::recursive_mutex mu;
+    bool inited = false;
+    hipStream_t stream = nullptr;
+    std::unordered_map<const void *, leaf_mirror> leaves;  // keyed by root host data pointer
+    std::map<std::pair<const void *, int>, tiled_mat> tiled;  // quantized src0 re-tiled for the hot path
+    std::unordered_set<const ggml_backend_buffer *> buffers;
+    char *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    uint16_t *gelu_tab = nullptr;
+    float *rope_c = nullptr, *rope_s = nullptr;
+    int rope_npos = 0, rope_dims = 0;
+    float rope_base = 0.f;
+};
+
+executor &ex() {
+    static executor e;
+    return e;
+}
+
+bool in_backend_buffer(const void *p) {
+    for (const ggml_backend_buffer *b : ex().buffers)
+        if ((const char *)p >= b->mem && (const char *)p < b->mem + b->size) return true;
+    return false;
+}
+
+int ensure_init() {
+    executor &e = ex();
+    if (e.inited) return 0;
+    if (hpc_init(0)) return -1;
+    GHIP_CHECK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
+    std::vector<uint16_t> et, gt;
+    build_f16_tables(et, gt);
+    GHIP_CHECK(hipMalloc(&e.gelu_tab, 65536 * 2));
+    GHIP_CHECK(hipMemcpy(e.gelu_tab, gt.data(), 65536 * 2, hipMemcpyHostToDevice));
+    e.inited = true;
+    return 0;
+}
+
+int ensure_rope(int npos, int n_dims, float base) {
+    executor &e = ex();
+    if (e.rope_c && e.rope_npos >= npos && e.rope_dims == n_dims && e.rope_base == base) return 0;
+    if (e.rope_c) (void)hipFree(e.rope_c);
+    if (e.rope_s) (void)hipFree(e.rope_s);
+    const int n = std::max(npos, 512);
+    std::vector<float> c, s;
+    build_rope(n, n_dims, base, c, s);
+    GHIP_CHECK(hipMalloc(&e.rope_c, c.size() * 4));
+    GHIP_CHECK(hipMalloc(&e.rope_s, s.size() * 4));
+    GHIP_CHECK(hipMemcpy(e.rope_c, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+    GHIP_CHECK(hipMemcpy(e.rope_s, s.data(), s.size() * 4, hipMemcpyHostToDevice));
+    e.rope_npos = n;
+    e.rope_dims = n_dims;
+    e.rope_base = base;
+    return 0;
+}
+
+ggml_tensor *root_of(ggml_tensor *t) { return t->view_src ? t->view_src : t; }
+bool is_view_op(int op) {
+    return op == GGML_OP_VIEW || op == GGML_OP_RESHAPE || op == GGML_OP_PERMUTE || op == GGML_OP_TRANSPOSE ||
+           op == GGML_OP_CPY;
+}
+
+struct run_state {
+    std::unordered_map<const ggml_tensor *, char *> node_dev;  // device base of computed roots
+    size_t scratch_used = 0;
+};
+
+int scratch_reserve(size_t bytes) {
+    executor &e = ex();
+    if (e.scratch_bytes >= bytes) return 0;
+    if (e.scratch) GHIP_CHECK(hipFree(e.scratch));
+    e.scratch = nullptr;
+    GHIP_CHECK(hipMalloc(&e.scratch, bytes));
+    e.scratch_bytes = bytes;
+    return 0;
+}
+
+char *scratch_take(run_state &rs, size_t bytes) {
+    const size_t off = (rs.scratch_used + 255) & ~(size_t)255;
+    rs.scratch_used = off + bytes;
+    return ex().scratch + off;
+}
+
+// device address of any tensor in the graph (its root's mirror + the view offset)
+char *dev_addr(run_state &rs, ggml_tensor *t) {
+    ggml_tensor *r = root_of(t);
+    const size_t off = (size_t)((char *)t->data - (char *)r->data);
+    auto it = rs.node_dev.find(r);
+    if (it != rs.node_dev.end()) return it->second + off;
+    auto lf = ex().leaves.find(r->data);
+    if (lf != ex().leaves.end()) return (char *)lf->second.dev + off;
+    return nullptr;
+}
+
+gt_desc desc(run_state &rs, ggml_tensor *t) {
+    gt_desc d;
+    d.data = dev_addr(rs, t);
+    for (int i = 0; i < 4; ++i) {
+        d.ne[i] = t->ne[i];
+        d.nb[i] = (int64_t)t->nb[i];
+    }
+    d.type = t->type;
+    return d;
+}
+
+// one leaf root: make its device mirror current
+int sync_leaf(ggml_tensor *r, bool graph_written) {
+    executor &e = ex();
+    const size_t bytes = ggml_nbytes(r);
+    leaf_mirror &m = e.leaves[r->data];
+    if (m.bytes < bytes) {
+        if (m.dev) GHIP_CHECK(hipFree(m.dev));
+        GHIP_CHECK(hipMalloc(&m.dev, bytes));
+        m.bytes = bytes;
+        m.valid = false;
+    }
+    const bool host_written_input = in_backend_buffer(r->data) && !graph_written;
+    if (!m.valid || host_written_input) {
+        GHIP_CHECK(hipMemcpyAsync(m.dev, r->data, bytes, hipMemcpyHostToDevice, e.stream));
+        m.valid = true;
+    }
+    return 0;
+}
+
+const tiled_mat *tiled_weight(run_state &rs, ggml_tensor *w) {
+    executor &e = ex();
+    ggml_tensor *r = root_of(w);
+    const auto key = std::make_pair((const void *)w->data, (int)w->type);
+    auto it = e.tiled.find(key);
+    if (it != e.tiled.end()) return &it->second;
+    if (!is_contiguous(w)) {
+        set_error("ggml mul_mat: quantized src0 must be contiguous");
+        return nullptr;
+    }
+    tiled_mat m = alloc_tiled(w->type, w->ne[1], w->ne[0], e.stream);
+    const char *src = dev_addr(rs, w);
+    if (!src || launch_repack(m, (const uint8_t *)src, (int64_t)w->nb[1], e.stream)) {
+        free_tiled(m);
+        if (!src) set_error("ggml mul_mat: src0 has no device data");
+        return nullptr;
+    }
+    (void)r;
+    return &(e.tiled[key] = m);
+}
+
+int run_mul_mat(run_state &rs, ggml_tensor *node) {
+    executor &e = ex();
+    ggml_tensor *a = node->src[0], *b = node->src[1];
+    if (b->type != GGML_TYPE_F32) {
+        set_error("ggml mul_mat: src1 must be f32");
+        return -1;
+    }
+    const int64_t K = a->ne[0], cols = b->ne[1] * b->ne[2] * b->ne[3];
+    if (a->type == GGML_TYPE_F16) {
+        // INIT: src1 -> contiguous f16 rows, then ggml_vec_dot_f16 per (row, column)
+        gt_desc b16 = desc(rs, b);
+        b16.type = T_F16;
+        b16.data = scratch_take(rs, (size_t)(K * cols * 2));
+        b16.nb[0] = 2;
+        for (int i = 1; i < 4; ++i) b16.nb[i] = b16.nb[i - 1] * b16.ne[i - 1];
+        if (launch_g_copy(desc(rs, b), b16, e.stream)) return -1;
+        if (b->ne[2] % a->ne[2] || b->ne[3] % a->ne[3] || a->nb[0] != 2) {
+            set_error("ggml mul_mat: unsupported f16 broadcast / stride");
+            return -1;
+        }
+        return launch_g_mul_mat_f16(desc(rs, a), (const uint16_t *)b16.data, K, desc(rs, node), b->ne[1], b->ne[2],
+                                    b->ne[3], e.stream);
+    }
+    if (a->type != GGML_TYPE_Q4_0 && a->type != GGML_TYPE_Q8_0) {
+        set_error("ggml mul_mat: src0 type " + std::to_string(a->type) + " not supported by the graph executor");
+        return -1;
+    }
+    if (K % 32 || a->ne[2] != 1 || a->ne[3] != 1 || b->nb[0] != 4 || b->nb[1] != (size_t)K * 4 ||
+        (cols > b->ne[1] && b->nb[2] != b->nb[1] * b->ne[1])) {
+        set_error("ggml mul_mat: quantized path needs contiguous src1 rows");
+        return -1;
+    }
+    const tiled_mat *W = tiled_weight(rs, a);
+    if (!W) return -1;
+    float *y = (float *)dev_addr(rs, node);
+    const char *x = dev_addr(rs, b);
+    if (cols <= 4) {
+        mv_args m;
+        m.qs = W->qs; m.sc = W->sc; m.rows = W->rows; m.n_rt = W->n_rt; m.n_bt = W->n_bt; m.nb = W->nb;
+        m.x = x; m.x_col_stride = (int64_t)b->nb[1];
+        m.y = y; m.y_col_stride = a->ne[1];
+        m.ncols = (int)cols;
+        const int grid = (int)std::min<int64_t>((W->n_rt + 3) / 4, 1024);
+        return launch_matvec(a->type, 1, PRO_F32, EPI_STORE, m, grid, e.stream);
+    }
+    const int64_t ldq = (K + 255) / 256 * 256, ldd = ldq / 32;
+    qrow_args q;
+    q.x = (const float *)x; q.ldx = K; q.K = K;
+    q.q = nullptr;
+    q.qh = (uint16_t *)scratch_take(rs, (size_t)(cols * ldq * 2));
+    q.ldq = ldq;
+    q.da = (float *)scratch_take(rs, (size_t)(cols * ldd * 4));
+    q.ldd = ldd;
+    if (launch_quant_rows(QR_F32, q, (int)cols, e.stream)) return -1;
+    gemm_args g;
+    g.qs = W->qs; g.sc = W->sc; g.rows = W->rows; g.n_rt = W->n_rt; g.n_bt = W->n_bt; g.nb = W->nb;
+    g.xh = q.qh; g.ldq = ldq; g.da = q.da; g.ldd = ldd; g.T = cols; g.y = y; g.ldy = a->ne[1];
+    return launch_gemm_exact(a->type, EPI_STORE, g, e.stream);
+}
+
+int run_node(run_state &rs, ggml_tensor *n) {
+    executor &e = ex();
+    hipStream_t s = e.stream;
+    switch (n->op) {
+        case GGML_OP_VIEW: case GGML_OP_RESHAPE: case GGML_OP_PERMUTE: case GGML_OP_TRANSPOSE: return 0;
+        case GGML_OP_GET_ROWS: return launch_g_get_rows(desc(rs, n->src[0]), desc(rs, n->src[1]), desc(rs, n), s);
+        case GGML_OP_SCALE: return launch_g_elementwise(0, desc(rs, n->src[0]), gt_desc(), desc(rs, n), get_f32(n, 0), nullptr, 0, s);
+        case GGML_OP_GELU: return launch_g_elementwise(1, desc(rs, n->src[0]), gt_desc(), desc(rs, n), 0.f, e.gelu_tab, n->op_params[0], s);
+        case GGML_OP_MUL: return launch_g_elementwise(2, desc(rs, n->src[0]), desc(rs, n->src[1]), desc(rs, n), 0.f, nullptr, 0, s);
+        case GGML_OP_ADD: return launch_g_elementwise(3, desc(rs, n->src[0]), desc(rs, n->src[1]), desc(rs, n), 0.f, nullptr, 0, s);
+        case GGML_OP_RMS_NORM: return launch_g_rms_norm(desc(rs, n->src[0]), desc(rs, n), get_f32(n, 0), s);
+        case GGML_OP_CPY: case GGML_OP_CONT: return launch_g_copy(desc(rs, n->src[0]), desc(rs, n), s);
+        case GGML_OP_MUL_MAT: return run_mul_mat(rs, n);
+        case GGML_OP_SOFT_MAX: {
+            ggml_tensor *mask = n->src[1];
+            if (n->src[2] || get_f32(n, 1) != 0.0f) {
+                set_error("ggml soft_max_ext: ALiBi (pos / max_bias) is not supported");
+                return -1;
+            }
+            return launch_g_soft_max(desc(rs, n->src[0]), mask ? desc(rs, mask) : gt_desc(), mask ? 1 : 0, desc(rs, n),
+                                     get_f32(n, 0), s);
+        }
+        case GGML_OP_ROPE: {
+            const int n_dims = n->op_params[1];
+            // the Gemma graph's rope: NEOX (mode 2), no YaRN extension, unit scales (src/macro.h:12-18)
+            if (n->op_params[2] != 2 || get_f32(n, 6) != 1.0f || get_f32(n, 7) != 0.0f || get_f32(n, 8) != 1.0f ||
+                n_dims > n->src[0]->ne[0] || n_dims % 2) {
+                set_error("ggml rope: only NEOX mode with freq_scale 1, ext_factor 0, attn_factor 1 is supported");
+                return -1;
+            }
+            // positions are a host-written input: size the cos/sin table from its values
+            const ggml_tensor *pos = n->src[1];
+            int maxp = 0;
+            for (int64_t i = 0; i < pos->ne[0]; ++i)
+                maxp = std::max(maxp, *(const int32_t *)((const char *)pos->data + i * pos->nb[0]));
+            if (ensure_rope(maxp + 1, n_dims, get_f32(n, 5))) return -1;
+            return launch_g_rope_neox(desc(rs, n->src[0]), desc(rs, n->src[1]), desc(rs, n), n_dims, e.rope_c, e.rope_s, s);
+        }
+        default:
+            set_error("ggml graph: op " + std::to_string(n->op) + " not supported");
+            return -1;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- context and sizes -------------------------------------------------------------------------
+struct ggml_context *ggml_init(struct ggml_init_params params) {
+    ggml_context *c = new ggml_context();
+    c->mem_size = params.mem_size;
+    c->no_alloc = params.no_alloc;
+    if (params.mem_buffer) {
+        c->mem = (char *)params.mem_buffer;
+    } else if (params.mem_size) {
+        c->mem = (char *)aligned_alloc(64, (params.mem_size + 63) & ~(size_t)63);
+        c->owns_mem = true;
+    }
+    return c;
+}
+
+void ggml_free(struct ggml_context *ctx) {
+    if (!ctx) return;
+    {
+        std::lock_guard<std::recursive_mutex> lk(ex().mu);
+        // a freed compute context's tensors leave the executor's caches keyed by their data
+        for (ggml_tensor *t : ctx->tensors) {
+            if (t->view_src || !t->data) continue;
+            auto it = ex().leaves.find(t->data);
+            if (it != ex().leaves.end() && !in_backend_buffer(t->data)) {
+                (void)hipFree(it->second.dev);
+                ex().leaves.erase(it);
+            }
+            auto tt = ex().tiled.find(std::make_pair((const void *)t->data, (int)t->type));
+            if (tt != ex().tiled.end()) {
+                free_tiled(tt->second);
+                ex().tiled.erase(tt);
+            }
+        }
+    }
+    for (ggml_tensor *t : ctx->tensors) delete t;
+    for (ggml_cgraph *g : ctx->graphs) {
+        delete[] g->nodes;
+        delete[] g->leafs;
+        delete g;
+    }
+    if (ctx->owns_mem) free(ctx->mem);
+    delete ctx;
+}
+
+size_t ggml_tensor_overhead(void) { return sizeof(struct ggml_tensor) + 32; }
+size_t ggml_graph_overhead(void) { return sizeof(struct ggml_cgraph) + 2 * kGraphSize * sizeof(void *) + 32; }
+size_t ggml_get_mem_size(const struct ggml_context *ctx) { return ctx->mem_size; }
+size_t ggml_type_size(enum ggml_type type) { return type_size(type); }
+int64_t ggml_blck_size(enum ggml_type type) { return blck_size(type); }
+size_t ggml_row_size(enum ggml_type type, int64_t ne) { return type_size(type) * ne / blck_size(type); }
+size_t ggml_element_size(const struct ggml_tensor *t) { return type_size(t->type); }
+int64_t ggml_nelements(const struct ggml_tensor *t) { return t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]; }
+size_t ggml_nbytes(const struct ggml_tensor *t) {
+    size_t nbytes = type_size(t->type);
+    if (blck_size(t->type) == 1) {
+        for (int i = 0; i < GGML_MAX_DIMS; ++i) nbytes += (size_t)(t->ne[i] - 1) * t->nb[i];
+    } else {
+        nbytes = (size_t)(t->ne[0] * t->nb[0] / blck_size(t->type));
+        for (int i = 1; i < GGML_MAX_DIMS; ++i) nbytes += (size_t)(t->ne[i] - 1) * t->nb[i];
+    }
+    return nbytes;
+}
+
+// ---- tensors and views -------------------------------------------------------------------------
+struct ggml_tensor *ggml_new_tensor(struct ggml_context *ctx, enum ggml_type type, int n_dims, const int64_t *ne) {
+    return new_tensor_impl(ctx, type, n_dims, ne, nullptr, 0);
+}
+struct ggml_tensor *ggml_new_tensor_1d(struct ggml_context *ctx, enum ggml_type type, int64_t ne0) {
+    return new_tensor_impl(ctx, type, 1, &ne0, nullptr, 0);
+}
+struct ggml_tensor *ggml_new_tensor_2d(struct ggml_context *ctx, enum ggml_type type, int64_t ne0, int64_t ne1) {
+    const int64_t ne[2] = {ne0, ne1};
+    return new_tensor_impl(ctx, type, 2, ne, nullptr, 0);
+}
+struct ggml_tensor *ggml_new_tensor_3d(struct ggml_context *ctx, enum ggml_type type, int64_t ne0, int64_t ne1,
+                                       int64_t ne2) {
+    const int64_t ne[3] = {ne0, ne1, ne2};
+    return new_tensor_impl(ctx, type, 3, ne, nullptr, 0);
+}
+struct ggml_tensor *ggml_view_1d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, size_t offset) {
+    ggml_tensor *t = view_of(ctx, a, 1, &ne0, offset);
+    t->op = GGML_OP_VIEW;
+    t->src[0] = a;
+    return t;
+}
+struct ggml_tensor *ggml_view_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1, size_t nb1,
+                                 size_t offset) {
+    const int64_t ne[2] = {ne0, ne1};
+    ggml_tensor *t = view_of(ctx, a, 2, ne, offset);
+    t->nb[1] = nb1;
+    t->nb[2] = t->nb[1] * ne1;
+    t->nb[3] = t->nb[2];
+    t->op = GGML_OP_VIEW;
+    t->src[0] = a;
+    return t;
+}
+struct ggml_tensor *ggml_view_3d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1, int64_t ne2,
+                                 size_t nb1, size_t nb2, size_t offset) {
+    const int64_t ne[3] = {ne0, ne1, ne2};
+    ggml_tensor *t = view_of(ctx, a, 3, ne, offset);
+    t->nb[1] = nb1;
+    t->nb[2] = nb2;
+    t->nb[3] = t->nb[2] * ne2;
+    t->op = GGML_OP_VIEW;
+    t->src[0] = a;
+    return t;
+}
+struct ggml_tensor *ggml_reshape_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1) {
+    const int64_t ne[2] = {ne0, ne1};
+    ggml_tensor *t = view_of(ctx, a, 2, ne, 0);
+    t->op = GGML_OP_RESHAPE;
+    t->src[0] = a;
+    return t;
+}
+struct ggml_tensor *ggml_reshape_3d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1,
+                                    int64_t ne2) {
+    const int64_t ne[3] = {ne0, ne1, ne2};
+    ggml_tensor *t = view_of(ctx, a, 3, ne, 0);
+    t->op = GGML_OP_RESHAPE;
+    t->src[0] = a;
+    return t;
+}
+struct ggml_tensor *ggml_permute(struct ggml_context *ctx, struct ggml_tensor *a, int axis0, int axis1, int axis2,
+                                 int axis3) {
+    ggml_tensor *t = view_of(ctx, a, 4, a->ne, 0);
+    const int ax[4] = {axis0, axis1, axis2, axis3};
+    for (int i = 0; i < 4; ++i) {
+        t->ne[ax[i]] = a->ne[i];
+        t->nb[ax[i]] = a->nb[i];
+    }
+    t->op = GGML_OP_PERMUTE;
+    t->src[0] = a;
+    return t;
+}
+struct ggml_tensor *ggml_transpose(struct ggml_context *ctx, struct ggml_tensor *a) {
+    ggml_tensor *t = view_of(ctx, a, 4, a->ne, 0);
+    for (int i = 0; i < 4; ++i) t->nb[i] = a->nb[i];
+    t->ne[0] = a->ne[1];
+    t->ne[1] = a->ne[0];
+    t->nb[0] = a->nb[1];
+    t->nb[1] = a->nb[0];
+    t->op = GGML_OP_TRANSPOSE;
+    t->src[0] = a;
+    return t;
+}
+struct ggml_tensor *ggml_cont_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1) {
+    const int64_t ne[2] = {ne0, ne1};
+    ggml_tensor *t = new_tensor_impl(ctx, a->type, 2, ne, nullptr, 0);
+    t->op = GGML_OP_CONT;
+    t->src[0] = a;
+    return t;
+}
+struct ggml_tensor *ggml_set_name(struct ggml_tensor *t, const char *name) {
+    snprintf(t->name, sizeof(t->name), "%s", name);
+    return t;
+}
+struct ggml_tensor *ggml_format_name(struct ggml_tensor *t, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(t->name, sizeof(t->name), fmt, ap);
+    va_end(ap);
+    return t;
+}
+const char *ggml_get_name(const struct ggml_tensor *t) { return t->name; }
+struct ggml_tensor *ggml_get_tensor(struct ggml_context *ctx, const char *name) {
+    for (ggml_tensor *t : ctx->tensors)
+        if (strcmp(t->name, name) == 0) return t;
+    return nullptr;
+}
+
+// ---- ops ---------------------------------------------------------------------------------------
+struct ggml_tensor *ggml_get_rows(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b) {
+    const int64_t ne[2] = {a->ne[0], b->ne[0]};
+    ggml_tensor *t = new_tensor_impl(ctx, GGML_TYPE_F32, 2, ne, nullptr, 0);
+    t->op = GGML_OP_GET_ROWS;
+    t->src[0] = a;
+    t->src[1] = b;
+    return t;
+}
+struct ggml_tensor *ggml_scale(struct ggml_context *ctx, struct ggml_tensor *a, float s) {
+    ggml_tensor *t = op_result(ctx, a, GGML_OP_SCALE, a);
+    set_f32(t, 0, s);
+    return t;
+}
+struct ggml_tensor *ggml_rms_norm(struct ggml_context *ctx, struct ggml_tensor *a, float eps) {
+    ggml_tensor *t = op_result(ctx, a, GGML_OP_RMS_NORM, a);
+    set_f32(t, 0, eps);
+    return t;
+}
+struct ggml_tensor *ggml_mul(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b) {
+    return op_result(ctx, a, GGML_OP_MUL, a, b);
+}
+struct ggml_tensor *ggml_add(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b) {
+    return op_result(ctx, a, GGML_OP_ADD, a, b);
+}
+struct ggml_tensor *ggml_mul_mat(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b) {
+    const int64_t ne[4] = {a->ne[1], b->ne[1], b->ne[2], b->ne[3]};
+    ggml_tensor *t = new_tensor_impl(ctx, GGML_TYPE_F32, 4, ne, nullptr, 0);
+    t->op = GGML_OP_MUL_MAT;
+    t->src[0] = a;
+    t->src[1] = b;
+    return t;
+}
+struct ggml_tensor *ggml_rope_custom(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b, int n_dims,
+                                     int mode, int n_ctx, int n_orig_ctx, float freq_base, float freq_scale,
+                                     float ext_factor, float attn_factor, float beta_fast, float beta_slow) {
+    ggml_tensor *t = op_result(ctx, a, GGML_OP_ROPE, a, b);
+    // ggml's param layout: n_past(0), n_dims, mode, n_ctx, n_orig_ctx, then the floats
+    t->op_params[0] = 0;
+    t->op_params[1] = n_dims;
+    t->op_params[2] = mode;
+    t->op_params[3] = n_ctx;
+    t->op_params[4] = n_orig_ctx;
+    set_f32(t, 5, freq_base);
+    set_f32(t, 6, freq_scale);
+    set_f32(t, 7, ext_factor);
+    set_f32(t, 8, attn_factor);
+    set_f32(t, 9, beta_fast);
+    set_f32(t, 10, beta_slow);
+    return t;
+}
+struct ggml_tensor *ggml_soft_max_ext(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *mask,
+                                      struct ggml_tensor *pos, float scale, float max_bias) {
+    ggml_tensor *t = op_result(ctx, a, GGML_OP_SOFT_MAX, a, mask, pos);
+    set_f32(t, 0, scale);
+    set_f32(t, 1, max_bias);
+    return t;
+}
+struct ggml_tensor *ggml_gelu(struct ggml_context *ctx, struct ggml_tensor *a) {
+    ggml_tensor *t = op_result(ctx, a, GGML_OP_GELU, a);
+    const char *clamp = getenv("GEMMA_HIP_GELU_CLAMP");  // later-ggml clamp variant
+    t->op_params[0] = clamp && atoi(clamp) ? 1 : 0;
+    return t;
+}
+struct ggml_tensor *ggml_cpy(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b) {
+    ggml_tensor *t = view_of(ctx, b, 4, b->ne, 0);
+    for (int i = 0; i < 4; ++i) t->nb[i] = b->nb[i];
+    t->op = GGML_OP_CPY;
+    t->src[0] = a;
+    t->src[1] = b;
+    return t;
+}
+
+// ---- graphs ------------------------------------------------------------------------------------
+struct ggml_cgraph *ggml_new_graph(struct ggml_context *ctx) {
+    ggml_cgraph *g = new ggml_cgraph();
+    g->size = kGraphSize;
+    g->nodes = new ggml_tensor *[kGraphSize];
+    g->leafs = new ggml_tensor *[kGraphSize];
+    g->grads = nullptr;
+    g->n_nodes = g->n_leafs = 0;
+    ctx->graphs.push_back(g);
+    return g;
+}
+
+static void visit(ggml_cgraph *g, std::unordered_set<ggml_tensor *> &seen, ggml_tensor *t) {
+    if (!t || seen.count(t)) return;
+    seen.insert(t);
+    for (int i = 0; i < GGML_MAX_SRC; ++i) visit(g, seen, t->src[i]);
+    if (t->op == GGML_OP_NONE) {
+        if (g->n_leafs < g->size) g->leafs[g->n_leafs++] = t;
+    } else {
+        if (g->n_nodes >= g->size) {
+            fprintf(stderr, "[gemma_hip] ggml: graph full\n");
+            abort();
+        }
+        g->nodes[g->n_nodes++] = t;
+    }
+}
+
+void ggml_build_forward_expand(struct ggml_cgraph *g, struct ggml_tensor *t) {
+    std::unordered_set<ggml_tensor *> seen;
+    for (int i = 0; i < g->n_nodes; ++i) seen.insert(g->nodes[i]);
+    for (int i = 0; i < g->n_leafs; ++i) seen.insert(g->leafs[i]);
+    visit(g, seen, t);
+}
+
+enum ggml_status ggml_graph_compute_with_ctx(struct ggml_context *ctx, struct ggml_cgraph *g, int n_threads) {
+    (void)ctx;
+    (void)n_threads;
+    executor &e = ex();
+    std::lock_guard<std::recursive_mutex> lk(e.mu);
+    set_error("");
+    if (ensure_init()) return GGML_STATUS_FAILED;
+    if (g->n_nodes == 0) return GGML_STATUS_SUCCESS;
+    // leaves the graph writes into (ggml_cpy destinations): device-authoritative
+    std::unordered_set<const void *> written;
+    for (int i = 0; i < g->n_nodes; ++i)
+        if (g->nodes[i]->op == GGML_OP_CPY) written.insert(root_of(g->nodes[i]->src[1])->data);
+    // leaf roots (graph leaves, and the roots of views over them)
+    std::vector<ggml_tensor *> roots;
+    std::unordered_set<ggml_tensor *> node_set(g->nodes, g->nodes + g->n_nodes), seen;
+    auto add_root = [&](ggml_tensor *t) {
+        ggml_tensor *r = root_of(t);
+        if (!node_set.count(r) && !seen.count(r)) {
+            seen.insert(r);
+            roots.push_back(r);
+        }
+    };
+    for (int i = 0; i < g->n_leafs; ++i) add_root(g->leafs[i]);
+    for (int i = 0; i < g->n_nodes; ++i) {
+        if (g->nodes[i]->view_src) add_root(g->nodes[i]);
+        for (int k = 0; k < GGML_MAX_SRC; ++k)
+            if (g->nodes[i]->src[k]) add_root(g->nodes[i]->src[k]);
+    }
+    for (ggml_tensor *r : roots) {
+        if (!r->data) {
+            set_error("ggml graph: leaf tensor without data");
+            return GGML_STATUS_FAILED;
+        }
+        if (sync_leaf(r, written.count(r->data) > 0)) return GGML_STATUS_FAILED;
+    }
+    // device memory for computed roots, plus per-op scratch
+    size_t need = 0;
+    for (int i = 0; i < g->n_nodes; ++i)
+        if (!g->nodes[i]->view_src) need += (ggml_nbytes(g->nodes[i]) + 255) & ~(size_t)255;
+    size_t extra = 0;
+    for (int i = 0; i < g->n_nodes; ++i) {
+        const ggml_tensor *n = g->nodes[i];
+        if (n->op == GGML_OP_MUL_MAT) {
+            const int64_t K = n->src[0]->ne[0], cols = n->src[1]->ne[1] * n->src[1]->ne[2] * n->src[1]->ne[3];
+            const int64_t ldq = (K + 255) / 256 * 256;
+            extra = std::max<size_t>(extra, (size_t)(cols * ldq * 2 + cols * ldq / 8 + cols * K * 2 + 1024));
+        }
+    }
+    if (scratch_reserve(need + extra + 4096)) return GGML_STATUS_ALLOC_FAILED;
+    run_state rs;
+    for (int i = 0; i < g->n_nodes; ++i)
+        if (!g->nodes[i]->view_src) rs.node_dev[g->nodes[i]] = scratch_take(rs, ggml_nbytes(g->nodes[i]));
+    const size_t node_end = rs.scratch_used;
+    for (int i = 0; i < g->n_nodes; ++i) {
+        rs.scratch_used = node_end;  // per-op scratch is reused node after node
+        if (run_node(rs, g->nodes[i])) return GGML_STATUS_FAILED;
+    }
+    for (const void *w : written) ex().leaves[w].valid = true;
+    // the last node back to the host (what src/gemma_model.cpp:280 reads)
+    ggml_tensor *last = g->nodes[g->n_nodes - 1];
+    if (last->data) {
+        const char *src = dev_addr(rs, last);
+        if (!is_contiguous(last)) {
+            set_error("ggml graph: last node not contiguous");
+            return GGML_STATUS_FAILED;
+        }
+        if (hipMemcpyAsync(last->data, src, ggml_nbytes(last), hipMemcpyDeviceToHost, e.stream) != hipSuccess)
+            return GGML_STATUS_FAILED;
+    }
+    if (hipStreamSynchronize(e.stream) != hipSuccess) {
+        set_error("ggml graph: device error");
+        return GGML_STATUS_FAILED;
+    }
+    return GGML_STATUS_SUCCESS;
+}
+
+// ---- backend ("CPU" buffers in host memory, mirrored by the executor) ---------------------------
+static ggml_backend_buffer_type g_cpu_buft = {"CPU"};
+ggml_backend_buffer_type_t ggml_backend_cpu_buffer_type(void) { return &g_cpu_buft; }
+
+ggml_backend_buffer_t ggml_backend_alloc_ctx_tensors_from_buft(struct ggml_context *ctx, ggml_backend_buffer_type_t buft) {
+    (void)buft;
+    size_t total = 0;
+    for (ggml_tensor *t : ctx->tensors)
+        if (!t->data && !t->view_src) total += (ggml_nbytes(t) + kAlign - 1) & ~(kAlign - 1);
+    ggml_backend_buffer *b = new ggml_backend_buffer();
+    b->size = total;
+    b->mem = (char *)aligned_alloc(64, (total + 63) & ~(size_t)63);
+    size_t off = 0;
+    for (ggml_tensor *t : ctx->tensors) {
+        if (t->data || t->view_src) continue;
+        t->data = b->mem + off;
+        off += (ggml_nbytes(t) + kAlign - 1) & ~(kAlign - 1);
+        b->tensors.push_back(t);
+    }
+    for (ggml_tensor *t : ctx->tensors)
+        if (t->view_src && !t->data && t->view_src->data) t->data = (char *)t->view_src->data + t->view_offs;
+    std::lock_guard<std::recursive_mutex> lk(ex().mu);
+    ex().buffers.insert(b);
+    return b;
+}
+
+void ggml_backend_buffer_clear(ggml_backend_buffer_t b, uint8_t value) {
+    memset(b->mem, value, b->size);
+    std::lock_guard<std::recursive_mutex> lk(ex().mu);
+    for (ggml_tensor *t : b->tensors) {  // device mirrors re-upload from the cleared host copy
+        auto it = ex().leaves.find(t->data);
+        if (it != ex().leaves.end()) it->second.valid = false;
+    }
+}
+const char *ggml_backend_buffer_name(ggml_backend_buffer_t b) {
+    (void)b;
+    return "CPU (MI355X-mirrored)";
+}
+size_t ggml_backend_buffer_get_size(ggml_backend_buffer_t b) { return b->size; }
+void ggml_backend_buffer_free(ggml_backend_buffer_t b) {
+    if (!b) return;
+    std::lock_guard<std::recursive_mutex> lk(ex().mu);
+    for (ggml_tensor *t : b->tensors) {
+        auto it = ex().leaves.find(t->data);
+        if (it != ex().leaves.end()) {
+            (void)hipFree(it->second.dev);
+            ex().leaves.erase(it);
+        }
+    }
+    ex().buffers.erase(b);
+    free(b->mem);
+    delete b;
+}
+
+void ggml_backend_tensor_set(struct ggml_tensor *t, const void *data, size_t offset, size_t size) {
+    memcpy((char *)t->data + offset, data, size);
+    std::lock_guard<std::recursive_mutex> lk(ex().mu);
+    ggml_tensor *r = root_of(t);
+    auto it = ex().leaves.find(r->data);
+    if (it != ex().leaves.end() && it->second.valid) {  // keep a device-authoritative mirror current
+        const size_t off = (size_t)((char *)t->data - (char *)r->data) + offset;
+        if (hipMemcpy((char *)it->second.dev + off, data, size, hipMemcpyHostToDevice) != hipSuccess)
+            it->second.valid = false;
+    }
+}
+void ggml_backend_tensor_get(const struct ggml_tensor *t, void *data, size_t offset, size_t size) {
+    memcpy(data, (const char *)t->data + offset, size);
+}
+
+}  // extern "C"

@@ -1,6 +1,8 @@
 // kernels.h — launch wrappers for the gfx950 kernels (host-callable, no torch types).
 #pragma once
 
+#include <vector>
+
 #include "common.h"
 
 namespace ghip {
@@ -54,6 +56,29 @@ struct mv_args {
 // ks: waves that split one row tile's K range (ordered carry hand-off); 1 = one wave per tile.
 int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int grid_x, hipStream_t s);
 size_t matvec_lds_bytes(int wtype, int ks, int64_t n_bt, int64_t segment_tiles);
+
+// ---- ggml graph executor kernels (ggml_ops.hip) ----------------------------------------------------
+struct gt_desc {  // a device view of a ggml tensor: data, ne, nb (bytes), type
+    char *data = nullptr;
+    int64_t ne[4] = {1, 1, 1, 1};
+    int64_t nb[4] = {0, 0, 0, 0};
+    int type = T_F32;
+};
+int launch_g_get_rows(const gt_desc &src, const gt_desc &idx, const gt_desc &dst, hipStream_t s);
+int launch_g_elementwise(int op, const gt_desc &a, const gt_desc &b, const gt_desc &dst, float scale,
+                         const uint16_t *gelu_tab, int gelu_clamp, hipStream_t s);
+int launch_g_rms_norm(const gt_desc &a, const gt_desc &dst, float eps, hipStream_t s);
+int launch_g_rope_neox(const gt_desc &a, const gt_desc &pos, const gt_desc &dst, int n_dims, const float *cs,
+                       const float *sn, hipStream_t s);
+int launch_g_soft_max(const gt_desc &a, const gt_desc &mask, int has_mask, const gt_desc &dst, float scale, hipStream_t s);
+int launch_g_copy(const gt_desc &src, const gt_desc &dst, hipStream_t s);
+int launch_g_mul_mat_f16(const gt_desc &a, const uint16_t *b16, int64_t ne10, const gt_desc &dst, int64_t ne11,
+                         int64_t ne12, int64_t ne13, hipStream_t s);
+// host tables and tiled weights shared with the engine (engine.cpp)
+void build_f16_tables(std::vector<uint16_t> &exp_t, std::vector<uint16_t> &gelu_t);
+void build_rope(int ctx, int hd, float base, std::vector<float> &c, std::vector<float> &s);
+tiled_mat alloc_tiled(int type, int64_t rows, int64_t K, hipStream_t s);
+void free_tiled(tiled_mat &m);
 
 // ---- K-quant matvec (kquant.hip) -----------------------------------------------------------------
 struct kq_args {  // y[c][r] = vec_dot_{q4_K,q6_K}_q8_K(row r of w, column c of x), ggml AVX2 lane order

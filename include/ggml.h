@@ -8,12 +8,13 @@
  *     grad, src[10], perf counters, view_src, view_offs, data, name[64], extra, padding) so that
  *     `src0->data` / `dst->data` (the only fields src/hpc.cpp:228-229 reads) sit at the same offsets,
  *   - ggml_vec_dot_t, the 8-argument vec_dot pointer type passed at src/hpc.cpp:223 / :35-36.
- * The wider ggml op/graph API used by src/gemma_model.cpp is declared in
- * ggml_amd_graph.h and implemented by the device graph executor.
+ * The wider ggml op/graph API used by src/gemma_model.cpp is declared below and
+ * implemented by the device graph executor.
  */
 #ifndef GGML_AMD_GGML_H
 #define GGML_AMD_GGML_H
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -78,6 +79,123 @@ struct ggml_tensor {
 /* src/hpc.cpp:35-36 calls vec_dot(n, s, bs, x, bx, y, by, nrc) */
 typedef void (*ggml_vec_dot_t)(int n, float *s, size_t bs, const void *x, size_t bx, const void *y, size_t by,
                                int nrc);
+
+/* ==== the ggml context / tensor / graph / op surface src/gemma_model.cpp uses ====
+ * Implemented by libgemma_hip.so (gemma.ggml_amd/csrc/ggml_api.cpp): tensors live in host memory
+ * exactly as in ggml (a context arena or a "CPU" backend buffer), and ggml_graph_compute_with_ctx
+ * runs every node on the GPU with device mirrors of the leaf data — weights uploaded once per
+ * pointer, host-written inputs re-uploaded each compute, leaves the graph writes (the KV cache)
+ * kept device-authoritative — and copies the LAST node's data back to the host (the one
+ * src/gemma_model.cpp:280 reads).  Arithmetic = the ggml CPU ops the oracle restates
+ * (bit-identical logits, tests/test_gpu_ggml_graph.py).  GGUF loading is out of scope.        */
+enum ggml_op {
+    GGML_OP_NONE = 0,
+    GGML_OP_GET_ROWS,
+    GGML_OP_SCALE,
+    GGML_OP_RMS_NORM,
+    GGML_OP_MUL,
+    GGML_OP_ADD,
+    GGML_OP_MUL_MAT,
+    GGML_OP_ROPE,
+    GGML_OP_SOFT_MAX,
+    GGML_OP_GELU,
+    GGML_OP_CPY,
+    GGML_OP_CONT,
+    GGML_OP_VIEW,
+    GGML_OP_RESHAPE,
+    GGML_OP_PERMUTE,
+    GGML_OP_TRANSPOSE,
+    GGML_OP_COUNT
+};
+
+enum ggml_status { GGML_STATUS_ALLOC_FAILED = -2, GGML_STATUS_FAILED = -1, GGML_STATUS_SUCCESS = 0 };
+
+struct ggml_init_params {
+    size_t mem_size;   /* bytes */
+    void *mem_buffer;  /* if NULL, memory is allocated internally */
+    bool no_alloc;     /* don't allocate memory for the tensor data */
+};
+
+struct ggml_context;
+struct ggml_cgraph {
+    int size;
+    int n_nodes;
+    int n_leafs;
+    struct ggml_tensor **nodes;
+    struct ggml_tensor **grads;
+    struct ggml_tensor **leafs;
+};
+
+typedef struct ggml_backend_buffer_type *ggml_backend_buffer_type_t;
+typedef struct ggml_backend_buffer *ggml_backend_buffer_t;
+
+/* context and sizes */
+struct ggml_context *ggml_init(struct ggml_init_params params);
+void ggml_free(struct ggml_context *ctx);
+size_t ggml_tensor_overhead(void);
+size_t ggml_graph_overhead(void);
+size_t ggml_get_mem_size(const struct ggml_context *ctx);
+size_t ggml_type_size(enum ggml_type type);
+int64_t ggml_blck_size(enum ggml_type type);
+size_t ggml_row_size(enum ggml_type type, int64_t ne);
+size_t ggml_element_size(const struct ggml_tensor *tensor);
+int64_t ggml_nelements(const struct ggml_tensor *tensor);
+size_t ggml_nbytes(const struct ggml_tensor *tensor);
+
+/* tensors and views */
+struct ggml_tensor *ggml_new_tensor(struct ggml_context *ctx, enum ggml_type type, int n_dims, const int64_t *ne);
+struct ggml_tensor *ggml_new_tensor_1d(struct ggml_context *ctx, enum ggml_type type, int64_t ne0);
+struct ggml_tensor *ggml_new_tensor_2d(struct ggml_context *ctx, enum ggml_type type, int64_t ne0, int64_t ne1);
+struct ggml_tensor *ggml_new_tensor_3d(struct ggml_context *ctx, enum ggml_type type, int64_t ne0, int64_t ne1,
+                                       int64_t ne2);
+struct ggml_tensor *ggml_view_1d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, size_t offset);
+struct ggml_tensor *ggml_view_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1,
+                                 size_t nb1, size_t offset);
+struct ggml_tensor *ggml_view_3d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1,
+                                 int64_t ne2, size_t nb1, size_t nb2, size_t offset);
+struct ggml_tensor *ggml_reshape_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1);
+struct ggml_tensor *ggml_reshape_3d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1,
+                                    int64_t ne2);
+struct ggml_tensor *ggml_permute(struct ggml_context *ctx, struct ggml_tensor *a, int axis0, int axis1, int axis2,
+                                 int axis3);
+struct ggml_tensor *ggml_transpose(struct ggml_context *ctx, struct ggml_tensor *a);
+struct ggml_tensor *ggml_cont_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1);
+struct ggml_tensor *ggml_set_name(struct ggml_tensor *tensor, const char *name);
+struct ggml_tensor *ggml_format_name(struct ggml_tensor *tensor, const char *fmt, ...);
+const char *ggml_get_name(const struct ggml_tensor *tensor);
+struct ggml_tensor *ggml_get_tensor(struct ggml_context *ctx, const char *name);
+
+/* ops (src/gemma_model.cpp:438-518, 665-747) */
+struct ggml_tensor *ggml_get_rows(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b);
+struct ggml_tensor *ggml_scale(struct ggml_context *ctx, struct ggml_tensor *a, float s);
+struct ggml_tensor *ggml_rms_norm(struct ggml_context *ctx, struct ggml_tensor *a, float eps);
+struct ggml_tensor *ggml_mul(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b);
+struct ggml_tensor *ggml_add(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b);
+struct ggml_tensor *ggml_mul_mat(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b);
+struct ggml_tensor *ggml_rope_custom(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b,
+                                     int n_dims, int mode, int n_ctx, int n_orig_ctx, float freq_base,
+                                     float freq_scale, float ext_factor, float attn_factor, float beta_fast,
+                                     float beta_slow);
+struct ggml_tensor *ggml_soft_max_ext(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *mask,
+                                      struct ggml_tensor *pos, float scale, float max_bias);
+struct ggml_tensor *ggml_gelu(struct ggml_context *ctx, struct ggml_tensor *a);
+struct ggml_tensor *ggml_cpy(struct ggml_context *ctx, struct ggml_tensor *a, struct ggml_tensor *b);
+
+/* graphs */
+struct ggml_cgraph *ggml_new_graph(struct ggml_context *ctx);
+void ggml_build_forward_expand(struct ggml_cgraph *cgraph, struct ggml_tensor *tensor);
+enum ggml_status ggml_graph_compute_with_ctx(struct ggml_context *ctx, struct ggml_cgraph *cgraph, int n_threads);
+
+/* backend ("CPU" buffer type: host memory, mirrored on the device by the graph executor) */
+ggml_backend_buffer_type_t ggml_backend_cpu_buffer_type(void);
+ggml_backend_buffer_t ggml_backend_alloc_ctx_tensors_from_buft(struct ggml_context *ctx,
+                                                               ggml_backend_buffer_type_t buft);
+void ggml_backend_buffer_clear(ggml_backend_buffer_t buffer, uint8_t value);
+const char *ggml_backend_buffer_name(ggml_backend_buffer_t buffer);
+size_t ggml_backend_buffer_get_size(ggml_backend_buffer_t buffer);
+void ggml_backend_buffer_free(ggml_backend_buffer_t buffer);
+void ggml_backend_tensor_set(struct ggml_tensor *tensor, const void *data, size_t offset, size_t size);
+void ggml_backend_tensor_get(const struct ggml_tensor *tensor, void *data, size_t offset, size_t size);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,287 @@
+// gemma_graph_driver.cpp — TEST DRIVER (not product code): the reference's model driver restated
+// against the ggml surface libgemma_hip.so exports (include/ggml.h), to show that code written like
+// src/gemma_model.cpp builds and runs its graphs on the MI355X executor unchanged.
+//
+// Restated (clean-room, same API calls in the same order) from the reference:
+//   init_input_tensor (src/gemma_model.cpp:341-359), init_kv_cache (:361-401),
+//   load_input_tokens_to_tensor (:288-338), update_kv_cache (:428-436), graph_build_norm / ffn /
+//   kqv / kv_store / kv (:438-529), greedy_sample (:532-546), reset_compute_context (:650-663),
+//   build_compute_graph (:665-747), inference (:231-286); constants of src/macro.h:7-24.
+// Differences: weights come from a file of raw ggml tensors (no GGUF reader here), the KV width is
+// n_head_kv * head_dim (the reference hard-codes one kv head), the context / batch sizes are
+// arguments, and the output matrix is the tied token embedding (src/gemma_model.cpp:161-163).
+//
+// usage: gemma_graph_driver <weights.bin> <prompt.bin> <out.bin> n_layer n_embd n_head n_head_kv
+//        head_dim n_ff n_vocab ctx wtype n_decode
+// out.bin: (1 + n_decode) rows of n_vocab f32 logits (prefill's last row, then each decode step),
+//          followed by the (1 + n_decode) greedy token ids (int32).
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "ggml.h"
+
+namespace {
+
+struct hparams {
+    int n_layer, n_embd, n_head, n_head_kv, head_dim, n_ff, n_vocab, ctx, wtype;
+    float eps = 1e-6f;
+};
+struct layer_w {
+    ggml_tensor *attn_norm, *q, *k, *v, *o, *ffn_norm, *gate, *up, *down;
+};
+struct model {
+    hparams hp;
+    ggml_context *weight_ctx = nullptr, *input_ctx = nullptr, *kv_ctx = nullptr, *compute_ctx = nullptr;
+    ggml_tensor *token_embd = nullptr, *output_norm = nullptr;
+    std::vector<layer_w> layers;
+    ggml_tensor *inp_tokens = nullptr, *inp_pos = nullptr, *inp_KQ_mask = nullptr;
+    ggml_backend_buffer_t input_buf = nullptr, kv_buf = nullptr;
+    std::vector<ggml_tensor *> k_layer, v_layer;
+    int kv_n = 0, kv_head = 0;
+    std::vector<char> compute_mem;
+};
+
+enum stage { PREFILL, DECODE };
+
+bool read_tensor(FILE *f, ggml_tensor *t) { return fread(t->data, 1, ggml_nbytes(t), f) == ggml_nbytes(t); }
+
+bool load_weights(model &m, const char *path) {
+    const hparams &h = m.hp;
+    const ggml_type wt = (ggml_type)h.wtype;
+    const int64_t qw = (int64_t)h.n_head * h.head_dim, kvw = (int64_t)h.n_head_kv * h.head_dim;
+    size_t bytes = ggml_row_size(wt, h.n_embd) * h.n_vocab + 4 * h.n_embd;
+    bytes += (size_t)h.n_layer * (8 * h.n_embd + ggml_row_size(wt, h.n_embd) * (qw + 2 * kvw + 2 * h.n_ff) +
+                                  ggml_row_size(wt, qw) * h.n_embd + ggml_row_size(wt, h.n_ff) * h.n_embd);
+    ggml_init_params p = {bytes + (size_t)(h.n_layer * 9 + 2) * (ggml_tensor_overhead() + 64), nullptr, false};
+    m.weight_ctx = ggml_init(p);
+    FILE *f = fopen(path, "rb");
+    if (!f) return false;
+    bool ok = true;
+    m.token_embd = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, h.n_vocab);
+    m.output_norm = ggml_new_tensor_1d(m.weight_ctx, GGML_TYPE_F32, h.n_embd);
+    ok = ok && read_tensor(f, m.token_embd) && read_tensor(f, m.output_norm);
+    for (int il = 0; il < h.n_layer && ok; ++il) {
+        layer_w L;
+        L.attn_norm = ggml_new_tensor_1d(m.weight_ctx, GGML_TYPE_F32, h.n_embd);
+        L.q = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, qw);
+        L.k = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, kvw);
+        L.v = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, kvw);
+        L.o = ggml_new_tensor_2d(m.weight_ctx, wt, qw, h.n_embd);
+        L.ffn_norm = ggml_new_tensor_1d(m.weight_ctx, GGML_TYPE_F32, h.n_embd);
+        L.gate = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, h.n_ff);
+        L.up = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, h.n_ff);
+        L.down = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_ff, h.n_embd);
+        for (ggml_tensor *t : {L.attn_norm, L.q, L.k, L.v, L.o, L.ffn_norm, L.gate, L.up, L.down}) ok = ok && read_tensor(f, t);
+        m.layers.push_back(L);
+    }
+    fclose(f);
+    return ok;
+}
+
+void init_input_tensor(model &m) {  // src/gemma_model.cpp:341-359
+    ggml_init_params p = {ggml_tensor_overhead() * 4, nullptr, true};
+    m.input_ctx = ggml_init(p);
+    m.inp_tokens = ggml_new_tensor_1d(m.input_ctx, GGML_TYPE_I32, m.hp.ctx);
+    m.inp_pos = ggml_new_tensor_1d(m.input_ctx, GGML_TYPE_I32, m.hp.ctx);
+    m.inp_KQ_mask = ggml_new_tensor_2d(m.input_ctx, GGML_TYPE_F32, m.hp.ctx, m.hp.ctx);
+    m.input_buf = ggml_backend_alloc_ctx_tensors_from_buft(m.input_ctx, ggml_backend_cpu_buffer_type());
+    ggml_backend_buffer_clear(m.input_buf, 0);
+}
+
+void init_kv_cache(model &m) {  // src/gemma_model.cpp:361-401
+    const int64_t kvw = (int64_t)m.hp.n_head_kv * m.hp.head_dim;
+    ggml_init_params p = {2u * m.hp.n_layer * ggml_tensor_overhead(), nullptr, true};
+    m.kv_ctx = ggml_init(p);
+    for (int i = 0; i < m.hp.n_layer; ++i) {
+        ggml_tensor *k = ggml_new_tensor_1d(m.kv_ctx, GGML_TYPE_F16, kvw * m.hp.ctx);
+        ggml_tensor *v = ggml_new_tensor_1d(m.kv_ctx, GGML_TYPE_F16, kvw * m.hp.ctx);
+        ggml_format_name(k, "cache_k_l%d", i);
+        ggml_format_name(v, "cache_v_l%d", i);
+        m.k_layer.push_back(k);
+        m.v_layer.push_back(v);
+    }
+    m.kv_buf = ggml_backend_alloc_ctx_tensors_from_buft(m.kv_ctx, ggml_backend_cpu_buffer_type());
+    ggml_backend_buffer_clear(m.kv_buf, 0);
+}
+
+void update_kv_cache(model &m, const std::vector<int32_t> &input, stage st) {  // :428-436
+    m.kv_n = std::min(m.hp.ctx, ((int)input.size() / 32 + 1) * 32);
+    m.kv_head = st == PREFILL ? 0 : (int)input.size() - 1;
+}
+
+void load_input_tokens_to_tensor(model &m, const std::vector<int32_t> &input, stage st) {  // :288-338
+    const size_t n = st == PREFILL ? input.size() : 1;
+    ggml_backend_tensor_set(m.inp_tokens, input.data() + (st == PREFILL ? 0 : input.size() - 1), 0,
+                            n * ggml_element_size(m.inp_tokens));
+    std::vector<int32_t> pos(n);
+    for (size_t i = 0; i < n; ++i) pos[i] = st == PREFILL ? (int32_t)i : (int32_t)input.size() - 1;
+    ggml_backend_tensor_set(m.inp_pos, pos.data(), 0, n * ggml_element_size(m.inp_pos));
+    float *mask = (float *)m.inp_KQ_mask->data;
+    size_t begin = st == PREFILL ? 0 : input.size() - 1;
+    for (size_t i = 0; i < n; ++i, ++begin)
+        for (int j = 0; j < m.kv_n; ++j) mask[i * m.kv_n + j] = (size_t)j > begin ? -INFINITY : 0.0f;
+}
+
+ggml_tensor *build_norm(model &m, ggml_context *ctx, ggml_tensor *x, ggml_tensor *w) {  // :438-442
+    x = ggml_rms_norm(ctx, x, m.hp.eps);
+    return ggml_mul(ctx, x, w);
+}
+
+ggml_tensor *build_ffn(ggml_context *ctx, ggml_tensor *cur, ggml_tensor *up, ggml_tensor *gate, ggml_tensor *down) {
+    ggml_tensor *tmp = ggml_mul_mat(ctx, up, cur);  // :444-452
+    cur = ggml_mul_mat(ctx, gate, cur);
+    cur = ggml_gelu(ctx, cur);
+    cur = ggml_mul(ctx, cur, tmp);
+    return ggml_mul_mat(ctx, down, cur);
+}
+
+ggml_tensor *build_kqv(model &m, ggml_context *ctx, ggml_cgraph *g, ggml_tensor *wo, ggml_tensor *q_cur,
+                       ggml_tensor *kq_mask, int n_tokens, float kq_scale, int il) {  // :454-497
+    const int64_t hd = m.hp.head_dim, H = m.hp.n_head, Hkv = m.hp.n_head_kv, ctx_n = m.hp.ctx;
+    ggml_tensor *q = ggml_permute(ctx, q_cur, 0, 2, 1, 3);
+    ggml_tensor *k = ggml_view_3d(ctx, m.k_layer[il], hd, m.kv_n, Hkv, ggml_row_size(m.k_layer[il]->type, hd * Hkv),
+                                  ggml_row_size(m.k_layer[il]->type, hd), 0);
+    ggml_tensor *kq = ggml_mul_mat(ctx, k, q);
+    kq = ggml_soft_max_ext(ctx, kq, kq_mask, nullptr, kq_scale, 0.0f);
+    ggml_tensor *v = ggml_view_3d(ctx, m.v_layer[il], m.kv_n, hd, Hkv, ggml_element_size(m.v_layer[il]) * ctx_n,
+                                  ggml_element_size(m.v_layer[il]) * ctx_n * hd, 0);
+    ggml_tensor *kqv = ggml_mul_mat(ctx, v, kq);
+    ggml_tensor *merged = ggml_permute(ctx, kqv, 0, 2, 1, 3);
+    ggml_tensor *cur = ggml_cont_2d(ctx, merged, hd * H, n_tokens);
+    ggml_build_forward_expand(g, cur);
+    return ggml_mul_mat(ctx, wo, cur);
+}
+
+void build_kv_store(model &m, ggml_context *ctx, ggml_cgraph *g, ggml_tensor *k_cur, ggml_tensor *v_cur, int n_tokens,
+                    int il) {  // :499-518
+    const int64_t kvw = (int64_t)m.hp.n_head_kv * m.hp.head_dim, ctx_n = m.hp.ctx;
+    ggml_tensor *v_cur_t = ggml_transpose(ctx, ggml_reshape_2d(ctx, v_cur, kvw, n_tokens));
+    ggml_tensor *k_view = ggml_view_1d(ctx, m.k_layer[il], n_tokens * kvw, ggml_row_size(m.k_layer[il]->type, kvw) * m.kv_head);
+    ggml_tensor *v_view = ggml_view_2d(ctx, m.v_layer[il], n_tokens, kvw, ctx_n * ggml_element_size(m.v_layer[il]),
+                                       m.kv_head * ggml_element_size(m.v_layer[il]));
+    ggml_build_forward_expand(g, ggml_cpy(ctx, k_cur, k_view));
+    ggml_build_forward_expand(g, ggml_cpy(ctx, v_cur_t, v_view));
+}
+
+void reset_compute_context(model &m) {  // :650-663
+    if (m.compute_ctx) ggml_free(m.compute_ctx);
+    ggml_init_params p = {m.compute_mem.size(), m.compute_mem.data(), false};
+    m.compute_ctx = ggml_init(p);
+}
+
+ggml_cgraph *build_compute_graph(model &m, const std::vector<int32_t> &input, stage st) {  // :665-747
+    reset_compute_context(m);
+    ggml_context *ctx = m.compute_ctx;
+    ggml_cgraph *g = ggml_new_graph(ctx);
+    const hparams &h = m.hp;
+    const int64_t T = st == PREFILL ? (int64_t)input.size() : 1;
+    ggml_tensor *tok = ggml_view_1d(ctx, m.inp_tokens, T, 0);
+    ggml_set_name(tok, "inp_tokens (view)");
+    ggml_tensor *inpL = ggml_get_rows(ctx, m.token_embd, tok);
+    inpL = ggml_scale(ctx, inpL, sqrtf((float)h.n_embd));
+    ggml_tensor *pos = ggml_view_1d(ctx, m.inp_pos, T, 0);
+    ggml_tensor *mask = ggml_view_2d(ctx, m.inp_KQ_mask, m.kv_n, T, m.kv_n * ggml_type_size(m.inp_KQ_mask->type), 0);
+    for (int il = 0; il < h.n_layer; ++il) {
+        const layer_w &L = m.layers[il];
+        ggml_tensor *cur = build_norm(m, ctx, inpL, L.attn_norm);
+        ggml_tensor *q = ggml_mul_mat(ctx, L.q, cur);
+        ggml_tensor *k = ggml_mul_mat(ctx, L.k, cur);
+        ggml_tensor *v = ggml_mul_mat(ctx, L.v, cur);
+        q = ggml_rope_custom(ctx, ggml_reshape_3d(ctx, q, h.head_dim, h.n_head, T), pos, h.head_dim, 2, 0, 8192, 10000,
+                             1, 0, 1, 32, 1);
+        q = ggml_scale(ctx, q, 1.0f / sqrtf((float)h.head_dim));
+        k = ggml_rope_custom(ctx, ggml_reshape_3d(ctx, k, h.head_dim, h.n_head_kv, T), pos, h.head_dim, 2, 0, 8192,
+                             10000, 1, 0, 1, 32, 1);
+        ggml_build_forward_expand(g, q);  // graph_build_kv (:520-529)
+        ggml_build_forward_expand(g, k);
+        ggml_build_forward_expand(g, v);
+        build_kv_store(m, ctx, g, k, v, (int)T, il);
+        cur = build_kqv(m, ctx, g, L.o, q, mask, (int)T, 1.0f, il);
+        ggml_tensor *sa = ggml_add(ctx, cur, inpL);
+        cur = build_norm(m, ctx, sa, L.ffn_norm);
+        cur = build_ffn(ctx, cur, L.up, L.gate, L.down);
+        inpL = ggml_add(ctx, cur, sa);
+    }
+    ggml_tensor *cur = build_norm(m, ctx, inpL, m.output_norm);
+    cur = ggml_mul_mat(ctx, m.token_embd, cur);  // tied output
+    ggml_build_forward_expand(g, cur);
+    ggml_set_name(g->nodes[g->n_nodes - 1], "result_output");
+    return g;
+}
+
+int32_t greedy_sample(const ggml_tensor *out, std::vector<float> &row) {  // :532-546
+    const float *logits = (const float *)out->data + out->ne[0] * (out->ne[1] - 1);
+    row.assign(logits, logits + out->ne[0]);
+    float max_val = -INFINITY;
+    int max_idx = -1;
+    for (int i = 0; i < out->ne[0]; ++i)
+        if (logits[i] > max_val) {
+            max_val = logits[i];
+            max_idx = i;
+        }
+    return max_idx;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc < 14) {
+        fprintf(stderr, "usage: %s weights prompt out n_layer n_embd n_head n_head_kv head_dim n_ff n_vocab ctx wtype n_decode\n",
+                argv[0]);
+        return 2;
+    }
+    model m;
+    m.hp = {atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8]), atoi(argv[9]), atoi(argv[10]),
+            atoi(argv[11]), atoi(argv[12])};
+    const int n_decode = atoi(argv[13]);
+    if (!load_weights(m, argv[1])) {
+        fprintf(stderr, "weights: read failed\n");
+        return 1;
+    }
+    std::vector<int32_t> input;
+    {
+        FILE *f = fopen(argv[2], "rb");
+        int32_t t;
+        while (f && fread(&t, 4, 1, f) == 1) input.push_back(t);
+        if (f) fclose(f);
+    }
+    init_input_tensor(m);
+    init_kv_cache(m);
+    // compute context: node metadata + the host copies of the intermediate data
+    const size_t T = input.size(), L = m.hp.n_layer, E = m.hp.n_embd, F = m.hp.n_ff;
+    const size_t qw = (size_t)m.hp.n_head * m.hp.head_dim, kvw = (size_t)m.hp.n_head_kv * m.hp.head_dim;
+    const size_t per_tok = m.hp.n_vocab + 2 * E + L * (6 * F + 16 * E + 8 * qw + 6 * kvw);
+    const size_t mid = (T * per_tok + L * T * (size_t)m.hp.ctx * m.hp.n_head * 4) * 4 + (64u << 20);
+    m.compute_mem.resize(ggml_tensor_overhead() * 4096 + ggml_graph_overhead() + mid);
+    FILE *out = fopen(argv[3], "wb");
+    std::vector<int32_t> toks;
+    std::vector<float> row;
+    for (int step = 0; step <= n_decode; ++step) {  // inference (:231-286)
+        const stage st = step == 0 ? PREFILL : DECODE;
+        update_kv_cache(m, input, st);
+        load_input_tokens_to_tensor(m, input, st);
+        ggml_cgraph *g = build_compute_graph(m, input, st);
+        if (ggml_graph_compute_with_ctx(m.compute_ctx, g, 1) != GGML_STATUS_SUCCESS) {
+            fprintf(stderr, "graph compute failed\n");
+            return 1;
+        }
+        const int32_t t = greedy_sample(g->nodes[g->n_nodes - 1], row);
+        fwrite(row.data(), 4, row.size(), out);
+        toks.push_back(t);
+        input.push_back(t);
+    }
+    fwrite(toks.data(), 4, toks.size(), out);
+    fclose(out);
+    ggml_free(m.compute_ctx);
+    ggml_backend_buffer_free(m.input_buf);
+    ggml_backend_buffer_free(m.kv_buf);
+    ggml_free(m.input_ctx);
+    ggml_free(m.kv_ctx);
+    ggml_free(m.weight_ctx);
+    return 0;
+}
