@@ -747,6 +747,10 @@ enum ggml_status ggml_graph_compute_with_ctx(struct ggml_context *ctx, struct gg
     return GGML_STATUS_SUCCESS;
 }
 
+int hpc_graph_compute(struct ggml_cgraph *graph) {
+    return ggml_graph_compute_with_ctx(nullptr, graph, 1) == GGML_STATUS_SUCCESS ? 0 : -1;
+}
+
 // ---- backend ("CPU" buffers in host memory, mirrored by the executor) ---------------------------
 static ggml_backend_buffer_type g_cpu_buft = {"CPU"};
 ggml_backend_buffer_type_t ggml_backend_cpu_buffer_type(void) { return &g_cpu_buft; }

@@ -20,7 +20,8 @@ GGML_TYPE_Q4_K, GGML_TYPE_Q6_K, GGML_TYPE_Q8_K = 12, 14, 15
 EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
            "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
            "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
-           "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact", "gemma_kq_time",
+           "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact", "gemma_kq_time", "hpc_graph_compute",
+           "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
            "gemma_engine_plan", "gemma_engine_set_plan", "gemma_hbm_read_gbs",
            "gemma_tp_unique_id", "gemma_engine_create_tp"]

@@ -44,7 +44,11 @@ void hpc_set_error_mode(int exit_on_error);
 int hpc_weight_cache_entries(void);
 void hpc_set_matvec_ks(int ks);          /* K-split of the quantized matvec (1/2/4/8; tests) */
 
-/* ---- device-resident Gemma engine (performance path; SURVEY §8(b) hpc_graph_compute role) ---- */
+/* ---- graph executor (SURVEY §8(b) `hpc_graph_compute(ggml_cgraph*)`): runs a graph built with the
+ * ggml surface of include/ggml.h on the GPU; 0 = ok, else hpc_last_error() tells */
+int hpc_graph_compute(struct ggml_cgraph *graph);
+
+/* ---- device-resident Gemma engine (performance path: the Gemma graph encoded as one hipGraph) ---- */
 typedef struct gemma_hip_config {
     int n_layer, n_embd, n_head, n_head_kv, head_dim, n_ff, n_vocab, n_ctx;
     int wtype; /* GGML_TYPE_Q4_0 or GGML_TYPE_Q8_0 (all matrices, incl. token_embd/output) */

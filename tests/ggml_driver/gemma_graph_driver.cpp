@@ -266,6 +266,7 @@ int main(int argc, char **argv) {
         update_kv_cache(m, input, st);
         load_input_tokens_to_tensor(m, input, st);
         ggml_cgraph *g = build_compute_graph(m, input, st);
+        // src/gemma_model.cpp:237 calls ggml_graph_compute_with_ctx; hpc_graph_compute is the same executor
         if (ggml_graph_compute_with_ctx(m.compute_ctx, g, 1) != GGML_STATUS_SUCCESS) {
             fprintf(stderr, "graph compute failed\n");
             return 1;
