@@ -82,6 +82,29 @@ def load_traffic(kernel_id):
         return None
 
 
+def run_tp_leg(args, world, rank):
+    """Every rank starts scripts/tp_leg.py as a child (its own gloo rendezvous on another port) and
+    waits with a time limit: a hung RCCL collective costs the leg, never the bench line."""
+    import subprocess
+    env = dict(os.environ)
+    if world > 1:
+        env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 1009)
+    cmd = [sys.executable, os.path.join(ROOT, "scripts", "tp_leg.py"), str(args.tp_steps), args.wtype,
+           "0" if args.no_tune else "1"]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.tp_timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {args.tp_timeout} s"}
+    if r.returncode != 0:
+        return {"error": (r.stderr or r.stdout)[-300:]}
+    if rank != 0:
+        return None
+    try:
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as ex:  # reported, never fatal to the headline line
+        return {"error": f"unparsable leg output: {ex}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,6 +119,7 @@ def main():
     ap.add_argument("--no-tune", action="store_true", help="default launch plan instead of the measured one")
     ap.add_argument("--tp-steps", type=int, default=48, help="Gemma-7B row-split decode leg steps (0 = skip)")
     ap.add_argument("--q8-steps", type=int, default=48, help="Gemma-2B Q8_0 decode leg steps (0 = skip)")
+    ap.add_argument("--tp-timeout", type=int, default=240, help="time limit of the TP leg's child processes (s)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -144,37 +168,7 @@ def main():
     # the job's GPUs with RCCL all-gathers (one rank per GPU; at N = 1 the same engine unsplit)
     tp = None
     if args.tp_steps > 0:
-        try:
-            import torch as _t
-            rid = None
-            if world > 1:
-                idt = _t.zeros(256, dtype=_t.uint8)
-                if rank == 0:
-                    raw = G.tp_unique_id()
-                    idt[: len(raw)] = _t.tensor(list(raw), dtype=_t.uint8)
-                dist.broadcast(idt, 0)
-                rid = bytes(idt.numpy())
-            te = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=(world, rank, rid))
-            tplan = te.tune(6) if not args.no_tune else te.plan()
-            te.begin(make_prompt(16, GEMMA_7B["n_vocab"]))
-            te.step(16 + 4, use_graph=True)
-            barrier_sync()
-            t0 = time.perf_counter()
-            te.step(args.tp_steps, use_graph=True)
-            te.L.gemma_engine_sync(te.h)
-            barrier_sync()
-            tdt = time.perf_counter() - t0
-            if dist is not None:
-                tt = torch.tensor([tdt], dtype=torch.float64)
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                tdt = float(tt.item())
-            te.close()
-            tp = {"model": "Gemma-7B " + args.wtype.upper(), "ranks": world, "tok_s": round(args.tp_steps / tdt, 2),
-                  "ms_per_token": round(tdt / args.tp_steps * 1e3, 4), "steps": args.tp_steps,
-                  "parallelism": f"row-split tp{world} (RCCL all-gather x4/layer)" if world > 1 else "1 GPU",
-                  "launch_plan": tplan}
-        except Exception as ex:  # reported, never fatal to the headline line
-            tp = {"error": str(ex)[:300]}
+        tp = run_tp_leg(args, world, rank)
 
     # second quant format (BASELINE config 5): the same decode with Q8_0 weights (2.66 GB/token)
     q8 = None
