@@ -30,31 +30,14 @@
 #include <vector>
 
 #include "../../include/gemma_hpc.h"
+#include "ggml_impl.h"
 #include "kernels.h"
 
 using namespace ghip;
 
-struct ggml_context {
-    char *mem = nullptr;
-    size_t mem_size = 0, used = 0;
-    bool owns_mem = false, no_alloc = false;
-    std::vector<ggml_tensor *> tensors;
-    std::vector<ggml_cgraph *> graphs;
-};
+namespace ggml_impl {
 
-struct ggml_backend_buffer_type {
-    const char *name;
-};
-struct ggml_backend_buffer {
-    char *mem = nullptr;
-    size_t size = 0;
-    std::vector<ggml_tensor *> tensors;
-};
-
-namespace {
-
-constexpr size_t kAlign = 32;
-constexpr int kGraphSize = 8192;
+constexpr size_t kArenaAlign = 32;
 
 size_t type_size(int t) {
     switch (t) {
@@ -62,8 +45,15 @@ size_t type_size(int t) {
         case GGML_TYPE_F16: case GGML_TYPE_I16: return 2;
         case GGML_TYPE_I8: return 1;
         case GGML_TYPE_Q4_0: return 18;
+        case GGML_TYPE_Q4_1: return 20;
+        case GGML_TYPE_Q5_0: return 22;
+        case GGML_TYPE_Q5_1: return 24;
         case GGML_TYPE_Q8_0: return 34;
+        case GGML_TYPE_Q8_1: return 36;
+        case GGML_TYPE_Q2_K: return 84;
+        case GGML_TYPE_Q3_K: return 110;
         case GGML_TYPE_Q4_K: return 144;
+        case GGML_TYPE_Q5_K: return 176;
         case GGML_TYPE_Q6_K: return 210;
         case GGML_TYPE_Q8_K: return 292;
         default: return 0;
@@ -71,8 +61,10 @@ size_t type_size(int t) {
 }
 int64_t blck_size(int t) {
     switch (t) {
-        case GGML_TYPE_Q4_0: case GGML_TYPE_Q8_0: return 32;
-        case GGML_TYPE_Q4_K: case GGML_TYPE_Q6_K: case GGML_TYPE_Q8_K: return 256;
+        case GGML_TYPE_Q4_0: case GGML_TYPE_Q4_1: case GGML_TYPE_Q5_0: case GGML_TYPE_Q5_1: case GGML_TYPE_Q8_0:
+        case GGML_TYPE_Q8_1: return 32;
+        case GGML_TYPE_Q2_K: case GGML_TYPE_Q3_K: case GGML_TYPE_Q4_K: case GGML_TYPE_Q5_K: case GGML_TYPE_Q6_K:
+        case GGML_TYPE_Q8_K: return 256;
         default: return 1;
     }
 }
@@ -96,7 +88,7 @@ ggml_tensor *new_tensor_impl(ggml_context *ctx, ggml_type type, int n_dims, cons
         t->data = view_src->data ? (char *)view_src->data + view_offs : nullptr;
     } else if (!ctx->no_alloc) {
         const size_t nbytes = ggml_nbytes(t);
-        const size_t off = (ctx->used + kAlign - 1) & ~(kAlign - 1);
+        const size_t off = (ctx->used + kArenaAlign - 1) & ~(kArenaAlign - 1);
         if (off + nbytes > ctx->mem_size) {
             fprintf(stderr, "[gemma_hip] ggml: context out of memory (%zu + %zu > %zu)\n", off, nbytes, ctx->mem_size);
             abort();
@@ -107,6 +99,14 @@ ggml_tensor *new_tensor_impl(ggml_context *ctx, ggml_type type, int n_dims, cons
     ctx->tensors.push_back(t);
     return t;
 }
+
+}  // namespace ggml_impl
+using namespace ggml_impl;
+
+namespace {
+
+constexpr size_t kAlign = 32;
+constexpr int kGraphSize = 8192;
 
 ggml_tensor *view_of(ggml_context *ctx, ggml_tensor *a, int n_dims, const int64_t *ne, size_t offset) {
     return new_tensor_impl(ctx, a->type, n_dims, ne, a, offset);

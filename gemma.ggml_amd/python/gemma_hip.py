@@ -24,7 +24,12 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
            "gemma_engine_plan", "gemma_engine_set_plan", "gemma_hbm_read_gbs",
-           "gemma_tp_unique_id", "gemma_engine_create_tp"]
+           "gemma_tp_unique_id", "gemma_engine_create_tp",
+           "gguf_init_from_file", "gguf_free", "gguf_get_n_kv", "gguf_get_key", "gguf_get_kv_type",
+           "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
+           "gguf_get_val_data", "gguf_get_n_tensors", "gguf_get_tensor_name", "gguf_get_tensor_type",
+           "gguf_get_tensor_offset", "gguf_get_version", "gguf_get_alignment", "gguf_get_data_offset",
+           "gguf_find_key", "gguf_find_tensor", "ggml_get_tensor", "ggml_nbytes"]
 
 
 def build():
@@ -45,6 +50,10 @@ class GgmlTensor(C.Structure):
                 ("grad", C.c_void_p), ("src", C.c_void_p * 10), ("perf_runs", C.c_int), ("perf_cycles", C.c_int64),
                 ("perf_time_us", C.c_int64), ("view_src", C.c_void_p), ("view_offs", C.c_size_t),
                 ("data", C.c_void_p), ("name", C.c_char * 64), ("extra", C.c_void_p), ("padding", C.c_char * 8)]
+
+
+class GGUFInitParams(C.Structure):
+    _fields_ = [("no_alloc", C.c_bool), ("ctx", C.POINTER(C.c_void_p))]
 
 
 _lib = None
@@ -108,6 +117,34 @@ def lib():
     L.gemma_hbm_read_gbs.argtypes = [C.c_int, C.c_size_t, C.c_int]
     L.gemma_engine_sync.restype = C.c_int
     L.gemma_engine_sync.argtypes = [vp]
+    # GGUF reader (include/ggml.h)
+    L.gguf_init_from_file.restype = vp
+    L.gguf_init_from_file.argtypes = [C.c_char_p, GGUFInitParams]
+    L.gguf_free.argtypes = [vp]
+    for fn in ("gguf_get_n_kv", "gguf_get_n_tensors", "gguf_get_version"):
+        getattr(L, fn).restype = C.c_int
+        getattr(L, fn).argtypes = [vp]
+    for fn in ("gguf_get_alignment", "gguf_get_data_offset"):
+        getattr(L, fn).restype = C.c_size_t
+        getattr(L, fn).argtypes = [vp]
+    for fn, rt in (("gguf_get_key", C.c_char_p), ("gguf_get_kv_type", C.c_int), ("gguf_get_arr_type", C.c_int),
+                   ("gguf_get_arr_n", C.c_int), ("gguf_get_arr_data", vp), ("gguf_get_val_str", C.c_char_p),
+                   ("gguf_get_val_data", vp), ("gguf_get_tensor_name", C.c_char_p),
+                   ("gguf_get_tensor_type", C.c_int), ("gguf_get_tensor_offset", C.c_size_t)):
+        getattr(L, fn).restype = rt
+        getattr(L, fn).argtypes = [vp, C.c_int]
+    L.gguf_get_arr_str.restype = C.c_char_p
+    L.gguf_get_arr_str.argtypes = [vp, C.c_int, C.c_int]
+    L.gguf_find_key.restype = C.c_int
+    L.gguf_find_key.argtypes = [vp, C.c_char_p]
+    L.gguf_find_tensor.restype = C.c_int
+    L.gguf_find_tensor.argtypes = [vp, C.c_char_p]
+    L.ggml_get_tensor.restype = C.POINTER(GgmlTensor)
+    L.ggml_get_tensor.argtypes = [vp, C.c_char_p]
+    L.ggml_nbytes.restype = C.c_size_t
+    L.ggml_nbytes.argtypes = [C.POINTER(GgmlTensor)]
+    L.ggml_free.restype = None
+    L.ggml_free.argtypes = [vp]
     _lib = L
     return L
 
@@ -258,3 +295,50 @@ def tp_unique_id():
     if n <= 0:
         raise RuntimeError("gemma_tp_unique_id failed: " + last_error())
     return buf.raw[:n]
+
+
+_GGUF_SCALAR = {0: C.c_uint8, 1: C.c_int8, 2: C.c_uint16, 3: C.c_int16, 4: C.c_uint32, 5: C.c_int32, 6: C.c_float,
+                7: C.c_bool, 10: C.c_uint64, 11: C.c_int64, 12: C.c_double}
+
+
+class GGUF:
+    """A GGUF file read by the library's gguf_init_from_file (include/ggml.h): `kv` maps keys to
+    values (scalars, str, lists), `tensors` maps names to (ggml type, ne, bytes) when load_tensors."""
+
+    def __init__(self, path, load_tensors=True):
+        L = lib()
+        ctx = C.c_void_p()
+        self.g = L.gguf_init_from_file(path.encode(), GGUFInitParams(not load_tensors, C.pointer(ctx)))
+        if not self.g:
+            raise ValueError(last_error())
+        self.version = L.gguf_get_version(self.g)
+        self.alignment = L.gguf_get_alignment(self.g)
+        self.data_offset = L.gguf_get_data_offset(self.g)
+        self.kv = {}
+        for i in range(L.gguf_get_n_kv(self.g)):
+            key = L.gguf_get_key(self.g, i).decode()
+            t = L.gguf_get_kv_type(self.g, i)
+            if t == 8:
+                v = L.gguf_get_val_str(self.g, i).decode()
+            elif t == 9:
+                at, n = L.gguf_get_arr_type(self.g, i), L.gguf_get_arr_n(self.g, i)
+                if at == 8:
+                    v = [L.gguf_get_arr_str(self.g, i, j).decode() for j in range(n)]
+                else:
+                    ct = _GGUF_SCALAR[at]
+                    v = list((ct * n).from_address(L.gguf_get_arr_data(self.g, i))) if n else []
+            else:
+                v = _GGUF_SCALAR[t].from_address(L.gguf_get_val_data(self.g, i)).value
+            self.kv[key] = v
+        self.tensors = {}
+        for i in range(L.gguf_get_n_tensors(self.g)):
+            name = L.gguf_get_tensor_name(self.g, i)
+            t = L.ggml_get_tensor(ctx, name)
+            data = None
+            if load_tensors:
+                data = C.string_at(t.contents.data, L.ggml_nbytes(t))
+            self.tensors[name.decode()] = (L.gguf_get_tensor_type(self.g, i), tuple(t.contents.ne), data,
+                                           L.gguf_get_tensor_offset(self.g, i))
+        L.ggml_free(ctx)
+        L.gguf_free(self.g)
+        self.g = None

@@ -197,6 +197,65 @@ void ggml_backend_buffer_free(ggml_backend_buffer_t buffer);
 void ggml_backend_tensor_set(struct ggml_tensor *tensor, const void *data, size_t offset, size_t size);
 void ggml_backend_tensor_get(const struct ggml_tensor *tensor, void *data, size_t offset, size_t size);
 
+/* ---- GGUF (v2/v3) reader: the gguf_* API src/gemma_model.cpp:19-229, 583-648 loads models with ----
+ * gguf_init_from_file reads the header, key/value pairs and tensor infos; with params.ctx != NULL it
+ * also creates a ggml context holding every tensor (named as in the file; data read from the file
+ * unless params.no_alloc).  Malformed files return NULL with a message (hpc_last_error).
+ * gguf_get_val_* / gguf_get_arr_* on a key of another type abort, as ggml's GGML_ASSERT does. */
+enum gguf_type {
+    GGUF_TYPE_UINT8 = 0,
+    GGUF_TYPE_INT8 = 1,
+    GGUF_TYPE_UINT16 = 2,
+    GGUF_TYPE_INT16 = 3,
+    GGUF_TYPE_UINT32 = 4,
+    GGUF_TYPE_INT32 = 5,
+    GGUF_TYPE_FLOAT32 = 6,
+    GGUF_TYPE_BOOL = 7,
+    GGUF_TYPE_STRING = 8,
+    GGUF_TYPE_ARRAY = 9,
+    GGUF_TYPE_UINT64 = 10,
+    GGUF_TYPE_INT64 = 11,
+    GGUF_TYPE_FLOAT64 = 12,
+    GGUF_TYPE_COUNT
+};
+struct gguf_context;
+struct gguf_init_params {
+    bool no_alloc;
+    struct ggml_context **ctx;  /* if not NULL, receives a context with the file's tensors */
+};
+struct gguf_context *gguf_init_from_file(const char *fname, struct gguf_init_params params);
+void gguf_free(struct gguf_context *ctx);
+const char *gguf_type_name(enum gguf_type type);
+int gguf_get_version(const struct gguf_context *ctx);
+size_t gguf_get_alignment(const struct gguf_context *ctx);
+size_t gguf_get_data_offset(const struct gguf_context *ctx);
+int gguf_get_n_kv(const struct gguf_context *ctx);
+int gguf_find_key(const struct gguf_context *ctx, const char *key); /* -1 if absent */
+const char *gguf_get_key(const struct gguf_context *ctx, int key_id);
+enum gguf_type gguf_get_kv_type(const struct gguf_context *ctx, int key_id);
+enum gguf_type gguf_get_arr_type(const struct gguf_context *ctx, int key_id);
+uint8_t gguf_get_val_u8(const struct gguf_context *ctx, int key_id);
+int8_t gguf_get_val_i8(const struct gguf_context *ctx, int key_id);
+uint16_t gguf_get_val_u16(const struct gguf_context *ctx, int key_id);
+int16_t gguf_get_val_i16(const struct gguf_context *ctx, int key_id);
+uint32_t gguf_get_val_u32(const struct gguf_context *ctx, int key_id);
+int32_t gguf_get_val_i32(const struct gguf_context *ctx, int key_id);
+float gguf_get_val_f32(const struct gguf_context *ctx, int key_id);
+uint64_t gguf_get_val_u64(const struct gguf_context *ctx, int key_id);
+int64_t gguf_get_val_i64(const struct gguf_context *ctx, int key_id);
+double gguf_get_val_f64(const struct gguf_context *ctx, int key_id);
+bool gguf_get_val_bool(const struct gguf_context *ctx, int key_id);
+const char *gguf_get_val_str(const struct gguf_context *ctx, int key_id);
+const void *gguf_get_val_data(const struct gguf_context *ctx, int key_id);
+int gguf_get_arr_n(const struct gguf_context *ctx, int key_id);
+const void *gguf_get_arr_data(const struct gguf_context *ctx, int key_id);
+const char *gguf_get_arr_str(const struct gguf_context *ctx, int key_id, int i);
+int gguf_get_n_tensors(const struct gguf_context *ctx);
+int gguf_find_tensor(const struct gguf_context *ctx, const char *name); /* -1 if absent */
+size_t gguf_get_tensor_offset(const struct gguf_context *ctx, int i);
+const char *gguf_get_tensor_name(const struct gguf_context *ctx, int i);
+enum ggml_type gguf_get_tensor_type(const struct gguf_context *ctx, int i);
+
 #ifdef __cplusplus
 }
 #endif
