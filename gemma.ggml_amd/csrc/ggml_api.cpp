@@ -15,7 +15,8 @@
 //     path's k_matvec for <= 4 columns and k_gemm_x otherwise, both in ggml's AVX2 lane order);
 //   * the LAST node's data is copied back to its host tensor (the one src/gemma_model.cpp:280
 //     samples from).
-// Not provided: GGUF, ops outside the Gemma graph (they fail with an error), K-quant src0 in graphs.
+// K-quant (Q4_K / Q6_K) src0: Q8_K INIT on the device + the K-quant dots; get_rows dequantizes
+// Q4_0 / Q8_0 / Q4_K / Q6_K rows.  Not provided: ops outside the Gemma graph (they fail with an error).
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -309,6 +310,29 @@ int run_mul_mat(run_state &rs, ggml_tensor *node) {
         }
         return launch_g_mul_mat_f16(desc(rs, a), (const uint16_t *)b16.data, K, desc(rs, node), b->ne[1], b->ne[2],
                                     b->ne[3], e.stream);
+    }
+    if (a->type == GGML_TYPE_Q4_K || a->type == GGML_TYPE_Q6_K) {
+        // ggml INIT quantizes src1 to Q8_K (vec_dot_type of the K-quants), then the AVX2-lane-order
+        // K-quant dot per (row, column): the same kernels as the C-ABI mul_mat (csrc/kquant.hip)
+        if (K % 256 || a->ne[2] != 1 || a->ne[3] != 1 || !is_contiguous(a) || b->nb[0] != 4 ||
+            b->nb[1] != (size_t)K * 4 || (cols > b->ne[1] && b->nb[2] != b->nb[1] * b->ne[1])) {
+            set_error("ggml mul_mat: K-quant path needs K % 256 == 0, contiguous src0 and src1 rows");
+            return -1;
+        }
+        const int64_t nsb = K / 256;
+        uint8_t *xq = (uint8_t *)scratch_take(rs, (size_t)(cols * nsb * 292));
+        if (launch_quant_q8_K((const float *)dev_addr(rs, b), K, K, (int)cols, xq, nsb * 292, e.stream)) return -1;
+        kq_args k;
+        k.w = (const uint8_t *)dev_addr(rs, a);
+        k.row_bytes = (int64_t)a->nb[1];
+        k.rows = a->ne[1];
+        k.nsb = (int)nsb;
+        k.x = xq;
+        k.x_col_stride = nsb * 292;
+        k.y = (float *)dev_addr(rs, node);
+        k.y_col_stride = a->ne[1];
+        k.ncols = (int)cols;
+        return launch_matvec_kq(a->type, k, e.stream);
     }
     if (a->type != GGML_TYPE_Q4_0 && a->type != GGML_TYPE_Q8_0) {
         set_error("ggml mul_mat: src0 type " + std::to_string(a->type) + " not supported by the graph executor");

@@ -44,6 +44,33 @@ __global__ void k_g_get_rows(gt_desc src, gt_desc idx, gt_desc dst) {
         } else if (src.type == T_Q8_0) {
             const uint8_t *blk = (const uint8_t *)srow + (i >> 5) * 34;
             v = (float)(int8_t)blk[2 + (i & 31)] * pin(h2f(*(const uint16_t *)blk));
+        } else if (src.type == T_Q4_K) {
+            // dequantize_row_q4_K: per 64 values j, d1 = d*sc, m1 = dmin*m, y = d1*q - m1 (no FMA:
+            // oracle/kquants_cpu.cpp orc_dequantize_row_q4_K)
+            const uint8_t *blk = (const uint8_t *)srow + (i >> 8) * 144;
+            const int e = (int)(i & 255), j = e >> 6, hi = (e >> 5) & 1, is = 2 * j + hi;
+            const uint8_t *sc = blk + 4;
+            int scv, mv;
+            if (is < 4) {
+                scv = sc[is] & 63;
+                mv = sc[is + 4] & 63;
+            } else {
+                scv = (sc[is + 4] & 0xF) | ((sc[is - 4] >> 6) << 4);
+                mv = (sc[is + 4] >> 4) | ((sc[is] >> 6) << 4);
+            }
+            const uint8_t qb = blk[16 + j * 32 + (e & 31)];
+            const float d1 = pin(h2f(*(const uint16_t *)blk) * (float)scv);
+            const float m1 = pin(h2f(*(const uint16_t *)(blk + 2)) * (float)mv);
+            v = pin(d1 * (float)(hi ? qb >> 4 : qb & 15)) - m1;
+        } else if (src.type == T_Q6_K) {
+            // dequantize_row_q6_K: y = d*sc*(q6 - 32), left to right
+            const uint8_t *blk = (const uint8_t *)srow + (i >> 8) * 210;
+            const int e = (int)(i & 255), n = e >> 7, g = (e >> 5) & 3, l = e & 31;
+            const uint8_t *ql = blk + n * 64, *qh = blk + 128 + n * 32;
+            const int lo = (g & 1) ? ql[l + 32] : ql[l];
+            const int q = (((g & 2) ? lo >> 4 : lo & 15) | (((qh[l] >> (2 * g)) & 3) << 4)) - 32;
+            const int8_t scv = ((const int8_t *)(blk + 192))[n * 8 + l / 16 + 2 * g];
+            v = pin(h2f(*(const uint16_t *)(blk + 208)) * (float)scv) * (float)q;
         } else if (src.type == T_F16) {
             v = h2f(((const uint16_t *)srow)[i]);
         } else {

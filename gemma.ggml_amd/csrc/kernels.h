@@ -92,6 +92,9 @@ struct kq_args {  // y[c][r] = vec_dot_{q4_K,q6_K}_q8_K(row r of w, column c of 
     int ncols = 1;
 };
 int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s);
+// ggml quantize_row_q8_K of ncols rows of K floats (row stride ldx floats) -> Q8_K rows ld_out bytes apart
+int launch_quant_q8_K(const float *x, int64_t ldx, int64_t K, int ncols, uint8_t *out, int64_t ld_out,
+                      hipStream_t s);
 
 // ---- prefill (prefill.hip) ----------------------------------------------------------------------
 enum qrow_mode { QR_F32 = 0, QR_NORM = 1, QR_EMBED_NORM = 2, QR_GELU = 3 };

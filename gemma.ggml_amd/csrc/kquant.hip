@@ -175,6 +175,68 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
 
 }  // namespace
 
+namespace {
+
+// ggml quantize_row_q8_K (INIT for K-quant src0, restated in oracle/kquants_cpu.cpp): per 256
+// values the first element of largest |x| gives max; iscale = -127/max; q = min(127, rne(iscale*x));
+// bsums = sums of 16; d = 1/iscale (all-zero block: d = 0, q = 0).  One wave per super-block, 4
+// values per lane.  Divisions in double then rounded: equal to fp32 division for fp32 operands.
+__global__ void __launch_bounds__(64) k_quant_q8_K(const float *x, int64_t ldx, uint8_t *out, int64_t ld_out) {
+    const int sb = blockIdx.x, c = blockIdx.y, lane = threadIdx.x;
+    const float4 v = *(const float4 *)(x + (int64_t)c * ldx + (int64_t)sb * 256 + lane * 4);
+    const float xv[4] = {v.x, v.y, v.z, v.w};
+    float amax = 0.0f, mx = 0.0f;
+    int idx = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float ax = fabsf(xv[j]);
+        if (ax > amax) {
+            amax = ax;
+            mx = xv[j];
+            idx = lane * 4 + j;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float oa = __shfl_xor(amax, off), om = __shfl_xor(mx, off);
+        const int oi = __shfl_xor(idx, off);
+        if (oa > amax || (oa == amax && oi < idx)) {
+            amax = oa;
+            mx = om;
+            idx = oi;
+        }
+    }
+    uint8_t *blk = out + (int64_t)c * ld_out + (int64_t)sb * 292;
+    int q[4] = {0, 0, 0, 0};
+    float d = 0.0f;
+    if (amax != 0.0f) {
+        const float iscale = (float)(-127.0 / (double)mx);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = min(127, (int)__builtin_rintf(iscale * xv[j]));
+        d = (float)(1.0 / (double)iscale);
+    }
+    int bs = q[0] + q[1] + q[2] + q[3];
+    bs += __shfl_xor(bs, 1);
+    bs += __shfl_xor(bs, 2);
+    *(uint32_t *)(blk + 4 + lane * 4) =
+        (uint32_t)(q[0] & 255) | ((uint32_t)(q[1] & 255) << 8) | ((uint32_t)(q[2] & 255) << 16) | ((uint32_t)q[3] << 24);
+    if ((lane & 3) == 0) *(int16_t *)(blk + 260 + (lane >> 2) * 2) = (int16_t)bs;
+    if (lane == 0) *(float *)blk = d;
+}
+
+}  // namespace
+
+int launch_quant_q8_K(const float *x, int64_t ldx, int64_t K, int ncols, uint8_t *out, int64_t ld_out,
+                      hipStream_t s) {
+    if (K % 256 || K <= 0 || ncols <= 0 || ldx % 4 || ld_out % 4 || ((uintptr_t)x & 15)) {
+        set_error("quant_q8_K: K must be a multiple of 256 with 16-byte aligned rows");
+        return -1;
+    }
+    hipLaunchKernelGGL(k_quant_q8_K, dim3((unsigned)(K / 256), (unsigned)ncols), dim3(64), 0, s, x, ldx, out, ld_out);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     if ((wtype != T_Q4_K && wtype != T_Q6_K) || a.nsb <= 0 || a.rows <= 0 || a.ncols <= 0 || a.x_col_stride % 4 ||
         a.nsb * 292 > 64 * 1024) {

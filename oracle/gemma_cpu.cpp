@@ -46,6 +46,7 @@ inline int tid_layer(int il, int k) { return 16 + il * 16 + k; }
 enum { L_ATTN_NORM = 0, L_Q = 1, L_K = 2, L_V = 3, L_O = 4, L_FFN_NORM = 5, L_GATE = 6, L_UP = 7, L_DOWN = 8 };
 
 struct qmat {
+    int type = ORC_Q4_0;
     int64_t rows = 0, cols = 0;
     size_t row_bytes = 0;
     std::vector<uint8_t> data;
@@ -66,6 +67,7 @@ void parallel_rows(int64_t rows, const std::function<void(int64_t, int64_t)> &fn
 
 qmat make_qmat(uint64_t seed, int tid, int64_t rows, int64_t cols, int wtype, double stdv) {
     qmat m;
+    m.type = wtype;
     m.rows = rows;
     m.cols = cols;
     m.row_bytes = orc_row_size(wtype, cols);
@@ -81,6 +83,37 @@ qmat make_qmat(uint64_t seed, int tid, int64_t rows, int64_t cols, int wtype, do
         }
     });
     return m;
+}
+
+// K-quant matrix: random valid super-blocks (orc_synth_kquant) with d (and dmin) rescaled so the
+// dequantized values have roughly the requested standard deviation (Q4_K values ~0.8 and Q6_K
+// ~0.68 rms before rescaling).  Weights are data here: the K-quant quantizer is not on the path.
+qmat make_kmat(uint64_t seed, int tid, int64_t rows, int64_t cols, int type, double stdv) {
+    qmat m;
+    m.type = type;
+    m.rows = rows;
+    m.cols = cols;
+    m.row_bytes = orc_row_size(type, cols);
+    m.data.resize(m.row_bytes * rows);
+    orc_synth_kquant(type, tensor_key(seed, tid), rows, cols, m.data.data());
+    const float f = (float)(stdv / (type == ORC_Q4_K ? 0.8 : 0.68));
+    const int64_t nb = rows * (cols / 256);
+    for (int64_t b = 0; b < nb; ++b) {
+        uint8_t *blk = m.data.data() + b * (type == ORC_Q4_K ? 144 : 210);
+        uint16_t *d = (uint16_t *)(blk + (type == ORC_Q4_K ? 0 : 208));
+        *d = orc_fp32_to_fp16(orc_fp16_to_fp32(*d) * f);
+        if (type == ORC_Q4_K) d[1] = orc_fp32_to_fp16(orc_fp16_to_fp32(d[1]) * f);
+    }
+    return m;
+}
+
+void dequantize_row(int type, const uint8_t *row, float *y, int n) {
+    switch (type) {
+        case ORC_Q4_0: orc_dequantize_row_q4_0(row, y, n); break;
+        case ORC_Q8_0: orc_dequantize_row_q8_0(row, y, n); break;
+        case ORC_Q4_K: orc_dequantize_row_q4_K(row, y, n); break;
+        case ORC_Q6_K: orc_dequantize_row_q6_K(row, y, n); break;
+    }
 }
 
 std::vector<float> make_norm(uint64_t seed, int tid, int64_t n) {
@@ -114,7 +147,12 @@ extern "C" orc_model *orc_model_create(const orc_config *cfg) {
     m->cfg = *cfg;
     const orc_config &c = *cfg;
     const int qw = c.n_head * c.head_dim, kvw = c.n_head_kv * c.head_dim;
-    m->embd = make_qmat(c.seed, TID_EMBD, c.n_vocab, c.n_embd, c.wtype, 1.0 / sqrt((double)c.n_embd));
+    if (c.kmix && (c.n_embd % 256 || c.n_ff % 256 || qw % 256)) {
+        delete m;
+        return nullptr;
+    }
+    m->embd = c.kmix ? make_kmat(c.seed, TID_EMBD, c.n_vocab, c.n_embd, ORC_Q6_K, 1.0 / sqrt((double)c.n_embd))
+                     : make_qmat(c.seed, TID_EMBD, c.n_vocab, c.n_embd, c.wtype, 1.0 / sqrt((double)c.n_embd));
     m->out_norm = make_norm(c.seed, TID_OUT_NORM, c.n_embd);
     m->layers.resize(c.n_layer);
     for (int il = 0; il < c.n_layer; ++il) {
@@ -124,13 +162,17 @@ extern "C" orc_model *orc_model_create(const orc_config *cfg) {
         // linear weights ~ N(0, 1/fan_in); residual writers (o, down) x4 gain so the tied output
         // is not dominated by the current token (DESIGN.md §Synthetic weights)
         const double se = 1.0 / sqrt((double)c.n_embd), sq = 1.0 / sqrt((double)qw), sf = 1.0 / sqrt((double)c.n_ff);
-        L.q = make_qmat(c.seed, tid_layer(il, L_Q), qw, c.n_embd, c.wtype, se);
-        L.k = make_qmat(c.seed, tid_layer(il, L_K), kvw, c.n_embd, c.wtype, se);
-        L.v = make_qmat(c.seed, tid_layer(il, L_V), kvw, c.n_embd, c.wtype, se);
-        L.o = make_qmat(c.seed, tid_layer(il, L_O), c.n_embd, qw, c.wtype, 4.0 * sq);
-        L.gate = make_qmat(c.seed, tid_layer(il, L_GATE), c.n_ff, c.n_embd, c.wtype, se);
-        L.up = make_qmat(c.seed, tid_layer(il, L_UP), c.n_ff, c.n_embd, c.wtype, se);
-        L.down = make_qmat(c.seed, tid_layer(il, L_DOWN), c.n_embd, c.n_ff, c.wtype, 4.0 * sf);
+        auto mat = [&](int k, int64_t rows, int64_t cols, int ktype, double stdv) {
+            return c.kmix ? make_kmat(c.seed, tid_layer(il, k), rows, cols, ktype, stdv)
+                          : make_qmat(c.seed, tid_layer(il, k), rows, cols, c.wtype, stdv);
+        };
+        L.q = mat(L_Q, qw, c.n_embd, ORC_Q4_K, se);
+        L.k = mat(L_K, kvw, c.n_embd, ORC_Q4_K, se);
+        L.v = mat(L_V, kvw, c.n_embd, ORC_Q6_K, se);
+        L.o = mat(L_O, c.n_embd, qw, ORC_Q4_K, 4.0 * sq);
+        L.gate = mat(L_GATE, c.n_ff, c.n_embd, ORC_Q4_K, se);
+        L.up = mat(L_UP, c.n_ff, c.n_embd, ORC_Q4_K, se);
+        L.down = mat(L_DOWN, c.n_embd, c.n_ff, ORC_Q6_K, 4.0 * sf);
     }
     orc_model_reset_kv(m);
     return m;
@@ -169,9 +211,12 @@ extern "C" void orc_model_reset_kv(orc_model *m) {
 namespace {
 
 // y[T][rows] = W . x[T][cols]  through the hpc-style mul_mat (INIT quantize + row split)
-void matmul_q(const qmat &W, const float *x, int64_t T, float *y, int wtype, int avx2,
+// (the matrix's own type picks vec_dot_type: Q8_0 for Q4_0/Q8_0, Q8_K for Q4_K/Q6_K)
+void matmul_q(const qmat &W, const float *x, int64_t T, float *y, int /*wtype*/, int avx2,
               std::vector<uint8_t> &wbuf) {
-    const size_t rs = orc_row_size(ORC_Q8_0, W.cols);
+    const int wtype = W.type;
+    const bool kq = wtype == ORC_Q4_K || wtype == ORC_Q6_K;
+    const size_t rs = orc_row_size(kq ? ORC_Q8_K : ORC_Q8_0, W.cols);
     wbuf.resize(rs * T);
     orc_mul_mat_init(wtype, x, W.cols, T, W.cols, wbuf.data());
     orc_mul_mat(W.rows, T, 1, (int64_t)W.row_bytes, T, W.rows * 4, W.rows * 4 * T, rs, W.cols, W.data.data(), y,
@@ -199,8 +244,7 @@ extern "C" int orc_model_inference(orc_model *m, const int32_t *tokens, int n_to
     const float emb_scale = sqrtf((float)E);
     for (int t = 0; t < T; ++t) {
         const int tok = tokens[head + t];
-        if (c.wtype == ORC_Q4_0) orc_dequantize_row_q4_0(m->embd.data.data() + (size_t)tok * m->embd.row_bytes, &inpL[(size_t)t * E], E);
-        else orc_dequantize_row_q8_0(m->embd.data.data() + (size_t)tok * m->embd.row_bytes, &inpL[(size_t)t * E], E);
+        dequantize_row(m->embd.type, m->embd.data.data() + (size_t)tok * m->embd.row_bytes, &inpL[(size_t)t * E], E);
         for (int i = 0; i < E; ++i) inpL[(size_t)t * E + i] *= emb_scale;
     }
 

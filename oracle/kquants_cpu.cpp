@@ -400,3 +400,52 @@ extern "C" void orc_synth_kquant(int type, uint64_t seed, int64_t rows, int64_t 
         }
     }
 }
+
+// ggml dequantize_row_q4_K / dequantize_row_q6_K [ext] (get_rows on a K-quant token_embd, as a
+// llama.cpp Q4_K_M / Q4_0 Gemma file stores it).  Q4_K, per 64 values j: d1 = d*sc[2j],
+// m1 = dmin*m[2j] -> y = d1*(low nibble) - m1, then d2, m2 for the high nibbles.  Q6_K, per 128
+// values: y = d*sc[is]*(q6 - 32), left to right.  ⚠ Q4_K's `d1*q - m1` is restated WITHOUT FMA
+// contraction (ISO C evaluation, this oracle's -ffp-contract=off policy); a ggml build that
+// contracts it would differ in the last bit of some embedding values (parity unpinned, §7).
+extern "C" void orc_dequantize_row_q4_K(const void *vx, float *y, int k) {
+    const block_q4_K *x = (const block_q4_K *)vx;
+    for (int i = 0; i < k / QK_K; ++i) {
+        const float d = orc_fp16_to_fp32(x[i].d), mn = orc_fp16_to_fp32(x[i].dmin);
+        uint8_t sc[8], m[8];
+        unpack_q4_K_scales(x[i].scales, sc, m);
+        const uint8_t *q = x[i].qs;
+        for (int j = 0; j < 4; ++j) {
+            const float d1 = d * (float)sc[2 * j], m1 = mn * (float)m[2 * j];
+            const float d2 = d * (float)sc[2 * j + 1], m2 = mn * (float)m[2 * j + 1];
+            for (int l = 0; l < 32; ++l) *y++ = d1 * (float)(q[l] & 0xF) - m1;
+            for (int l = 0; l < 32; ++l) *y++ = d2 * (float)(q[l] >> 4) - m2;
+            q += 32;
+        }
+    }
+}
+
+extern "C" void orc_dequantize_row_q6_K(const void *vx, float *y, int k) {
+    const block_q6_K *x = (const block_q6_K *)vx;
+    for (int i = 0; i < k / QK_K; ++i) {
+        const float d = orc_fp16_to_fp32(x[i].d);
+        const uint8_t *ql = x[i].ql, *qh = x[i].qh;
+        const int8_t *sc = x[i].scales;
+        for (int n = 0; n < QK_K; n += 128) {
+            for (int l = 0; l < 32; ++l) {
+                const int is = l / 16;
+                const int q1 = (int)((ql[l] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+                const int q2 = (int)((ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+                const int q3 = (int)((ql[l] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+                const int q4 = (int)((ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+                y[l + 0] = d * (float)sc[is + 0] * (float)q1;
+                y[l + 32] = d * (float)sc[is + 2] * (float)q2;
+                y[l + 64] = d * (float)sc[is + 4] * (float)q3;
+                y[l + 96] = d * (float)sc[is + 6] * (float)q4;
+            }
+            y += 128;
+            ql += 64;
+            qh += 32;
+            sc += 8;
+        }
+    }
+}

@@ -7,11 +7,17 @@
 //   load_input_tokens_to_tensor (:288-338), update_kv_cache (:428-436), graph_build_norm / ffn /
 //   kqv / kv_store / kv (:438-529), greedy_sample (:532-546), reset_compute_context (:650-663),
 //   build_compute_graph (:665-747), inference (:231-286); constants of src/macro.h:7-24.
-// Differences: weights come from a file of raw ggml tensors (no GGUF reader here), the KV width is
-// n_head_kv * head_dim (the reference hard-codes one kv head), the context / batch sizes are
-// arguments, and the output matrix is the tied token embedding (src/gemma_model.cpp:161-163).
+// Differences: the KV width is n_head_kv * head_dim (the reference hard-codes one kv head), the
+// context / batch sizes are arguments, a fixed number of decode steps runs (no stop at eos), and the
+// output matrix is the tied token embedding (src/gemma_model.cpp:161-163).
 //
-// usage: gemma_graph_driver <weights.bin> <prompt.bin> <out.bin> n_layer n_embd n_head n_head_kv
+// Weights come either from a GGUF file, loaded as src/gemma_model.cpp:19-229 / 403-415 / 583-601
+// does (gguf_init_from_file into a weight context, kv index, ggml_get_tensor by name, hyper
+// parameters and tokenizer tables from the metadata; head_dim = gemma.attention.key_length when
+// present, else n_embd / n_head as the reference computes it), or from a file of raw tensors.
+//
+// usage: gemma_graph_driver <model.gguf> <prompt.bin> <out.bin> ctx n_decode
+//        gemma_graph_driver <weights.bin> <prompt.bin> <out.bin> n_layer n_embd n_head n_head_kv
 //        head_dim n_ff n_vocab ctx wtype n_decode
 // out.bin: (1 + n_decode) rows of n_vocab f32 logits (prefill's last row, then each decode step),
 //          followed by the (1 + n_decode) greedy token ids (int32).
@@ -21,6 +27,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <string>
 #include <vector>
 
 #include "ggml.h"
@@ -44,6 +52,11 @@ struct model {
     std::vector<ggml_tensor *> k_layer, v_layer;
     int kv_n = 0, kv_head = 0;
     std::vector<char> compute_mem;
+    // GGUF-loaded models: kv index, tensors by name, tokenizer tables (src/gemma_model.cpp:200-214)
+    std::map<std::string, int> kv_index;
+    std::map<std::string, ggml_tensor *> tensors;
+    std::vector<std::string> tokens;
+    int32_t bos = -1, eos = -1;
 };
 
 enum stage { PREFILL, DECODE };
@@ -81,6 +94,72 @@ bool load_weights(model &m, const char *path) {
     }
     fclose(f);
     return ok;
+}
+
+// ---- GGUF loading (src/gemma_model.cpp:19-50 load_model_from_file and the helpers it calls) ----
+uint32_t get_u32(gguf_context *g, model &m, const char *key) { return gguf_get_val_u32(g, m.kv_index.at(key)); }
+
+bool load_model_from_file(model &m, const char *path) {
+    gguf_init_params gp = {false, &m.weight_ctx};
+    gguf_context *g = gguf_init_from_file(path, gp);
+    if (!g) return false;
+    for (int i = 0; i < gguf_get_n_kv(g); ++i) m.kv_index[gguf_get_key(g, i)] = i;  // :596-603
+    for (int i = 0; i < gguf_get_n_tensors(g); ++i) {                               // :583-593
+        const char *name = gguf_get_tensor_name(g, i);
+        m.tensors[name] = ggml_get_tensor(m.weight_ctx, name);
+    }
+    auto get = [&](const std::string &n) -> ggml_tensor * {
+        auto it = m.tensors.find(n);
+        return it == m.tensors.end() ? nullptr : it->second;
+    };
+    hparams &h = m.hp;  // init_hyper_param (:403-415)
+    h.n_layer = (int)get_u32(g, m, "gemma.block_count");
+    h.n_embd = (int)get_u32(g, m, "gemma.embedding_length");
+    h.n_head = (int)get_u32(g, m, "gemma.attention.head_count");
+    h.n_head_kv = (int)get_u32(g, m, "gemma.attention.head_count_kv");
+    h.eps = gguf_get_val_f32(g, m.kv_index.at("gemma.attention.layer_norm_rms_epsilon"));
+    h.head_dim = m.kv_index.count("gemma.attention.key_length") ? (int)get_u32(g, m, "gemma.attention.key_length")
+                                                                 : h.n_embd / h.n_head;
+    // composite_model (:145-182): the tied output is token_embd
+    m.token_embd = get("token_embd.weight");
+    m.output_norm = get("output_norm.weight");
+    if (!m.token_embd || !m.output_norm) return false;
+    h.n_vocab = (int)m.token_embd->ne[1];
+    h.wtype = (int)m.token_embd->type;
+    char name[64];
+    for (int il = 0; il < h.n_layer; ++il) {
+        layer_w L;
+        ggml_tensor **slots[9] = {&L.o, &L.k, &L.v, &L.q, &L.gate, &L.up, &L.down, &L.attn_norm, &L.ffn_norm};
+        const char *names[9] = {"attn_output", "attn_k", "attn_v", "attn_q", "ffn_gate", "ffn_up", "ffn_down",
+                                "attn_norm", "ffn_norm"};
+        for (int k = 0; k < 9; ++k) {
+            snprintf(name, sizeof(name), "blk.%d.%s.weight", il, names[k]);
+            if (!(*slots[k] = get(name))) {
+                fprintf(stderr, "missing tensor %s\n", name);
+                return false;
+            }
+        }
+        m.layers.push_back(L);
+    }
+    h.n_ff = (int)m.layers[0].gate->ne[1];
+    // load_tokenizer (:200-214)
+    m.bos = (int32_t)get_u32(g, m, "tokenizer.ggml.bos_token_id");
+    m.eos = (int32_t)get_u32(g, m, "tokenizer.ggml.eos_token_id");
+    const int it = m.kv_index.at("tokenizer.ggml.tokens");
+    for (int i = 0; i < gguf_get_arr_n(g, it); ++i) m.tokens.push_back(gguf_get_arr_str(g, it, i));
+    gguf_free(g);
+    return true;
+}
+
+// gemma_tokenizer::print_tokens (:757-767): concatenate, drop "<bos>", U+2581 -> ' '
+std::string detokenize(const model &m, const std::vector<int32_t> &ids) {
+    std::string s;
+    for (int32_t id : ids) s += m.tokens.at(id);
+    const size_t b = s.find("<bos>");
+    if (b != std::string::npos) s.replace(b, 5, "");
+    const std::string u = "\xe2\x96\x81";
+    for (size_t p = 0; (p = s.find(u, p)) != std::string::npos;) s.replace(p, u.size(), " ");
+    return s;
 }
 
 void init_input_tensor(model &m) {  // src/gemma_model.cpp:341-359
@@ -230,18 +309,31 @@ int32_t greedy_sample(const ggml_tensor *out, std::vector<float> &row) {  // :53
 }  // namespace
 
 int main(int argc, char **argv) {
-    if (argc < 14) {
-        fprintf(stderr, "usage: %s weights prompt out n_layer n_embd n_head n_head_kv head_dim n_ff n_vocab ctx wtype n_decode\n",
-                argv[0]);
+    const size_t alen = argc > 1 ? strlen(argv[1]) : 0;
+    const bool gguf = alen > 5 && strcmp(argv[1] + alen - 5, ".gguf") == 0;
+    if ((gguf && argc < 6) || (!gguf && argc < 14)) {
+        fprintf(stderr, "usage: %s model.gguf prompt out ctx n_decode\n"
+                        "       %s weights prompt out n_layer n_embd n_head n_head_kv head_dim n_ff n_vocab ctx wtype n_decode\n",
+                argv[0], argv[0]);
         return 2;
     }
     model m;
-    m.hp = {atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8]), atoi(argv[9]), atoi(argv[10]),
-            atoi(argv[11]), atoi(argv[12])};
-    const int n_decode = atoi(argv[13]);
-    if (!load_weights(m, argv[1])) {
-        fprintf(stderr, "weights: read failed\n");
-        return 1;
+    int n_decode;
+    if (gguf) {
+        if (!load_model_from_file(m, argv[1])) {
+            fprintf(stderr, "gguf: load failed\n");
+            return 1;
+        }
+        m.hp.ctx = atoi(argv[4]);
+        n_decode = atoi(argv[5]);
+    } else {
+        m.hp = {atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8]), atoi(argv[9]), atoi(argv[10]),
+                atoi(argv[11]), atoi(argv[12])};
+        n_decode = atoi(argv[13]);
+        if (!load_weights(m, argv[1])) {
+            fprintf(stderr, "weights: read failed\n");
+            return 1;
+        }
     }
     std::vector<int32_t> input;
     {
@@ -278,6 +370,14 @@ int main(int argc, char **argv) {
     }
     fwrite(toks.data(), 4, toks.size(), out);
     fclose(out);
+    if (gguf) {  // the sequence as text, through the GGUF tokenizer table
+        const std::string txt = detokenize(m, input);
+        FILE *tf = fopen((std::string(argv[3]) + ".txt").c_str(), "wb");
+        if (tf) {
+            fwrite(txt.data(), 1, txt.size(), tf);
+            fclose(tf);
+        }
+    }
     ggml_free(m.compute_ctx);
     ggml_backend_buffer_free(m.input_buf);
     ggml_backend_buffer_free(m.kv_buf);

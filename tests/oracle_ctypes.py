@@ -25,7 +25,7 @@ class OrcConfig(C.Structure):
     _fields_ = [("n_layer", C.c_int), ("n_embd", C.c_int), ("n_head", C.c_int), ("n_head_kv", C.c_int),
                 ("head_dim", C.c_int), ("n_ff", C.c_int), ("n_vocab", C.c_int), ("n_ctx", C.c_int),
                 ("wtype", C.c_int), ("eps", C.c_float), ("rope_base", C.c_float), ("seed", C.c_uint64),
-                ("gelu_clamp", C.c_int)]
+                ("gelu_clamp", C.c_int), ("kmix", C.c_int)]
 
 
 _lib = None
@@ -48,7 +48,8 @@ def lib():
     L.orc_table_gelu_f16.restype = vp
     for fn in ("orc_quantize_row_q4_0_ref", "orc_quantize_row_q8_0_ref", "orc_quantize_row_q8_0"):
         getattr(L, fn).argtypes = [vp, vp, C.c_int]
-    for fn in ("orc_dequantize_row_q4_0", "orc_dequantize_row_q8_0"):
+    for fn in ("orc_dequantize_row_q4_0", "orc_dequantize_row_q8_0", "orc_dequantize_row_q4_K",
+               "orc_dequantize_row_q6_K"):
         getattr(L, fn).argtypes = [vp, vp, C.c_int]
     L.orc_row_size.restype = C.c_size_t
     L.orc_row_size.argtypes = [C.c_int, i64]
@@ -178,9 +179,19 @@ GEMMA_7B = dict(n_layer=28, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, 
 TINY = dict(n_layer=2, n_embd=512, n_head=2, n_head_kv=1, head_dim=256, n_ff=2048, n_vocab=4096)
 
 
-def make_config(shape, n_ctx=512, wtype=Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0, gelu_clamp=0):
+def make_config(shape, n_ctx=512, wtype=Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0, gelu_clamp=0, kmix=0):
     return OrcConfig(n_ctx=n_ctx, wtype=wtype, eps=eps, rope_base=rope_base, seed=seed, gelu_clamp=gelu_clamp,
-                     **shape)
+                     kmix=kmix, **shape)
+
+
+def dequantize(wtype, row_bytes, k):
+    """ggml dequantize_row_{q4_0,q8_0,q4_K,q6_K} of one row (get_rows)."""
+    fn = {Q4_0: "orc_dequantize_row_q4_0", Q8_0: "orc_dequantize_row_q8_0", Q4_K: "orc_dequantize_row_q4_K",
+          Q6_K: "orc_dequantize_row_q6_K"}[wtype]
+    src = np.ascontiguousarray(row_bytes, dtype=np.uint8)
+    out = np.zeros(k, dtype=np.float32)
+    getattr(lib(), fn)(ptr(src), ptr(out), k)
+    return out
 
 
 class Model:
@@ -188,6 +199,8 @@ class Model:
         self.cfg = cfg
         self.L = lib()
         self.h = self.L.orc_model_create(C.byref(cfg))
+        if not self.h:
+            raise ValueError("orc_model_create rejected the config")
 
     def close(self):
         if self.h:

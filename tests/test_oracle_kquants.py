@@ -86,3 +86,104 @@ def test_kquant_mul_mat_matches_vec_dot():
     for c in range(2):
         for r in range(rows):
             assert Y[c, r] == np.float32(O.vec_dot_k(O.Q4_K, W[r], wdata[c], k, "avx2"))
+
+
+# ---- dequantize_row_q4_K / q6_K (get_rows on a K-quant token_embd) -------------------------------
+def _q4_K_scale_min(scales, j):
+    """get_scale_min_k4 of ggml (the 6-bit packing src/kernals.cl:79-84 unpacks), written out."""
+    if j < 4:
+        return scales[j] & 63, scales[j + 4] & 63
+    return (scales[j + 4] & 0xF) | ((scales[j - 4] >> 6) << 4), (scales[j + 4] >> 4) | ((scales[j] >> 6) << 4)
+
+
+def _deq_q4_K_np(blocks):
+    """numpy float32 restatement (same op order: d1 = d*sc, m1 = dmin*m, y = d1*q - m1)."""
+    out = []
+    for b in blocks.reshape(-1, 144):
+        d = np.frombuffer(b[0:2].tobytes(), np.float16)[0].astype(np.float32)
+        dmin = np.frombuffer(b[2:4].tobytes(), np.float16)[0].astype(np.float32)
+        sc = b[4:16]
+        q = b[16:]
+        for j in range(4):
+            s1, m1 = _q4_K_scale_min(sc, 2 * j)
+            s2, m2 = _q4_K_scale_min(sc, 2 * j + 1)
+            d1, mm1 = np.float32(d * np.float32(s1)), np.float32(dmin * np.float32(m1))
+            d2, mm2 = np.float32(d * np.float32(s2)), np.float32(dmin * np.float32(m2))
+            qq = q[32 * j:32 * j + 32]
+            out.append((d1 * (qq & 15).astype(np.float32)).astype(np.float32) - mm1)
+            out.append((d2 * (qq >> 4).astype(np.float32)).astype(np.float32) - mm2)
+    return np.concatenate(out).astype(np.float32)
+
+
+def _deq_q6_K_np(blocks):
+    out = []
+    for b in blocks.reshape(-1, 210):
+        ql, qh = b[0:128].astype(np.int32), b[128:192].astype(np.int32)
+        sc = b[192:208].view(np.int8).astype(np.float32)
+        d = np.frombuffer(b[208:210].tobytes(), np.float16)[0].astype(np.float32)
+        y = np.zeros(256, np.float32)
+        for n in range(2):
+            L, H, S = ql[64 * n:64 * n + 64], qh[32 * n:32 * n + 32], sc[8 * n:8 * n + 8]
+            l = np.arange(32)
+            is_ = l // 16
+            qs = [(L[l] & 15) | ((H >> 0) & 3) << 4, (L[l + 32] & 15) | ((H >> 2) & 3) << 4,
+                  (L[l] >> 4) | ((H >> 4) & 3) << 4, (L[l + 32] >> 4) | ((H >> 6) & 3) << 4]
+            for g in range(4):
+                y[128 * n + 32 * g + l] = (d * S[is_ + 2 * g]).astype(np.float32) * (qs[g] - 32).astype(np.float32)
+        out.append(y)
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("wtype", [O.Q4_K, O.Q6_K])
+def test_dequantize_k_matches_numpy_restatement(wtype):
+    k = 1024
+    blocks = O.synth_kquant(wtype, 11, 1, k)
+    got = O.dequantize(wtype, blocks, k)
+    ref = _deq_q4_K_np(blocks) if wtype == O.Q4_K else _deq_q6_K_np(blocks)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_dequantize_k_known_answers():
+    # Q4_K: d = 1, dmin = 0.5, scales all 1 / mins all 2 -> y = q - 1 exactly
+    b = np.zeros(144, np.uint8)
+    b[0:2] = np.frombuffer(np.float16(1.0).tobytes(), np.uint8)
+    b[2:4] = np.frombuffer(np.float16(0.5).tobytes(), np.uint8)
+    b[4:8], b[8:12] = 1, 2          # j < 4: sc = scales[j] & 63, m = scales[j+4] & 63
+    b[12:16] = 0x21                 # j >= 4: sc = low nibble | ..., m = high nibble | ...
+    b[16:] = np.arange(128, dtype=np.uint8)
+    y = O.dequantize(O.Q4_K, b, 256)
+    q = np.concatenate([np.r_[np.arange(32 * j, 32 * j + 32) & 15, np.arange(32 * j, 32 * j + 32) >> 4]
+                        for j in range(4)]).astype(np.float32)
+    assert np.array_equal(y, q - 1.0)
+    # Q6_K: d = 1, scales = 1: y = q6 - 32; all-zero quants -> -32
+    b = np.zeros(210, np.uint8)
+    b[192:208] = 1
+    b[208:210] = np.frombuffer(np.float16(1.0).tobytes(), np.uint8)
+    assert np.all(O.dequantize(O.Q6_K, b, 256) == -32.0)
+    b[0:128] = 0xFF
+    b[128:192] = 0xFF
+    assert np.all(O.dequantize(O.Q6_K, b, 256) == 31.0)
+
+
+KMIX = dict(n_layer=2, n_embd=256, n_head=2, n_head_kv=1, head_dim=128, n_ff=512, n_vocab=1024)
+
+
+def test_kmix_model_avx2_equals_ordered_and_prefill_equals_decode():
+    cfg = O.make_config(KMIX, n_ctx=64, kmix=1)
+    m = O.Model(cfg)
+    prompt = O.make_prompt(9, KMIX["n_vocab"])
+    seq, logits = m.generate(prompt, 4, avx2=True)
+    seq_o, logits_o = m.generate(prompt, 4, avx2=False)
+    assert seq == seq_o and np.array_equal(logits, logits_o)
+    assert np.all(np.isfinite(logits)) and np.std(logits[-1]) > 0
+    # the whole sequence in one PREFILL reproduces each decode step's last row
+    m.reset()
+    _, _, allv = m.inference(np.array(seq[:-1], np.int32), 0, want_all=True)
+    for i in range(5):
+        assert np.array_equal(allv[len(prompt) - 1 + i], logits[i])
+    m.close()
+
+
+def test_kmix_rejects_unaligned_shapes():
+    with pytest.raises(ValueError):
+        O.Model(O.make_config(dict(KMIX, n_embd=384), n_ctx=64, kmix=1))
