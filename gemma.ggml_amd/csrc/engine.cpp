@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/gemma_hpc.h"
+#include "../../include/ggml.h"
 #include "kernels.h"
 
 namespace ghip {
@@ -162,6 +163,13 @@ struct gemma_engine {
     hipStream_t stream = nullptr;
     int qw = 0, kvw = 0, qkv_rows = 0;
     tiled_mat embd;
+    // token_embd / tied output in Q6_K (llama.cpp's Q4_0 / Q8_0 Gemma files): raw ggml rows, the
+    // embedding dequantized by k_embed_q6K and the logits through the K-quant matvec
+    int out_type = 0;
+    uint8_t *embd_q6k = nullptr;
+    int64_t embd_row_bytes = 0;
+    uint8_t *xq8k = nullptr;  // Q8_K rows of rms_norm(x)*out_norm (decode: 1 row; prefill: T rows)
+    int64_t xq8k_rows = 0;
     float *out_norm = nullptr;
     std::vector<layer_dev> layers;
     uint16_t *kc = nullptr, *vc = nullptr;  // [L][ctx][kvw], [L][kvw][ctx]
@@ -275,6 +283,9 @@ static int enqueue_step(gemma_engine *e) {
     const int wt = c.wtype;
     hipStream_t s = e->stream;
     const int E = c.n_embd;
+    if (e->out_type == T_Q6_K &&
+        launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s))
+        return -1;
     for (int il = 0; il < c.n_layer; ++il) {
         // K1: [embed | rms_norm*attn_norm] + quantize -> Wq|Wk|Wv   (:677-696); each rank its rows
         for (int vr = 0; vr < e->n_virtual; ++vr) {
@@ -284,7 +295,7 @@ static int enqueue_step(gemma_engine *e) {
             a.nb = L.qkv.nb;
             a.norm_w = L.attn_norm; a.eps = c.eps;
             int pro = PRO_NORM;
-            if (il == 0) {
+            if (il == 0 && e->out_type != T_Q6_K) {
                 pro = PRO_EMBED;
                 a.x = e->hist; a.tok_pos = e->pos;
                 a.emb_qs = e->embd.qs; a.emb_sc = e->embd.sc; a.emb_n_bt = e->embd.n_bt;
@@ -377,6 +388,15 @@ static int enqueue_step(gemma_engine *e) {
     // never overwritten: hist writes only land at positions >= n_prompt
     rope_row rr;
     rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+    if (e->out_type == T_Q6_K) {  // rms_norm*out_norm -> Q8_K -> Q6_K tied output -> argmax
+        if (launch_norm_q8K(e->x, E, e->out_norm, E, c.eps, 1, e->xq8k, (E / 256) * 292, s)) return -1;
+        kq_args k;
+        k.w = e->embd_q6k; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = E / 256;
+        k.x = e->xq8k; k.x_col_stride = (E / 256) * 292; k.y = e->logits; k.y_col_stride = c.n_vocab; k.ncols = 1;
+        if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
+        if (launch_row_argmax(e->logits, c.n_vocab, e->key, 256, s)) return -1;
+        return launch_advance(e->key, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
+    }
     int lg_grid = 0;
     for (int vr = 0; vr < e->n_virtual; ++vr) {
         const int rk = rank_of(e, vr);
@@ -403,12 +423,40 @@ static int enqueue_step(gemma_engine *e) {
     return launch_advance(e->rank_keys, e->tp_n, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
 }
 
-static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int tp_n, int tp_rank, const void *nccl_id) {
+// real weights in ggml row-major layout (a GGUF file's tensors, src/gemma_model.cpp:145-182)
+struct host_weights {
+    const void *embd = nullptr;  // token_embd, type cfg.out_type (or wtype)
+    const float *out_norm = nullptr;
+    struct layer {
+        const float *attn_norm = nullptr, *ffn_norm = nullptr;
+        const void *q = nullptr, *k = nullptr, *v = nullptr, *o = nullptr, *gate = nullptr, *up = nullptr, *down = nullptr;
+    };
+    std::vector<layer> layers;
+};
+
+// rows [r0, r0 + dst.rows) of a host row-major Q4_0 / Q8_0 matrix into the tiled layout
+static int upload_rows(const tiled_mat &dst, const void *host, int64_t r0, hipStream_t s) {
+    const int64_t rb = dst.nb * (dst.type == T_Q4_0 ? 18 : 34);
+    uint8_t *tmp = nullptr;
+    GHIP_CHECK(hipMalloc(&tmp, (size_t)(rb * dst.rows)));
+    GHIP_CHECK(hipMemcpyAsync(tmp, (const uint8_t *)host + r0 * rb, (size_t)(rb * dst.rows), hipMemcpyHostToDevice, s));
+    const int rc = launch_repack(dst, tmp, rb, s);
+    GHIP_CHECK(hipStreamSynchronize(s));
+    GHIP_CHECK(hipFree(tmp));
+    return rc;
+}
+
+static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int tp_n, int tp_rank, const void *nccl_id,
+                                   const host_weights *hw = nullptr) {
     set_error("");
     const gemma_hip_config &c = *cfg;
     if (c.head_dim % 32 || c.n_embd % 32 || c.n_ff % 32 || c.n_ctx % 32 || c.n_head % c.n_head_kv ||
-        (c.wtype != T_Q4_0 && c.wtype != T_Q8_0)) {
+        (c.wtype != T_Q4_0 && c.wtype != T_Q8_0) || (c.out_type != 0 && c.out_type != c.wtype && c.out_type != T_Q6_K)) {
         set_error("gemma_engine_create: unsupported config");
+        return nullptr;
+    }
+    if (c.out_type == T_Q6_K && (c.n_embd % 256 || c.n_embd > 4096 || tp_n > 1)) {
+        set_error("gemma_engine_create: a Q6_K output needs n_embd % 256 == 0, n_embd <= 4096 and one rank");
         return nullptr;
     }
     if (hipSetDevice(device) != hipSuccess) {
@@ -442,10 +490,30 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     const uint64_t seed = c.seed;
     hipStream_t s = e->stream;
     // weights: synthetic generator straight into the tiled layout (matches oracle/gemma_cpu.cpp)
-    e->embd = alloc_tiled(wt, c.n_vocab, c.n_embd, s);
-    launch_synth_tiled(e->embd, tensor_key(seed, TID_EMBD), synth_scale(1.0 / sqrt((double)c.n_embd)), 0, s);
+    bool up_fail = false;  // a host-weight upload failed (last_error says which)
+    e->out_type = c.out_type == T_Q6_K ? T_Q6_K : wt;
+    if (e->out_type == T_Q6_K) {  // oracle make_kmat(TID_EMBD, Q6_K, 1/sqrt(E)) on the device
+        e->embd_row_bytes = (int64_t)c.n_embd / 256 * 210;
+        GHIP_FATAL(hipMalloc(&e->embd_q6k, (size_t)(e->embd_row_bytes * c.n_vocab)));
+        GHIP_FATAL(hipMalloc(&e->xq8k, (size_t)c.n_embd / 256 * 292));
+        e->xq8k_rows = 1;
+        if (!hw)
+            launch_synth_kquant(T_Q6_K, e->embd_q6k, c.n_vocab, c.n_embd, tensor_key(seed, TID_EMBD),
+                                (float)(1.0 / sqrt((double)c.n_embd) / 0.68), s);
+    } else {
+        e->embd = alloc_tiled(wt, c.n_vocab, c.n_embd, s);
+        if (!hw) launch_synth_tiled(e->embd, tensor_key(seed, TID_EMBD), synth_scale(1.0 / sqrt((double)c.n_embd)), 0, s);
+    }
     GHIP_FATAL(hipMalloc(&e->out_norm, (size_t)c.n_embd * 4));
-    launch_synth_norm(e->out_norm, c.n_embd, tensor_key(seed, TID_OUT_NORM), synth_scale(0.05), s);
+    if (hw) {
+        if (e->out_type == T_Q6_K)
+            GHIP_FATAL(hipMemcpy(e->embd_q6k, hw->embd, (size_t)(e->embd_row_bytes * c.n_vocab), hipMemcpyHostToDevice));
+        else
+            up_fail |= upload_rows(e->embd, hw->embd, 0, s) != 0;
+        GHIP_FATAL(hipMemcpy(e->out_norm, hw->out_norm, (size_t)c.n_embd * 4, hipMemcpyHostToDevice));
+    } else {
+        launch_synth_norm(e->out_norm, c.n_embd, tensor_key(seed, TID_OUT_NORM), synth_scale(0.05), s);
+    }
     e->n_virtual = (tp_n > 1 && !nccl_id) ? tp_n : 1;
     e->layers.resize((size_t)c.n_layer * e->n_virtual);
     const double se = 1.0 / sqrt((double)c.n_embd), sq = 1.0 / sqrt((double)e->qw), sf = 1.0 / sqrt((double)c.n_ff);
@@ -456,8 +524,13 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         if (vr == 0) {
             GHIP_FATAL(hipMalloc(&L.attn_norm, (size_t)c.n_embd * 4));
             GHIP_FATAL(hipMalloc(&L.ffn_norm, (size_t)c.n_embd * 4));
-            launch_synth_norm(L.attn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_ATTN_NORM)), synth_scale(0.05), s);
-            launch_synth_norm(L.ffn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_FFN_NORM)), synth_scale(0.05), s);
+            if (hw) {
+                GHIP_FATAL(hipMemcpy(L.attn_norm, hw->layers[il].attn_norm, (size_t)c.n_embd * 4, hipMemcpyHostToDevice));
+                GHIP_FATAL(hipMemcpy(L.ffn_norm, hw->layers[il].ffn_norm, (size_t)c.n_embd * 4, hipMemcpyHostToDevice));
+            } else {
+                launch_synth_norm(L.attn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_ATTN_NORM)), synth_scale(0.05), s);
+                launch_synth_norm(L.ffn_norm, c.n_embd, tensor_key(seed, tid_layer(il, L_FFN_NORM)), synth_scale(0.05), s);
+            }
         } else {  // norms are replicated: the slot-0 copy serves every virtual rank
             L.attn_norm = layer_of(e, il, 0).attn_norm;
             L.ffn_norm = layer_of(e, il, 0).ffn_norm;
@@ -467,11 +540,28 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         L.qkv = alloc_tiled(wt, qn, c.n_embd, s);
         const int64_t src_start[3] = {0, e->qw, e->qw + e->kvw}, src_rows[3] = {e->qw, e->kvw, e->kvw};
         const int src_tid[3] = {L_Q, L_K, L_V};
+        const void *src_host[3] = {hw ? hw->layers[il].q : nullptr, hw ? hw->layers[il].k : nullptr,
+                                   hw ? hw->layers[il].v : nullptr};
         for (int k = 0; k < 3; ++k) {
             const int64_t a0 = std::max(q0, src_start[k]), a1 = std::min(q0 + qn, src_start[k] + src_rows[k]);
-            if (a1 > a0)
+            if (a1 > a0 && hw) {
+                up_fail |= upload_rows(sub_rows(L.qkv, a0 - q0, a1 - a0), src_host[k], a0 - src_start[k], s) != 0;
+            } else if (a1 > a0) {
                 launch_synth_tiled(sub_rows(L.qkv, a0 - q0, a1 - a0), tensor_key(seed, tid_layer(il, src_tid[k])),
                                    synth_scale(se), a0 - src_start[k], s);
+            }
+        }
+        if (hw) {
+            const host_weights::layer &H = hw->layers[il];
+            L.o = alloc_tiled(wt, e->sh_e, e->qw, s);
+            L.gate = alloc_tiled(wt, e->sh_ff, c.n_embd, s);
+            L.up = alloc_tiled(wt, e->sh_ff, c.n_embd, s);
+            L.down = alloc_tiled(wt, e->sh_e, c.n_ff, s);
+            up_fail |= upload_rows(L.o, H.o, (int64_t)tp_rank * e->sh_e, s) != 0;
+            up_fail |= upload_rows(L.gate, H.gate, (int64_t)tp_rank * e->sh_ff, s) != 0;
+            up_fail |= upload_rows(L.up, H.up, (int64_t)tp_rank * e->sh_ff, s) != 0;
+            up_fail |= upload_rows(L.down, H.down, (int64_t)tp_rank * e->sh_e, s) != 0;
+            continue;
         }
         L.o = alloc_tiled(wt, e->sh_e, e->qw, s);
         launch_synth_tiled(L.o, tensor_key(seed, tid_layer(il, L_O)), synth_scale(4.0 * sq), (int64_t)tp_rank * e->sh_e, s);
@@ -482,6 +572,10 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         L.down = alloc_tiled(wt, e->sh_e, c.n_ff, s);
         launch_synth_tiled(L.down, tensor_key(seed, tid_layer(il, L_DOWN)), synth_scale(4.0 * sf), (int64_t)tp_rank * e->sh_e,
                            s);
+    }
+    if (up_fail) {
+        gemma_engine_free(e);
+        return nullptr;
     }
     // caches, tables, activations
     const size_t kv_elems = (size_t)c.n_layer * c.n_ctx * e->kvw;
@@ -563,6 +657,95 @@ extern "C" gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int de
     return engine_create(cfg, device, 1, 0, nullptr);
 }
 
+// A Gemma GGUF file: hyper parameters as src/gemma_model.cpp:403-415 reads them (head_dim =
+// gemma.attention.key_length when present, else n_embd / n_head as the reference computes it;
+// rope base gemma.rope.freq_base, else 10000 as src/macro.h), tensors by the names of :145-182.
+extern "C" gemma_engine *gemma_engine_create_from_gguf(const char *path, int n_ctx, int device) {
+    set_error("");
+    ggml_context *w = nullptr;
+    gguf_init_params gp = {false, &w};
+    gguf_context *g = gguf_init_from_file(path, gp);
+    if (!g) return nullptr;
+    std::string err;
+    auto u32 = [&](const char *key, int def) -> int {
+        const int i = gguf_find_key(g, key);
+        if (i < 0 || gguf_get_kv_type(g, i) != GGUF_TYPE_UINT32) {
+            if (def < 0 && err.empty()) err = std::string("missing u32 key ") + key;
+            return def;
+        }
+        return (int)gguf_get_val_u32(g, i);
+    };
+    auto f32 = [&](const char *key, float def) -> float {
+        const int i = gguf_find_key(g, key);
+        return i >= 0 && gguf_get_kv_type(g, i) == GGUF_TYPE_FLOAT32 ? gguf_get_val_f32(g, i) : def;
+    };
+    gemma_hip_config c{};
+    c.n_layer = u32("gemma.block_count", -1);
+    c.n_embd = u32("gemma.embedding_length", -1);
+    c.n_head = u32("gemma.attention.head_count", -1);
+    c.n_head_kv = u32("gemma.attention.head_count_kv", -1);
+    c.head_dim = c.n_head > 0 ? u32("gemma.attention.key_length", c.n_embd / c.n_head) : 0;
+    c.eps = f32("gemma.attention.layer_norm_rms_epsilon", 1e-6f);
+    c.rope_base = f32("gemma.rope.freq_base", 10000.0f);
+    c.n_ctx = n_ctx;
+    const int qw = c.n_head * c.head_dim, kvw = c.n_head_kv * c.head_dim;
+    auto tensor = [&](const std::string &name, int type, int64_t ne0, int64_t ne1) -> const void * {
+        ggml_tensor *t = err.empty() ? ggml_get_tensor(w, name.c_str()) : nullptr;
+        if (!err.empty()) return nullptr;
+        if (!t) {
+            err = "missing tensor " + name;
+            return nullptr;
+        }
+        if ((type >= 0 && (int)t->type != type) || t->ne[0] != ne0 || t->ne[1] != ne1 || t->ne[2] != 1) {
+            err = "tensor " + name + ": type " + std::to_string(t->type) + " [" + std::to_string(t->ne[0]) + ", " +
+                  std::to_string(t->ne[1]) + "] does not fit this engine";
+            return nullptr;
+        }
+        return t->data;
+    };
+    host_weights hw;
+    ggml_tensor *te = err.empty() ? ggml_get_tensor(w, "token_embd.weight") : nullptr;
+    ggml_tensor *tq = err.empty() ? ggml_get_tensor(w, "blk.0.attn_q.weight") : nullptr;
+    ggml_tensor *tg = err.empty() ? ggml_get_tensor(w, "blk.0.ffn_gate.weight") : nullptr;
+    if (err.empty() && (!te || !tq || !tg)) err = "missing token_embd / blk.0 tensors";
+    if (err.empty()) {
+        c.n_vocab = (int)te->ne[1];
+        c.n_ff = (int)tg->ne[1];
+        c.wtype = (int)tq->type;
+        c.out_type = te->type == GGML_TYPE_Q6_K ? T_Q6_K : 0;
+        if ((c.wtype != T_Q4_0 && c.wtype != T_Q8_0) || (te->type != tq->type && te->type != GGML_TYPE_Q6_K))
+            err = "layer matrices must all be Q4_0 or all Q8_0, token_embd that type or Q6_K";
+    }
+    hw.embd = tensor("token_embd.weight", c.out_type ? T_Q6_K : c.wtype, c.n_embd, c.n_vocab);
+    hw.out_norm = (const float *)tensor("output_norm.weight", GGML_TYPE_F32, c.n_embd, 1);
+    for (int il = 0; il < c.n_layer && err.empty(); ++il) {
+        const std::string b = "blk." + std::to_string(il) + ".";
+        host_weights::layer L;
+        L.attn_norm = (const float *)tensor(b + "attn_norm.weight", GGML_TYPE_F32, c.n_embd, 1);
+        L.ffn_norm = (const float *)tensor(b + "ffn_norm.weight", GGML_TYPE_F32, c.n_embd, 1);
+        L.q = tensor(b + "attn_q.weight", c.wtype, c.n_embd, qw);
+        L.k = tensor(b + "attn_k.weight", c.wtype, c.n_embd, kvw);
+        L.v = tensor(b + "attn_v.weight", c.wtype, c.n_embd, kvw);
+        L.o = tensor(b + "attn_output.weight", c.wtype, qw, c.n_embd);
+        L.gate = tensor(b + "ffn_gate.weight", c.wtype, c.n_embd, c.n_ff);
+        L.up = tensor(b + "ffn_up.weight", c.wtype, c.n_embd, c.n_ff);
+        L.down = tensor(b + "ffn_down.weight", c.wtype, c.n_ff, c.n_embd);
+        hw.layers.push_back(L);
+    }
+    gemma_engine *e = nullptr;
+    if (err.empty()) e = engine_create(&c, device, 1, 0, nullptr, &hw);
+    else set_error("gemma_engine_create_from_gguf: " + std::string(path) + ": " + err);
+    gguf_free(g);
+    ggml_free(w);  // the device holds the weights now
+    return e;
+}
+
+extern "C" int gemma_engine_config(const gemma_engine *e, gemma_hip_config *out) {
+    if (!e || !out) return -1;
+    *out = e->cfg;
+    return 0;
+}
+
 // row-split tensor parallelism: one process per GPU; rank 0 makes the id, every rank gets a copy
 extern "C" int gemma_tp_unique_id(void *out, int cap) {
     set_error("");
@@ -610,6 +793,8 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
                     e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.XH, e->pf.keys};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
+    if (e->embd_q6k) (void)hipFree(e->embd_q6k);
+    if (e->xq8k) (void)hipFree(e->xq8k);
     (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -724,6 +909,12 @@ extern "C" int64_t gemma_engine_tensor(gemma_engine *e, int tid, void *dst, int6
         GHIP_CHECK(hipFree(tmp));
         return bytes;
     };
+    if (tid == TID_EMBD && e->out_type == T_Q6_K) {
+        const int64_t bytes = e->embd_row_bytes * c.n_vocab;
+        if (cap < bytes) return -1;
+        GHIP_CHECK(hipMemcpy(dst, e->embd_q6k, (size_t)bytes, hipMemcpyDeviceToHost));
+        return bytes;
+    }
     if (tid == TID_EMBD) return copy_mat(e->embd);
     if (tid == TID_OUT_NORM) return copy_f32(e->out_norm, c.n_embd);
     const int il = (tid - 16) / 16, k = (tid - 16) % 16;
@@ -800,6 +991,10 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
             break;
     }
     };
+    if (which == 4 && e->out_type == T_Q6_K) {
+        set_error("gemma_engine_time: the logits kernel of a Q6_K output is the K-quant matvec (gemma_kq_time)");
+        return -1.0;
+    }
     if (which < 0 || which > 5) {
         set_error("gemma_engine_time: bad kernel id");
         return -1.0;
@@ -897,6 +1092,7 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
     const int order[MC_N] = {MC_DOWN, MC_GU, MC_QKV, MC_O, MC_LOGITS};
     for (int oi = 0; oi < MC_N && rc == 0; ++oi) {
         const int cls = order[oi];
+        if (cls == MC_LOGITS && e->out_type == T_Q6_K) continue;  // the K-quant matvec has no plan
         std::vector<launch_plan> cands;
         const bool splits = cls == MC_QKV || cls == MC_O || cls == MC_DOWN;
         for (int ks = 1; ks <= (splits ? 8 : 1); ks *= 2) {
@@ -1037,9 +1233,12 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
     };
     int n_kv = 32 * (T / 32 + 1);  // src/gemma_model.cpp:429 with n_total = T
     if (n_kv > c.n_ctx) n_kv = c.n_ctx;
+    const bool q6 = e->out_type == T_Q6_K;
+    if (q6 && launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, nullptr, T, (int)E, sqrtf((float)E), p.X, s))
+        return -1;
     for (int il = 0; il < c.n_layer; ++il) {
         layer_dev &L = e->layers[il];
-        if (quant(il == 0 ? QR_EMBED_NORM : QR_NORM, p.X, nullptr, E, L.attn_norm)) return -1;
+        if (quant(il == 0 && !q6 ? QR_EMBED_NORM : QR_NORM, p.X, nullptr, E, L.attn_norm)) return -1;
         if (gemm(L.qkv, EPI_STORE, nullptr, p.QKV, e->qkv_rows)) return -1;
         ropekv_args r;
         r.qkv = p.QKV; r.ldqkv = e->qkv_rows; r.rope_cos = e->rope_cos; r.rope_sin = e->rope_sin; r.q16 = p.Q16;
@@ -1060,8 +1259,22 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
         if (gemm(L.down, EPI_ADD, p.SA, p.X, E)) return -1;
         if (taps) GHIP_CHECK(hipMemcpyAsync(taps + (size_t)il * T * E, p.X, (size_t)T * E * 4, hipMemcpyDeviceToDevice, s));
     }
-    if (quant(QR_NORM, p.X, nullptr, E, e->out_norm)) return -1;
-    if (gemm(e->embd, EPI_STORE, nullptr, p.LG, c.n_vocab)) return -1;
+    if (q6) {  // Q6_K tied output: Q8_K INIT of every row, then the K-quant dot per (vocab row, position)
+        const int64_t ld = E / 256 * 292;
+        if (e->xq8k_rows < T) {
+            GHIP_CHECK(hipFree(e->xq8k));
+            GHIP_CHECK(hipMalloc(&e->xq8k, (size_t)(ld * T)));
+            e->xq8k_rows = T;
+        }
+        if (launch_norm_q8K(p.X, E, e->out_norm, (int)E, c.eps, T, e->xq8k, ld, s)) return -1;
+        kq_args k;
+        k.w = e->embd_q6k; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = (int)(E / 256);
+        k.x = e->xq8k; k.x_col_stride = ld; k.y = p.LG; k.y_col_stride = c.n_vocab; k.ncols = T;
+        if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
+    } else {
+        if (quant(QR_NORM, p.X, nullptr, E, e->out_norm)) return -1;
+        if (gemm(e->embd, EPI_STORE, nullptr, p.LG, c.n_vocab)) return -1;
+    }
     // greedy token from the last row; position T-1 -> T, token appended at hist[T]
     if (launch_row_argmax(p.LG + (size_t)(T - 1) * c.n_vocab, c.n_vocab, (unsigned long long *)p.keys, 256, s)) return -1;
     const int last = T - 1;

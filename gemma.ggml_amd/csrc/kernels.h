@@ -95,6 +95,14 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s);
 // ggml quantize_row_q8_K of ncols rows of K floats (row stride ldx floats) -> Q8_K rows ld_out bytes apart
 int launch_quant_q8_K(const float *x, int64_t ldx, int64_t K, int ncols, uint8_t *out, int64_t ld_out,
                       hipStream_t s);
+// rows of rms_norm(x)*w quantized to Q8_K (the tied output's INIT when token_embd is Q6_K)
+int launch_norm_q8K(const float *x, int64_t ldx, const float *w, int E, float eps, int rows, uint8_t *out,
+                    int64_t ld_out, hipStream_t s);
+// T rows of get_rows(Q6_K token_embd, tokens)*scale; token of row t: tokens[*pos] if pos else tokens[t]
+int launch_embed_q6K(const uint8_t *embd, int64_t row_bytes, const int *tokens, const int *pos, int T, int E,
+                     float scale, float *out, hipStream_t s);
+// synthetic Q4_K / Q6_K rows: oracle orc_synth_kquant(seed) with d (and dmin) rescaled by f
+int launch_synth_kquant(int wtype, uint8_t *out, int64_t rows, int64_t K, uint64_t seed, float f, hipStream_t s);
 
 // ---- prefill (prefill.hip) ----------------------------------------------------------------------
 enum qrow_mode { QR_F32 = 0, QR_NORM = 1, QR_EMBED_NORM = 2, QR_GELU = 3 };

@@ -180,11 +180,9 @@ namespace {
 // ggml quantize_row_q8_K (INIT for K-quant src0, restated in oracle/kquants_cpu.cpp): per 256
 // values the first element of largest |x| gives max; iscale = -127/max; q = min(127, rne(iscale*x));
 // bsums = sums of 16; d = 1/iscale (all-zero block: d = 0, q = 0).  One wave per super-block, 4
-// values per lane.  Divisions in double then rounded: equal to fp32 division for fp32 operands.
-__global__ void __launch_bounds__(64) k_quant_q8_K(const float *x, int64_t ldx, uint8_t *out, int64_t ld_out) {
-    const int sb = blockIdx.x, c = blockIdx.y, lane = threadIdx.x;
-    const float4 v = *(const float4 *)(x + (int64_t)c * ldx + (int64_t)sb * 256 + lane * 4);
-    const float xv[4] = {v.x, v.y, v.z, v.w};
+// values per lane (all 64 lanes take part).  Divisions in double then rounded: equal to fp32
+// division for fp32 operands.
+__device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *blk) {
     float amax = 0.0f, mx = 0.0f;
     int idx = 0x7fffffff;
 #pragma unroll
@@ -206,7 +204,6 @@ __global__ void __launch_bounds__(64) k_quant_q8_K(const float *x, int64_t ldx, 
             idx = oi;
         }
     }
-    uint8_t *blk = out + (int64_t)c * ld_out + (int64_t)sb * 292;
     int q[4] = {0, 0, 0, 0};
     float d = 0.0f;
     if (amax != 0.0f) {
@@ -224,6 +221,101 @@ __global__ void __launch_bounds__(64) k_quant_q8_K(const float *x, int64_t ldx, 
     if (lane == 0) *(float *)blk = d;
 }
 
+__global__ void __launch_bounds__(64) k_quant_q8_K(const float *x, int64_t ldx, uint8_t *out, int64_t ld_out) {
+    const int sb = blockIdx.x, c = blockIdx.y, lane = threadIdx.x;
+    const float4 v = *(const float4 *)(x + (int64_t)c * ldx + (int64_t)sb * 256 + lane * 4);
+    const float xv[4] = {v.x, v.y, v.z, v.w};
+    q8K_store(xv, lane, out + (int64_t)c * ld_out + (int64_t)sb * 292);
+}
+
+// rms_norm(x) * w (src/gemma_model.cpp:438-442; ggml: double sum of the fp32 squares, mean as
+// float, scale = 1/sqrtf(mean + eps), y = (x*scale)*w) then quantize_row_q8_K: the tied output's
+// INIT when token_embd is Q6_K.  One workgroup per row, one wave per super-block (E <= 4096).
+__global__ void __launch_bounds__(1024) k_norm_q8K(const float *x, int64_t ldx, const float *w, int E, float eps,
+                                                   uint8_t *out, int64_t ld_out) {
+    __shared__ double red[1024];
+    const int r = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const float4 v = *(const float4 *)(x + (int64_t)r * ldx + tid * 4);
+    const float xv[4] = {v.x, v.y, v.z, v.w};
+    double part = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part += (double)(xv[j] * xv[j]);
+    red[tid] = part;
+    __syncthreads();
+    int n = nt;
+    while (n > 1) {  // pairwise tree over any thread count
+        const int h = (n + 1) >> 1;
+        if (tid + h < n) red[tid] += red[tid + h];
+        __syncthreads();
+        n = h;
+    }
+    const float mean = (float)(red[0] / (double)E);
+    const float scale = 1.0f / sqrtf(mean + eps);
+    const float4 wv = *(const float4 *)(w + tid * 4);
+    const float ww[4] = {wv.x, wv.y, wv.z, wv.w};
+    float y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = pin(xv[j] * scale) * ww[j];
+    q8K_store(y, tid & 63, out + (int64_t)r * ld_out + (int64_t)(tid >> 6) * 292);
+}
+
+// ---- Q6_K token_embd / tied output (llama.cpp's choice for Q4_0 / Q8_0 Gemma files) -------------
+// dequantize_row_q6_K of element e of a row (y = d*sc*(q6 - 32), left to right)
+__device__ __forceinline__ float q6K_elem(const uint8_t *row, int64_t i) {
+    const uint8_t *blk = row + (i >> 8) * 210;
+    const int e = (int)(i & 255), n = e >> 7, g = (e >> 5) & 3, l = e & 31;
+    const uint8_t *ql = blk + n * 64, *qh = blk + 128 + n * 32;
+    const int lo = (g & 1) ? ql[l + 32] : ql[l];
+    const int q = (((g & 2) ? lo >> 4 : lo & 15) | (((qh[l] >> (2 * g)) & 3) << 4)) - 32;
+    const int8_t scv = ((const int8_t *)(blk + 192))[n * 8 + l / 16 + 2 * g];
+    return pin(h2f(*(const uint16_t *)(blk + 208)) * (float)scv) * (float)q;
+}
+
+// get_rows(token_embd, tokens) * sqrt(E) (src/gemma_model.cpp:677-679): row t reads token
+// tokens[*pos] (decode: the engine's device-side position) or tokens[t] (prefill)
+__global__ void k_embed_q6K(const uint8_t *embd, int64_t row_bytes, const int *tokens, const int *pos, int E,
+                            float scale, float *out) {
+    const int t = blockIdx.x;
+    const int tok = pos ? tokens[*pos] : tokens[t];
+    const uint8_t *row = embd + (int64_t)tok * row_bytes;
+    for (int i = threadIdx.x; i < E; i += blockDim.x) out[(int64_t)t * E + i] = q6K_elem(row, i) * scale;
+}
+
+// device twin of oracle orc_synth_kquant (splitmix64 stream: draw n of the matrix is mix(st0 +
+// (n + 1)·γ), block b's draws start at b·DRAWS) plus make_kmat's rescale d' = f16(f32(d)·f)
+__device__ __forceinline__ uint64_t sm64_draw(uint64_t st0, uint64_t n) {
+    uint64_t z = st0 + (n + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ float div1000(float a) { return (float)((double)a / 1000.0); }
+
+template <int WT>
+__global__ void k_synth_kquant(uint8_t *out, int64_t nblk, uint64_t st0, float f) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    uint64_t n = (uint64_t)b * (WT == T_Q4_K ? 142u : 209u);
+    if (WT == T_Q4_K) {
+        uint8_t *x = out + b * 144;
+        const uint32_t d = f2h(1e-3f + div1000(3e-3f * (float)(sm64_draw(st0, n++) % 1000)));
+        const uint32_t dm = f2h(div1000(2e-3f * (float)(sm64_draw(st0, n++) % 1000)));
+        for (int i = 0; i < 12; ++i) x[4 + i] = (uint8_t)sm64_draw(st0, n++);
+        for (int i = 0; i < 128; ++i) x[16 + i] = (uint8_t)sm64_draw(st0, n++);
+        const uint32_t d2 = f2h(pin(h2f(d) * f)), dm2 = f2h(pin(h2f(dm) * f));
+        x[0] = (uint8_t)d2; x[1] = (uint8_t)(d2 >> 8);
+        x[2] = (uint8_t)dm2; x[3] = (uint8_t)(dm2 >> 8);
+    } else {
+        uint8_t *x = out + b * 210;
+        for (int i = 0; i < 128; ++i) x[i] = (uint8_t)sm64_draw(st0, n++);
+        for (int i = 0; i < 64; ++i) x[128 + i] = (uint8_t)sm64_draw(st0, n++);
+        for (int i = 0; i < 16; ++i) x[192 + i] = (uint8_t)(int8_t)((int)(int8_t)(uint8_t)(sm64_draw(st0, n++) % 255) - 127);
+        const uint32_t d = f2h(2e-4f + div1000(6e-4f * (float)(sm64_draw(st0, n++) % 1000)));
+        const uint32_t d2 = f2h(pin(h2f(d) * f));
+        x[208] = (uint8_t)d2; x[209] = (uint8_t)(d2 >> 8);
+    }
+}
+
 }  // namespace
 
 int launch_quant_q8_K(const float *x, int64_t ldx, int64_t K, int ncols, uint8_t *out, int64_t ld_out,
@@ -233,6 +325,42 @@ int launch_quant_q8_K(const float *x, int64_t ldx, int64_t K, int ncols, uint8_t
         return -1;
     }
     hipLaunchKernelGGL(k_quant_q8_K, dim3((unsigned)(K / 256), (unsigned)ncols), dim3(64), 0, s, x, ldx, out, ld_out);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_norm_q8K(const float *x, int64_t ldx, const float *w, int E, float eps, int rows, uint8_t *out,
+                    int64_t ld_out, hipStream_t s) {
+    if (E % 256 || E > 4096 || rows <= 0 || ldx % 4 || ld_out % 4) {
+        set_error("norm_q8K: needs n_embd % 256 == 0 and n_embd <= 4096");
+        return -1;
+    }
+    hipLaunchKernelGGL(k_norm_q8K, dim3((unsigned)rows), dim3(E / 4), 0, s, x, ldx, w, E, eps, out, ld_out);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_embed_q6K(const uint8_t *embd, int64_t row_bytes, const int *tokens, const int *pos, int T, int E,
+                     float scale, float *out, hipStream_t s) {
+    if (E % 256 || T <= 0) {
+        set_error("embed_q6K: needs n_embd % 256 == 0");
+        return -1;
+    }
+    hipLaunchKernelGGL(k_embed_q6K, dim3((unsigned)T), dim3(256), 0, s, embd, row_bytes, tokens, pos, E, scale, out);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_synth_kquant(int wtype, uint8_t *out, int64_t rows, int64_t K, uint64_t seed, float f, hipStream_t s) {
+    if ((wtype != T_Q4_K && wtype != T_Q6_K) || K % 256) {
+        set_error("synth_kquant: Q4_K / Q6_K with K % 256 == 0");
+        return -1;
+    }
+    const int64_t nblk = rows * (K / 256);
+    const uint64_t st0 = seed * 0x2545F4914F6CDD1Dull + (uint64_t)wtype;  // orc_synth_kquant's state
+    const unsigned grid = (unsigned)((nblk + 255) / 256);
+    if (wtype == T_Q4_K) hipLaunchKernelGGL(k_synth_kquant<T_Q4_K>, dim3(grid), dim3(256), 0, s, out, nblk, st0, f);
+    else hipLaunchKernelGGL(k_synth_kquant<T_Q6_K>, dim3(grid), dim3(256), 0, s, out, nblk, st0, f);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -29,7 +29,8 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
            "gguf_get_val_data", "gguf_get_n_tensors", "gguf_get_tensor_name", "gguf_get_tensor_type",
            "gguf_get_tensor_offset", "gguf_get_version", "gguf_get_alignment", "gguf_get_data_offset",
-           "gguf_find_key", "gguf_find_tensor", "ggml_get_tensor", "ggml_nbytes"]
+           "gguf_find_key", "gguf_find_tensor", "ggml_get_tensor", "ggml_nbytes",
+           "gemma_engine_create_from_gguf", "gemma_engine_config"]
 
 
 def build():
@@ -40,7 +41,7 @@ class GemmaConfig(C.Structure):
     _fields_ = [("n_layer", C.c_int), ("n_embd", C.c_int), ("n_head", C.c_int), ("n_head_kv", C.c_int),
                 ("head_dim", C.c_int), ("n_ff", C.c_int), ("n_vocab", C.c_int), ("n_ctx", C.c_int),
                 ("wtype", C.c_int), ("eps", C.c_float), ("rope_base", C.c_float), ("seed", C.c_uint64),
-                ("gelu_clamp", C.c_int)]
+                ("gelu_clamp", C.c_int), ("out_type", C.c_int)]
 
 
 class GgmlTensor(C.Structure):
@@ -117,6 +118,10 @@ def lib():
     L.gemma_hbm_read_gbs.argtypes = [C.c_int, C.c_size_t, C.c_int]
     L.gemma_engine_sync.restype = C.c_int
     L.gemma_engine_sync.argtypes = [vp]
+    L.gemma_engine_create_from_gguf.restype = vp
+    L.gemma_engine_create_from_gguf.argtypes = [C.c_char_p, C.c_int, C.c_int]
+    L.gemma_engine_config.restype = C.c_int
+    L.gemma_engine_config.argtypes = [vp, C.POINTER(GemmaConfig)]
     # GGUF reader (include/ggml.h)
     L.gguf_init_from_file.restype = vp
     L.gguf_init_from_file.argtypes = [C.c_char_p, GGUFInitParams]
@@ -185,11 +190,11 @@ def mul_mat(src0_bytes, src0_type, ne01, nb01, shared_edge, wdata, row_size, nco
 
 class Engine:
     def __init__(self, shape, n_ctx=512, wtype=GGML_TYPE_Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0,
-                 gelu_clamp=0, device=0, tp=None):
+                 gelu_clamp=0, device=0, tp=None, out_type=0):
         """tp = (n_ranks, rank, rccl_id_bytes) for the row-split engine (one process per GPU);
         rccl_id_bytes None = all ranks' shards virtual in this engine (single-GPU parity mode)."""
         self.cfg = GemmaConfig(n_ctx=n_ctx, wtype=wtype, eps=eps, rope_base=rope_base, seed=seed,
-                               gelu_clamp=gelu_clamp, **shape)
+                               gelu_clamp=gelu_clamp, out_type=out_type, **shape)
         self.L = lib()
         if tp is not None and tp[0] > 1:
             idbuf = C.create_string_buffer(bytes(tp[2]), len(tp[2])) if tp[2] is not None else None
@@ -198,6 +203,18 @@ class Engine:
             self.h = self.L.gemma_engine_create(C.byref(self.cfg), device)
         if not self.h:
             raise RuntimeError("gemma_engine_create failed: " + last_error())
+
+    @classmethod
+    def from_gguf(cls, path, n_ctx=512, device=0):
+        """An engine on a Gemma GGUF file's weights (gemma_engine_create_from_gguf)."""
+        self = cls.__new__(cls)
+        self.L = lib()
+        self.h = self.L.gemma_engine_create_from_gguf(path.encode(), n_ctx, device)
+        if not self.h:
+            raise RuntimeError("gemma_engine_create_from_gguf failed: " + last_error())
+        self.cfg = GemmaConfig()
+        self.L.gemma_engine_config(self.h, C.byref(self.cfg))
+        return self
 
     def close(self):
         if self.h:

@@ -51,15 +51,21 @@ int hpc_graph_compute(struct ggml_cgraph *graph);
 /* ---- device-resident Gemma engine (performance path: the Gemma graph encoded as one hipGraph) ---- */
 typedef struct gemma_hip_config {
     int n_layer, n_embd, n_head, n_head_kv, head_dim, n_ff, n_vocab, n_ctx;
-    int wtype; /* GGML_TYPE_Q4_0 or GGML_TYPE_Q8_0 (all matrices, incl. token_embd/output) */
+    int wtype; /* GGML_TYPE_Q4_0 or GGML_TYPE_Q8_0 (the layer matrices) */
     float eps, rope_base;
     uint64_t seed;
     int gelu_clamp;
+    int out_type; /* token_embd / tied output: 0 = wtype, or GGML_TYPE_Q6_K (llama.cpp's Q4_0 / Q8_0 files) */
 } gemma_hip_config;
 
 typedef struct gemma_engine gemma_engine;
 
 gemma_engine *gemma_engine_create(const gemma_hip_config *cfg, int device);
+/* real weights from a Gemma GGUF file (src/gemma_model.cpp:19-229 loads the same tensors and keys):
+ * layer matrices all Q4_0 or all Q8_0, token_embd that type or Q6_K (llama.cpp's layout); NULL with
+ * hpc_last_error on anything else.  gemma_engine_config returns the configuration read. */
+gemma_engine *gemma_engine_create_from_gguf(const char *path, int n_ctx, int device);
+int gemma_engine_config(const gemma_engine *e, gemma_hip_config *out);
 /* row-split tensor parallelism: one process per GPU; rank r holds rows
  * [r*rows/n, (r+1)*rows/n) of every matrix and RCCL all-gathers complete each activation vector
  * (4 per layer + one argmax key per rank), so logits are bit-identical to one GPU.

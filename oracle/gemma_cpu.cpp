@@ -147,7 +147,7 @@ extern "C" orc_model *orc_model_create(const orc_config *cfg) {
     m->cfg = *cfg;
     const orc_config &c = *cfg;
     const int qw = c.n_head * c.head_dim, kvw = c.n_head_kv * c.head_dim;
-    if (c.kmix && (c.n_embd % 256 || c.n_ff % 256 || qw % 256)) {
+    if ((c.kmix == 1 && (c.n_embd % 256 || c.n_ff % 256 || qw % 256)) || (c.kmix == 2 && c.n_embd % 256)) {
         delete m;
         return nullptr;
     }
@@ -163,7 +163,7 @@ extern "C" orc_model *orc_model_create(const orc_config *cfg) {
         // is not dominated by the current token (DESIGN.md §Synthetic weights)
         const double se = 1.0 / sqrt((double)c.n_embd), sq = 1.0 / sqrt((double)qw), sf = 1.0 / sqrt((double)c.n_ff);
         auto mat = [&](int k, int64_t rows, int64_t cols, int ktype, double stdv) {
-            return c.kmix ? make_kmat(c.seed, tid_layer(il, k), rows, cols, ktype, stdv)
+            return c.kmix == 1 ? make_kmat(c.seed, tid_layer(il, k), rows, cols, ktype, stdv)
                           : make_qmat(c.seed, tid_layer(il, k), rows, cols, c.wtype, stdv);
         };
         L.q = mat(L_Q, qw, c.n_embd, ORC_Q4_K, se);

@@ -159,3 +159,32 @@ def test_length_bombs_are_rejected_before_allocating(tmp_path):
     _expect_error(p, "longer than the file")
     open(p, "wb").write(head + struct.pack("<Q", 1) + b"k" + struct.pack("<IIQ", ARR, STR, 2 ** 60))
     _expect_error(p, "longer than the file")
+
+
+def _model_file(tmp_path, kmix, wtype=2, drop=None):
+    import oracle_ctypes as O
+    from test_gpu_ggml_graph import write_gguf
+    shape = dict(n_layer=1, n_embd=256, n_head=2, n_head_kv=1, head_dim=128, n_ff=512, n_vocab=512)
+    m = O.Model(O.make_config(shape, n_ctx=64, wtype=wtype, kmix=kmix))
+    p = str(tmp_path / "m.gguf")
+    write_gguf(m, shape, p, kmix)
+    m.close()
+    return p
+
+
+def test_engine_from_gguf_rejects_unsupported_layouts(tmp_path):
+    """The engine's GGUF loader validates before touching the GPU (runs on the CPU)."""
+    import ctypes as C
+    L = G.lib()
+    p = _model_file(tmp_path, kmix=1)  # Q4_K / Q6_K layer matrices: the ggml-API path, not the engine
+    assert not L.gemma_engine_create_from_gguf(p.encode(), 64, 0)
+    assert "Q4_0 or all Q8_0" in G.last_error()
+    bad = str(tmp_path / "bad.gguf")
+    w = GGUFWriter()
+    w.add("gemma.block_count", U32, 1)
+    w.write(bad)
+    assert not L.gemma_engine_create_from_gguf(bad.encode(), 64, 0)
+    assert "missing u32 key gemma.embedding_length" in G.last_error()
+    assert not L.gemma_engine_create_from_gguf(str(tmp_path / "none.gguf").encode(), 64, 0)
+    assert "cannot open" in G.last_error()
+    del C

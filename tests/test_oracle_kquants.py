@@ -187,3 +187,16 @@ def test_kmix_model_avx2_equals_ordered_and_prefill_equals_decode():
 def test_kmix_rejects_unaligned_shapes():
     with pytest.raises(ValueError):
         O.Model(O.make_config(dict(KMIX, n_embd=384), n_ctx=64, kmix=1))
+
+
+def test_q6_K_output_layout_model_runs_and_is_consistent():
+    """kmix = 2: llama.cpp's Q4_0 file layout (Q4_0 layers, Q6_K token_embd / output)."""
+    shape = dict(KMIX, n_ff=384)
+    m = O.Model(O.make_config(shape, n_ctx=64, kmix=2))
+    prompt = O.make_prompt(6, shape["n_vocab"])
+    seq, logits = m.generate(prompt, 3, avx2=True)
+    seq_o, logits_o = m.generate(prompt, 3, avx2=False)
+    assert seq == seq_o and np.array_equal(logits, logits_o) and np.all(np.isfinite(logits))
+    assert len(m.tensor(16 + 1)) == 256 * shape["n_embd"] // 32 * 18   # a Q4_0 layer matrix
+    assert len(m.tensor(0)) == shape["n_vocab"] * shape["n_embd"] // 256 * 210  # Q6_K token_embd
+    m.close()
