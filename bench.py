@@ -193,6 +193,28 @@ def main():
         except Exception as ex:  # reported, never fatal to the headline line
             q8 = {"error": str(ex)[:300]}
 
+    # llama.cpp's Q4_0 file layout: the same decode with a Q6_K token_embd / tied output
+    # (1,544,847,360 weight bytes per token; logits through Q8_K INIT + the K-quant matvec)
+    q6o = None
+    if args.wtype == "q4_0" and args.q8_steps > 0:
+        try:
+            ke = G.Engine(GEMMA_2B, n_ctx=args.ctx, wtype=G.GGML_TYPE_Q4_0, device=local_rank,
+                          out_type=G.GGML_TYPE_Q6_K)
+            kplan = ke.tune(6) if not args.no_tune else ke.plan()
+            ke.begin(prompt)
+            ke.step(args.prompt + args.warmup, use_graph=True)
+            ke.L.gemma_engine_sync(ke.h)
+            t0 = time.perf_counter()
+            ke.step(args.q8_steps, use_graph=True)
+            ke.L.gemma_engine_sync(ke.h)
+            kdt = time.perf_counter() - t0
+            ke.close()
+            q6o = {"model": "Gemma-2B Q4_0 layers + Q6_K token_embd/output (llama.cpp layout)",
+                   "tok_s": round(args.q8_steps / kdt, 2), "ms_per_token": round(kdt / args.q8_steps * 1e3, 4),
+                   "steps": args.q8_steps, "token_weight_bytes": 1544847360, "launch_plan": kplan}
+        except Exception as ex:  # reported, never fatal to the headline line
+            q6o = {"error": str(ex)[:300]}
+
     # prefill leg (BASELINE config 3): batched prefill of a 2048-token synthetic prompt, logits for
     # every row as the reference computes them.  "exact": bit-identical to the CPU path (the
     # headline prefill_tok_s); "fast": int8/f16 MFMA, fp32 summation order differs
@@ -271,6 +293,7 @@ def main():
             "prefill": prefill,
             "kquant_matvec": kquant,
             "q8_0_decode": q8,
+            "q4_0_q6k_output_decode": q6o,
             "tp_decode": tp,
             "launch_plan": {k: ({"k_split": v[0], "rows_per_wg": v[1], "image": v[2]} if isinstance(v, tuple) else
                                 ("split" if v else "per_head")) for k, v in plan.items()},
