@@ -15,6 +15,13 @@
 namespace ghip {
 
 // ggml type ids (GGUF numbering)
+// diagnostic phase stamps (s_memrealtime per workgroup into mv_args/attn_args::dbg_t): compiled
+// out of the product build (the checks and stores cost ~5 % of a decode token); the stamp tools use
+// a variant built with -DGHIP_STAMPS=1 (scripts/build_variant.sh stamps ...)
+#ifndef GHIP_STAMPS
+#define GHIP_STAMPS 0
+#endif
+
 enum : int { T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q8_0 = 8, T_Q4_K = 12, T_Q6_K = 14, T_Q8_K = 15 };
 
 // ggml on-disk/host block formats

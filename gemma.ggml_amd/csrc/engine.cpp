@@ -1331,6 +1331,10 @@ extern "C" int gemma_engine_prefill_fast(gemma_engine *e, float *logits_last, fl
 // out: 6 * 4096 * 16 u64; unused slots are 0.
 extern "C" int gemma_engine_stamp_step(gemma_engine *e, int layer, unsigned long long *out) {
     set_error("");
+    if (!GHIP_STAMPS) {
+        set_error("gemma_engine_stamp_step: library built without -DGHIP_STAMPS=1 (scripts/build_variant.sh)");
+        return -1;
+    }
     (void)hipSetDevice(e->device);
     const size_t n = 6 * kStampRegion;
     GHIP_CHECK(hipMalloc(&e->stamp, n * 8));

@@ -51,6 +51,9 @@ struct mv_args {
     int ncols = 1;
     int ablate = 0;  // timing-only ablations (bench): 1 = no prologue, 4 = no carry
     unsigned long long *dbg_t = nullptr;  // diagnostics: 8 s_memrealtime stamps per workgroup
+    // launch geometry precomputed by launch_t (no 64-bit divisions in the kernel prologue):
+    // a wave's row-tile count is rt_q + (rt0 < rt_r); ygroups = EPI_GELU_MUL image groups per WG
+    int64_t rt_q = 0, rt_r = 0, ygroups = 0;
 };
 
 // ks: waves that split one row tile's K range (ordered carry hand-off); 1 = one wave per tile.

@@ -161,11 +161,14 @@ __device__ __forceinline__ const uint4 *img_item(const mv_args &a, int64_t i) {
     return i < n_act ? (const uint4 *)a.x + i : (const uint4 *)a.x_da + (i - n_act);
 }
 
-template <int WT, int PRO, int R>
+// NTH: the launch's thread count as a constant.  blockDim.x would be read from the implicit kernel
+// arguments with a global load the prologue then waits for (one HBM round trip, ~1 us, before the
+// first weight load could issue).
+template <int WT, int PRO, int R, int NTH>
 __device__ __forceinline__ void prefetch_activation(const mv_args &a, int col, act_regs<R> &r) {
     if (PRO == PRO_IMG) {
         const int64_t T = a.nb * 2 + a.nb / 4;
-        const int tid = threadIdx.x, nth = blockDim.x;
+        const int tid = threadIdx.x, nth = NTH;
 #pragma unroll
         for (int i = 0; i < 2 * R; ++i) {
             int64_t it = tid + (int64_t)i * nth;
@@ -178,7 +181,7 @@ __device__ __forceinline__ void prefetch_activation(const mv_args &a, int col, a
         return;
     }
     if (PRO != PRO_F32 && PRO != PRO_NORM) return;
-    const int tid = threadIdx.x, q = tid & 3, nquads = blockDim.x >> 2;
+    const int tid = threadIdx.x, q = tid & 3, nquads = NTH >> 2;
     const float *x = (const float *)((const uint8_t *)a.x + (int64_t)col * a.x_col_stride);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -194,11 +197,11 @@ __device__ __forceinline__ void prefetch_activation(const mv_args &a, int col, a
     }
 }
 
-template <int WT, int PRO, int R, bool NSA>
+template <int WT, int PRO, int R, bool NSA, int NTH>
 __device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const lds_map &m, const act_regs<R> &r) {
     constexpr int BT = wfmt<WT>::BT;
     constexpr bool CACHED = PRO == PRO_F32 || PRO == PRO_NORM;
-    const int tid = threadIdx.x, nth = blockDim.x;
+    const int tid = threadIdx.x, nth = NTH;
     const int64_t nb = a.nb, nb_pad = a.n_bt * BT;
     const int q = tid & 3;
     const int nquads = nth >> 2;
@@ -691,6 +694,9 @@ __device__ __forceinline__ float carry_chain(const void *st_s, const float *st_d
     return carry_run<2, false>(ps, pd, total, acc);
 }
 
+#ifndef GHIP_HOSTDIV
+#define GHIP_HOSTDIV 1  // 1: the wave's item count from launch_t's precomputed quotient (no 64-bit division)
+#endif
 #ifndef GHIP_UPRE
 #define GHIP_UPRE 4
 #endif
@@ -702,34 +708,36 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     constexpr int NM = EPI == EPI_GELU_MUL ? 2 : 1;  // matrices per row tile (gate, up)
     // readfirstlane: makes the wave index (and every cursor derived from it) provably uniform, so
     // the stream bookkeeping lives in SGPRs and its branches are scalar (cdna_hip_programming T20)
+    constexpr int NTH = KS > 1 ? 64 * KS : 256;  // launch_t's block size
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int rr = lane >> 3, l = lane & 7;
     const int col = blockIdx.y;
-    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 0] = __builtin_amdgcn_s_memrealtime();
+    if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 0] = __builtin_amdgcn_s_memrealtime();
     const int64_t seg_tiles = KS > 1 ? a.n_bt / KS : a.n_bt;
     // EPI_GELU_MUL with an image output: row-tile groups (4 consecutive tiles = one Q8_0 block of y)
     // this workgroup produces, buffered in LDS until the end
     const bool yimg = EPI == EPI_GELU_MUL && KS == 1 && a.out_act != nullptr;
-    const int64_t ygroups = yimg ? ((a.n_rt >> 2) + gridDim.x - 1) / gridDim.x : 0;
+    const int64_t ygroups = !yimg ? 0 : GHIP_HOSTDIV ? a.ygroups : ((a.n_rt >> 2) + gridDim.x - 1) / gridDim.x;
     const lds_map m = make_lds_map<WT, NSA>(KS, a.n_bt, seg_tiles, ygroups);
     const int nbt = (int)seg_tiles;
     const int bt0 = KS > 1 ? wave * nbt : 0;
     // this wave's row tiles
     int64_t rt0, rstride;
     if (KS == 1) {
-        const int nw = blockDim.x >> 6;
+        constexpr int nw = NTH >> 6;
         rt0 = (int64_t)blockIdx.x * nw + wave;
         rstride = (int64_t)gridDim.x * nw;
     } else {
         rt0 = blockIdx.x;
         rstride = gridDim.x;
     }
-    const int64_t n_my_rt = rt0 < a.n_rt ? (a.n_rt - rt0 + rstride - 1) / rstride : 0;
+    const int64_t n_my_rt = GHIP_HOSTDIV ? a.rt_q + (rt0 < a.rt_r ? 1 : 0)
+                                         : rt0 < a.n_rt ? (a.n_rt - rt0 + rstride - 1) / rstride : 0;
     const int64_t n_items = n_my_rt * NM * nbt;
 
     // 0) this thread's activation values (older than the weight loads -> waited for by count)
     act_regs<R> ar;
-    prefetch_activation<WT, PRO, R>(a, col, ar);
+    prefetch_activation<WT, PRO, R, NTH>(a, col, ar);
 
     // 1) fill the register ring: the HBM round trip overlaps the prologue below.  Loads are
     //    never inside a runtime branch (hipcc would wait vmcnt(0) around them): past the last item
@@ -777,15 +785,15 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     constexpr int UP = GHIP_UPRE < U ? GHIP_UPRE : U;
 #pragma unroll
     for (int u = 0; u < UP; ++u) issue(qb[u], sb[u]);
-    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 1] = __builtin_amdgcn_s_memrealtime();
+    if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 1] = __builtin_amdgcn_s_memrealtime();
 
     // 2) activation image in LDS
-    if (!(a.ablate & 1)) build_activation<WT, PRO, R, NSA>(a, col, smem, m, ar);
+    if (!(a.ablate & 1)) build_activation<WT, PRO, R, NSA, NTH>(a, col, smem, m, ar);
 #pragma unroll
     for (int u = UP; u < U; ++u) issue(qb[u], sb[u]);
-    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 2] = __builtin_amdgcn_s_memrealtime();
+    if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 2] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
-    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 3] = __builtin_amdgcn_s_memrealtime();
+    if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 3] = __builtin_amdgcn_s_memrealtime();
 
     // 3) stream
     const int seg_blocks = nbt * BT;
@@ -865,9 +873,9 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
                         // (7.5 clk/step): tests/micro/carry_bench*.hip.
                         float *hand = (float *)(smem + m.red);
                         if (wave == 0) hand[lane] = acc;
-                        if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 6] = __builtin_amdgcn_s_memrealtime();
+                        if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 6] = __builtin_amdgcn_s_memrealtime();
                         __syncthreads();
-                        if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 7] = __builtin_amdgcn_s_memrealtime();
+                        if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 7] = __builtin_amdgcn_s_memrealtime();
                         {
                             // one carrier wave: a wave pays ~16-21 clk per ds_read_b128 whatever its
                             // active lanes, so more carriers only add LDS-array contention
@@ -876,15 +884,15 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
                             if (wave < NCAR && lane < RPW * 8) {
                                 float c = hand[gl];
                                 if (!(a.ablate & 4)) c = carry_chain<WT, KS>(st_s, st_d, m, seg_blocks, gl, c);
-                                if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 8] = __builtin_amdgcn_s_memrealtime();
+                                if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 8] = __builtin_amdgcn_s_memrealtime();
                                 const float v = fold8(c);
                                 if ((lane & 7) == 0) epilogue<EPI>(a, col, cc.rt * 8 + (gl >> 3), v, 0.0f, best);
-                                if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 9] = __builtin_amdgcn_s_memrealtime();
+                                if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 9] = __builtin_amdgcn_s_memrealtime();
                             }
                         }
                         acc = 0.0f;
                         __syncthreads();
-                        if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 10] = __builtin_amdgcn_s_memrealtime();
+                        if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 10] = __builtin_amdgcn_s_memrealtime();
                     }
                 }
                 if (++cc.bt == nbt) {
@@ -897,13 +905,13 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
             }
         }
     }
-    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 4] = __builtin_amdgcn_s_memrealtime();
+    if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 4] = __builtin_amdgcn_s_memrealtime();
     if (EPI == EPI_GELU_MUL && yimg) {
         // y's Q8_0 image: group g = blockIdx.x + k*gridDim.x of 4 row tiles is block g of y
         __syncthreads();
         const int64_t n_groups = a.n_rt >> 2;
         const int64_t mine = blockIdx.x < n_groups ? (n_groups - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
-        for (int64_t t = tid; t < mine * 4; t += blockDim.x) {
+        for (int64_t t = tid; t < mine * 4; t += NTH) {
             const int64_t k = t >> 2;
             const float *yv = (const float *)(smem + m.ybuf) + k * 32 + (t & 3) * 8;
             float v[8];
@@ -925,11 +933,11 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
         if (lane == 0) red[wave] = best;
         __syncthreads();
         if (tid == 0) {
-            for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
+            for (int w = 1; w < NTH / 64; ++w) best = red[w] > best ? red[w] : best;
             a.argmax_key[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = best;
         }
     }
-    if (a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 5] = __builtin_amdgcn_s_memrealtime();
+    if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 5] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <int WT, int KS, int PRO, int EPI>
@@ -945,8 +953,9 @@ int launch_t(const mv_args &a, int grid_x, hipStream_t s) {
         set_error("matvec: PRO_IMG needs K % 128 == 0");
         return -1;
     }
-    const lds_map m = make_lds_map<WT, NSA>(KS, a.n_bt, seg, yimg ? ((a.n_rt >> 2) + grid_x - 1) / grid_x : 0);
-    const int threads = KS > 1 ? 64 * KS : 256;
+    const int64_t ygroups = yimg ? ((a.n_rt >> 2) + grid_x - 1) / grid_x : 0;
+    const lds_map m = make_lds_map<WT, NSA>(KS, a.n_bt, seg, ygroups);
+    const int threads = KS > 1 ? 64 * KS : 256;  // = k_matvec's NTH
     if (KS > 1 && a.n_bt % KS != 0) {
         set_error("matvec: n_bt not divisible by KS");
         return -1;
@@ -961,13 +970,18 @@ int launch_t(const mv_args &a, int grid_x, hipStream_t s) {
     // one-shot when every wave owns at most one row tile of at most U items
     const int64_t waves_x = (int64_t)grid_x * (KS > 1 ? 1 : threads / 64);
     const bool one_shot = KS > 1 && seg <= U && waves_x >= a.n_rt;
+    mv_args la = a;  // + the launch geometry (see mv_args::rt_q)
+    const int64_t rstride = KS > 1 ? grid_x : (int64_t)grid_x * (threads / 64);
+    la.rt_q = a.n_rt / rstride;
+    la.rt_r = a.n_rt % rstride;
+    la.ygroups = ygroups;
     const void *fn = one_shot ? (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1>
                               : (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>;
     if (m.total > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m.total));
     if (one_shot)
-        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, a);
+        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, la);
     else
-        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, a);
+        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, la);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -308,7 +308,7 @@ __device__ __forceinline__ int ld_sc1_i(const int *p) {
 
 #define ATT_STAMP(i)                                                                                        \
     do {                                                                                                    \
-        if (a.dbg_t && tid == 0) a.dbg_t[(int64_t)(kvh * a.nwg + wg) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[(int64_t)(kvh * a.nwg + wg) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
 // One token's attention for the G = H/Hkv query heads of kv head kvh = blockIdx.x / nwg, split over
@@ -620,7 +620,7 @@ constexpr int AH_VPF = GHIP_AH_PF;  // V steps (of 32 positions) prefetched per 
 
 #define AH_STAMP(i)                                                                                         \
     do {                                                                                                    \
-        if (a.dbg_t && tid == 0) a.dbg_t[(int64_t)(blockIdx.x >> 3) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[(int64_t)(blockIdx.x >> 3) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
 // One token's attention for query head h, one 1024-thread workgroup per head (SURVEY A.4/A.6 order,
@@ -932,7 +932,7 @@ __global__ void __launch_bounds__(256) k_reduce_keys(const unsigned long long *k
                                                      unsigned long long *out) {
     __shared__ unsigned long long red[4];
     unsigned long long best = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) best = keys[i] > best ? keys[i] : best;
+    for (int i = threadIdx.x; i < n; i += 256) best = keys[i] > best ? keys[i] : best;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         const unsigned long long o = __shfl_xor(best, off);
@@ -941,7 +941,7 @@ __global__ void __launch_bounds__(256) k_reduce_keys(const unsigned long long *k
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
     __syncthreads();
     if (threadIdx.x != 0) return;
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
+    for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
     const uint32_t local = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull);
     *out = (best & 0xFFFFFFFF00000000ull) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)(local + row_base));
 }
@@ -951,7 +951,7 @@ __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys,
     __shared__ unsigned long long red[4];
     __shared__ int sp;
     unsigned long long best = 0;
-    for (int i = threadIdx.x; i < n_parts; i += blockDim.x) best = keys[i] > best ? keys[i] : best;
+    for (int i = threadIdx.x; i < n_parts; i += 256) best = keys[i] > best ? keys[i] : best;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         const unsigned long long o = __shfl_xor(best, off);
@@ -960,7 +960,7 @@ __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys,
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = red[w] > best ? red[w] : best;
+        for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
         // strict '>' argmax, first max wins (src/gemma_model.cpp:538-543): the key's low word is ~index
         const int idx = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
         const int p = *pos + 1;
@@ -972,7 +972,7 @@ __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys,
     __syncthreads();
     // the RoPE row of the next position, at a fixed address (attention loads it without *pos)
     if (r.cur && sp < r.ctx) {
-        for (int i = threadIdx.x; i < r.half; i += blockDim.x) {
+        for (int i = threadIdx.x; i < r.half; i += 256) {
             r.cur[i] = r.cos[(int64_t)sp * r.half + i];
             r.cur[r.half + i] = r.sin[(int64_t)sp * r.half + i];
         }
