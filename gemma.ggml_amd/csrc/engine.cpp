@@ -232,7 +232,7 @@ static bool att_img_ok(const gemma_engine *e) { return e->att_mode == ATTN_PER_H
 // KS > 1 workgroup its KS waves on one row tile; each workgroup repeats for rpw row-tile groups
 static int mv_grid(const gemma_engine *e, int cls, int64_t n_rt) {
     const launch_plan &p = e->plan[cls];
-    const int64_t per = (p.ks == 1 ? 4 : 1) * (int64_t)std::max(p.rpw, 1);
+    const int64_t per = (p.ks == 1 || cls == MC_GU ? 4 : 1) * (int64_t)std::max(p.rpw, 1);  // gate/up ks 2: 4 row tiles
     int64_t g = (n_rt + per - 1) / per;
     if (cls == MC_LOGITS || cls == MC_GU) g = std::min<int64_t>(g, e->grid_big);  // key slots
     return (int)std::max<int64_t>(g, 1);
@@ -357,7 +357,7 @@ static int enqueue_step(gemma_engine *e) {
                 g.out_da = e->h_da + b0;
             }
             g.dbg_t = stamp_region(e, il, 3);
-            if (launch_matvec(wt, 1, PRO_NORM, EPI_GELU_MUL, g, mv_grid(e, MC_GU, L.gate.n_rt), s))
+            if (launch_matvec(wt, e->plan[MC_GU].ks, PRO_NORM, EPI_GELU_MUL, g, mv_grid(e, MC_GU, L.gate.n_rt), s))
                 return -1;
         }
         if (h_img) {
@@ -956,7 +956,7 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
             set_mat(L.gate);
             a.qs2 = L.up.qs; a.sc2 = L.up.sc;
             a.x = e->sa; a.norm_w = L.ffn_norm; a.eps = c.eps; a.y = e->h; a.gelu_tab = e->gelu_tab;
-            pro = PRO_NORM; epi = EPI_GELU_MUL;
+            pro = PRO_NORM; epi = EPI_GELU_MUL; ks = e->plan[MC_GU].ks;  // 2 = gate and up on separate waves
             grid = mv_grid(e, MC_GU, L.gate.n_rt);
             bytes = (double)L.gate.algo_bytes() + L.up.algo_bytes() + c.n_embd * 4.0 * 2 + c.n_ff * 4.0;
             break;
@@ -1094,8 +1094,8 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
         const int cls = order[oi];
         if (cls == MC_LOGITS && e->out_type == T_Q6_K) continue;  // the K-quant matvec has no plan
         std::vector<launch_plan> cands;
-        const bool splits = cls == MC_QKV || cls == MC_O || cls == MC_DOWN;
-        for (int ks = 1; ks <= (splits ? 8 : 1); ks *= 2) {
+        const bool splits = cls == MC_QKV || cls == MC_O || cls == MC_DOWN || cls == MC_GU;
+        for (int ks = 1; ks <= (cls == MC_GU ? 2 : splits ? 8 : 1); ks *= 2) {
             if (pick_ks(wt, nbt[cls], ks) != ks) continue;  // not a divisor, or the LDS image overflows
             const int rmax = cls == MC_LOGITS ? 16 : ks == 1 ? 2 : 4;
             for (int rpw = 1; rpw <= rmax; rpw *= 2) cands.push_back({ks, rpw, e->plan[cls].img});
@@ -1160,9 +1160,9 @@ extern "C" int gemma_engine_set_plan(gemma_engine *e, const int *in, int n) {
     const int64_t nbt[MC_N] = {L0.qkv.n_bt, L0.o.n_bt, L0.gate.n_bt, L0.down.n_bt, e->embd.n_bt};
     for (int cls = 0; cls < MC_N && 3 * cls + 2 < n; ++cls) {
         const int ks = in[3 * cls], rpw = in[3 * cls + 1], img = in[3 * cls + 2];
-        const bool splits = cls == MC_QKV || cls == MC_O || cls == MC_DOWN;
+        const bool splits = cls == MC_QKV || cls == MC_O || cls == MC_DOWN || cls == MC_GU;
         const bool img_ok = (cls == MC_O && e->att_act) || (cls == MC_DOWN && e->h_act);
-        if (ks < 1 || (!splits && ks != 1) || pick_ks(c.wtype, nbt[cls], ks) != ks || rpw < 1 || rpw > 64 ||
+        if (ks < 1 || (!splits && ks != 1) || (cls == MC_GU && ks > 2) || pick_ks(c.wtype, nbt[cls], ks) != ks || rpw < 1 || rpw > 64 ||
             (img && !img_ok)) {
             set_error("gemma_engine_set_plan: infeasible plan");
             return -1;

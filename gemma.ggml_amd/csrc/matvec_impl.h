@@ -940,6 +940,134 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 5] = __builtin_amdgcn_s_memrealtime();
 }
 
+// gate/up with the two matrices on separate waves (launch_matvec ks = 2, EPI_GELU_MUL): wave w of a
+// 512-thread workgroup streams matrix w & 1 (gate, up) of row tile 4*blockIdx.x + (w >> 1)
+// (+ k * 4*gridDim.x), each in its own ordered chain exactly as the paired form computes it.  Twice
+// the waves with half the items each: at Gemma-2B shapes the register ring holds a wave's whole row
+// tile (one-shot), so all of the launch's weight loads are in flight after the prologue.  The two
+// chains meet in LDS for gelu(gate)*up and the optional Q8_0 image of y.
+template <int WT, int U, bool ONE_SHOT>
+__global__ void __launch_bounds__(512) k_matvec_gu2(mv_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NTH = 512, SB = wfmt<WT>::SCALE_BYTES;
+    constexpr bool NSA = true;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rr = lane >> 3, l = lane & 7, mat = wave & 1, pair = wave >> 1;
+    const lds_map m = make_lds_map<WT, NSA>(1, a.n_bt, a.n_bt, 0);
+    float *vbuf = (float *)(smem + m.ybuf);  // [round][gate | up][32 rows of the 4 row tiles]
+    const int nbt = (int)a.n_bt;
+    const int64_t rt0 = (int64_t)blockIdx.x * 4 + pair, rstride = (int64_t)gridDim.x * 4;
+    const int64_t n_my_rt = a.rt_q + (rt0 < a.rt_r ? 1 : 0);
+    const int64_t n_items = n_my_rt * nbt;
+    act_regs<1> ar;
+    prefetch_activation<WT, PRO_NORM, 1, NTH>(a, 0, ar);
+    const uint8_t *qsm = mat ? a.qs2 : a.qs, *scm = mat ? a.sc2 : a.sc;
+    uint4 qb[U], sb[U];
+    int64_t rt_i = n_items ? rt0 : 0, issued = 0;
+    int bt_i = 0;
+    const uint32_t q_off = (uint32_t)lane * 16u, s_off = (uint32_t)rr * SB;
+    auto issue = [&](uint4 &qd, uint4 &sd) {  // past the last item the cursor stays (L2 re-read)
+        const int64_t tile = rt_i * a.n_bt + bt_i;
+        qd = ld_nt16(qsm + tile * 1024 + q_off);
+        if (WT == T_Q4_0) {
+            sd = ld_nt16(scm + tile * 8 * SB + s_off);
+        } else {
+            const uint2 v = ld_nt8(scm + tile * 8 * SB + s_off);
+            sd = make_uint4(v.x, v.y, 0, 0);
+        }
+        ++issued;
+        if (issued < n_items && ++bt_i == nbt) {
+            bt_i = 0;
+            rt_i += rstride;
+        }
+    };
+    constexpr int UP = GHIP_UPRE < U ? GHIP_UPRE : U;
+#pragma unroll
+    for (int u = 0; u < UP; ++u) issue(qb[u], sb[u]);
+    build_activation<WT, PRO_NORM, 1, NSA, NTH>(a, 0, smem, m, ar);
+#pragma unroll
+    for (int u = UP; u < U; ++u) issue(qb[u], sb[u]);
+    __syncthreads();
+    float acc = 0.0f;
+    int bt_c = 0, y_it = 0;
+    const int64_t n_pad = ONE_SHOT ? U : (n_items + U - 1) / U * U;
+    for (int64_t k = 0; k < n_pad; k += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint4 q = qb[u], sc = sb[u];
+            if (!ONE_SHOT) issue(qb[u], sb[u]);
+            if (k + u < n_items) {
+                const act_tile<WT> at = load_act<WT, NSA>(smem, m, bt_c, l);
+                acc = tile_dot_a<WT>(q, sc, at, acc);
+                if (++bt_c == nbt) {
+                    const float v = fold8(acc);
+                    acc = 0.0f;
+                    bt_c = 0;
+                    if (l == 0) vbuf[(y_it * 2 + mat) * 32 + pair * 8 + rr] = v;
+                    ++y_it;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // y = gelu(gate) * up for this workgroup's rows (round k: row tiles 4*blockIdx.x + k*rstride + 0..3)
+    const bool yimg = a.out_act != nullptr;
+    for (int64_t t = tid; (int64_t)blockIdx.x * 4 + (t >> 5) * rstride < a.n_rt; t += NTH) {
+        const int64_t k = t >> 5;
+        const int j = (int)(t & 31);
+        const int64_t rt = (int64_t)blockIdx.x * 4 + k * rstride + (j >> 3);
+        if (rt >= a.n_rt) continue;
+        const float yv = gelu_tab(a, vbuf[(k * 2) * 32 + j]) * vbuf[(k * 2 + 1) * 32 + j];
+        const int64_t row = rt * 8 + (j & 7);
+        if (row < a.rows) a.y[row] = yv;
+        if (yimg) vbuf[(k * 2) * 32 + j] = yv;  // the image reads y from the gate slot
+    }
+    if (yimg) {
+        __syncthreads();
+        // group g = blockIdx.x + k*gridDim.x of 4 row tiles is Q8_0 block g of y (n_rt % 4 == 0)
+        for (int64_t t = tid; (int64_t)blockIdx.x * 4 + (t >> 2) * rstride < a.n_rt; t += NTH) {
+            const int64_t k = t >> 2;
+            const float *yv = vbuf + (k * 2) * 32 + (t & 3) * 8;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = yv[j];
+            image_put_quad(a.out_act, nullptr, a.out_da, blockIdx.x + k * gridDim.x, (int)(t & 3), v);
+        }
+    }
+}
+
+template <int WT>
+int launch_gu2(const mv_args &a, int grid_x, hipStream_t s) {
+    constexpr int U = 8;
+    const bool yimg = a.out_act != nullptr;
+    if (a.ncols != 1) {
+        set_error("matvec: the split gate/up form is single-column");
+        return -1;
+    }
+    if (yimg && (a.n_rt % 4 || a.rows % 32)) {
+        set_error("matvec: the gelu image output needs whole 32-row blocks");
+        return -1;
+    }
+    mv_args la = a;
+    const int64_t rstride = (int64_t)grid_x * 4;
+    la.rt_q = a.n_rt / rstride;
+    la.rt_r = a.n_rt % rstride;
+    const int64_t rounds = la.rt_q + (la.rt_r ? 1 : 0);
+    const lds_map m = make_lds_map<WT, true>(1, a.n_bt, a.n_bt, 0);
+    const size_t lds = m.total + (size_t)rounds * 2 * 32 * 4;
+    if (lds > 160 * 1024) {
+        set_error("matvec: LDS image too large");
+        return -1;
+    }
+    const bool one_shot = rounds <= 1 && a.n_bt <= U;
+    const void *fn = one_shot ? (const void *)k_matvec_gu2<WT, U, true> : (const void *)k_matvec_gu2<WT, U, false>;
+    if (lds > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (one_shot) hipLaunchKernelGGL((k_matvec_gu2<WT, U, true>), dim3(grid_x), dim3(512), lds, s, la);
+    else hipLaunchKernelGGL((k_matvec_gu2<WT, U, false>), dim3(grid_x), dim3(512), lds, s, la);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 template <int WT, int KS, int PRO, int EPI>
 int launch_t(const mv_args &a, int grid_x, hipStream_t s) {
     constexpr bool NSA = KS != 8;  // 8-way split: recompute -8*sum(a) to leave LDS for the stash
@@ -996,6 +1124,7 @@ int dispatch_pro(int pro, int epi, const mv_args &a, int g, hipStream_t s) {
     if (pro == PRO_IMG && epi == EPI_ADD) return launch_t<WT, KS, PRO_IMG, EPI_ADD>(a, g, s);         // wo, wdown (image)
     if (KS == 1 && pro == PRO_NORM && epi == EPI_GELU_MUL)
         return launch_t<WT, 1, PRO_NORM, EPI_GELU_MUL>(a, g, s);                                      // gate/up
+    if (KS == 2 && pro == PRO_NORM && epi == EPI_GELU_MUL) return launch_gu2<WT>(a, g, s);            // gate/up, split
     if (KS == 1 && pro == PRO_NORM && epi == EPI_ARGMAX)
         return launch_t<WT, 1, PRO_NORM, EPI_ARGMAX>(a, g, s);                                        // logits
     if (pro == PRO_F32 && epi == EPI_STORE) return launch_t<WT, KS, PRO_F32, EPI_STORE>(a, g, s);

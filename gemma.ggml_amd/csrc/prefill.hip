@@ -288,6 +288,7 @@ __global__ void __launch_bounds__(256) k_gemm_q(gemm_args g) {
 // together and the weights leave HBM about once per XCD.
 typedef _Float16 xh8 __attribute__((ext_vector_type(8)));
 typedef float xf4 __attribute__((ext_vector_type(4)));
+typedef float xf16v __attribute__((ext_vector_type(16)));
 
 // four small integers (bytes of v, biased so they are in [0, 1024)) -> 2 dwords of f16 pairs
 // f16(1024 + u) has bits 0x6400 | u; subtracting the bias (1024 + b) in f16 is exact
@@ -326,12 +327,23 @@ static_assert(XN * XKB * 64 / 16 % XNT == 0, "token records");
 #ifndef GHIP_XWPE
 #define GHIP_XWPE 0
 #endif
-template <int WT, int EPI>
+#ifndef GHIP_X32
+#define GHIP_X32 1
+#endif
+// W32: the lane sums from v_mfma_f32_32x32x16_f16 instead (the default).  K = 16 covers half a
+// block, and only the four AVX2 lanes 4h..4h+3 have elements in half h, so MFMA row m = 4*row + i
+// (i = lane & 3 of half h) wastes 3/4 of each A row instead of 7/8: a wave's 8 rows x 32 tokens per
+// block take two 32x32x16 MFMAs (h = 0, 1) instead of eight 16x16x32 ones, and four 16-B LDS
+// fragment reads instead of six.  D row m = (reg & 3) + 8*(reg >> 2) + 4*(lane >> 5) puts the
+// four lanes of one (row, token) in consecutive registers and both halves in the same lane, so the
+// hsum needs no lane exchange.  Same operands, same products, same fmaf chains: bit-identical.
+template <int WT, int EPI, bool W32>
 __global__ void __launch_bounds__(XNT)
 #if GHIP_XWPE
 __attribute__((amdgpu_waves_per_eu(GHIP_XWPE, GHIP_XWPE)))
 #endif
 k_gemm_x(gemm_args g) {
+    static_assert(!W32 || (XRT == 4 && XCT == 2), "W32: waves of 8 rows x 32 tokens");
     // A fragments: [b][row][lane] 16 B (lane l's 4 f16 in half l&1 of the fragment)
     // + a zero region the inactive lanes read at the same strides (no per-lane select)
     __shared__ __attribute__((aligned(16))) uint4 Wf[XKB * XM * 8 + 7 * 16 + 1];
@@ -349,9 +361,14 @@ k_gemm_x(gemm_args g) {
     const int64_t n_rt = g.n_rt, n_bt = g.n_bt, nb = g.nb;
     // this lane's A fragment: MFMA row l16 = (weight row wr + 2*rt + (l16 >> 3), lane l16 & 7);
     // nonzero only when the lane's 4 elements fall in the lane's k range 8*kg .. 8*kg+7
-    const bool a_act = ((l16 & 7) >> 1) == kg;
-    const uint4 *a_ptr = a_act ? &Wf[(wr + (l16 >> 3)) * 8 + (l16 & 7)] : &Wf[XKB * XM * 8];
+    // W32: MFMA row (lane & 31) = 4 * row + (lane & 3); lane's k group 8*(lane >> 5) .. holds the
+    // elements of AVX2 lane 4h + (lane & 3) iff (lane >> 5) == (lane & 3) >> 1
+    const bool a_act = W32 ? (lane >> 5) == ((lane & 3) >> 1) : ((l16 & 7) >> 1) == kg;
+    const uint4 *a_ptr = !a_act ? &Wf[XKB * XM * 8]
+                         : W32  ? &Wf[(wr + ((lane & 31) >> 2)) * 8 + (lane & 3)]
+                                : &Wf[(wr + (l16 >> 3)) * 8 + (l16 & 7)];
     const int a_bstride = a_act ? XM * 8 : 0;
+    const int a_hoff = a_act ? 4 : 0;  // W32: the half-1 lanes' fragments (lane 4 + (lane & 3))
     for (int i = tid; i < 7 * 16 + 1; i += XNT) Wf[XKB * XM * 8 + i] = make_uint4(0u, 0u, 0u, 0u);
 
     float acc[XRT][XCT][4];
@@ -471,12 +488,54 @@ k_gemm_x(gemm_args g) {
             }
     };
 
+    // ---- W32 operands and block step ----
+    const int n32 = lane & 31, g32 = lane >> 5;
+    float acc32[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) acc32[j][l] = 0.0f;
+    struct frag32 { xh8 a[2]; xh8 b[2]; float dw[4]; float da; };
+    auto ldfrag32 = [&](int b, frag32 &f) {
+        const uint4 *ab = a_ptr + b * a_bstride;
+        f.a[0] = *(const xh8 *)ab;
+        f.a[1] = *(const xh8 *)(ab + a_hoff);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) f.b[h] = *(const xh8 *)(Xs + (wt + n32) * XS_ROW + b * 64 + h * 32 + g32 * 16);
+        f.da = das[b][wt + n32];
+        const float4 dwq = *(const float4 *)&dws[b][g32][wr / 2];
+        f.dw[0] = dwq.x; f.dw[1] = dwq.y; f.dw[2] = dwq.z; f.dw[3] = dwq.w;
+    };
+    auto block32 = [&](const frag32 &f) {
+        const xf16v z = {};
+        const xf16v d0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[0], f.b[0], z, 0, 0, 0);
+        const xf16v d1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[1], f.b[1], z, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float d = f.dw[j] * f.da;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                acc32[j][i] = __builtin_fmaf(d, d0[4 * j + i], acc32[j][i]);
+                acc32[j][4 + i] = __builtin_fmaf(d, d1[4 * j + i], acc32[j][4 + i]);
+            }
+        }
+    };
+
     gload(0);
     for (int64_t kb0 = 0; kb0 < nb; kb0 += XKB) {
         lstore();
         __syncthreads();
         if (kb0 + XKB < nb) gload(kb0 + XKB);
         const int nbs = (int)(nb - kb0 < XKB ? nb - kb0 : XKB);
+        if constexpr (W32) {
+            for (int b = 0; b < nbs; ++b) {
+                frag32 cur;
+                ldfrag32(b, cur);
+                block32(cur);
+            }
+            __syncthreads();
+            continue;
+        }
 #if GHIP_XPF
         frag cur;
         ldfrag(0, cur);
@@ -494,6 +553,19 @@ k_gemm_x(gemm_args g) {
         }
 #endif
         __syncthreads();
+    }
+    if constexpr (W32) {  // hsum in registers: ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7))
+        const int64_t t = t0 + wt + n32;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float *a = acc32[j];
+            float o = ((a[0] + a[4]) + (a[2] + a[6])) + ((a[1] + a[5]) + (a[3] + a[7]));
+            const int64_t r = r0 + wr + 2 * j + g32;
+            if (t >= g.T || r >= g.rows) continue;
+            if (EPI == EPI_ADD) o = o + g.resid[t * g.ldy + r];
+            g.y[t * g.ldy + r] = o;
+        }
+        return;
     }
     // hsum: lane kg even holds lanes 0-3 of (row, token), lane^16 lanes 4-7
 #pragma unroll
@@ -765,10 +837,11 @@ int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
         return -1;
     }
     const dim3 grid((unsigned)((g.T + XN - 1) / XN), (unsigned)gy);
-    if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_STORE>), grid, dim3(XNT), 0, s, g);
-    else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_ADD>), grid, dim3(XNT), 0, s, g);
-    else if (wtype == T_Q8_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_STORE>), grid, dim3(XNT), 0, s, g);
-    else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_ADD>), grid, dim3(XNT), 0, s, g);
+    constexpr bool W32 = GHIP_X32 != 0;
+    if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_STORE, W32>), grid, dim3(XNT), 0, s, g);
+    else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_ADD, W32>), grid, dim3(XNT), 0, s, g);
+    else if (wtype == T_Q8_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_STORE, W32>), grid, dim3(XNT), 0, s, g);
+    else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q8_0, EPI_ADD, W32>), grid, dim3(XNT), 0, s, g);
     else {
         set_error("gemm_exact: unsupported (type, epilogue)");
         return -1;

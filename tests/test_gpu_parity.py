@@ -262,3 +262,35 @@ def test_tuned_plan_bitexact():
         assert list(e.tokens()[: len(seq_ref)]) == list(seq_ref), p
         assert np.array_equal(lg[len(prompt) - 1:].view(np.uint32), lg_ref.view(np.uint32)), p
     e.close()
+
+
+def _check_decode_plan(shape, n_prompt, n_decode, n_ctx, wtype, plan_edit):
+    m = O.Model(O.make_config(shape, n_ctx=n_ctx, wtype=wtype))
+    prompt = O.make_prompt(n_prompt, shape["n_vocab"])
+    seq_ref, lg_ref = m.generate(prompt, n_decode)
+    e = _engine(shape, n_ctx=n_ctx, wtype=wtype)
+    p = e.plan()
+    p.update(plan_edit(p))
+    e.set_plan(p)
+    e.begin(prompt)
+    lg = e.step(n_prompt + n_decode, want_logits=True)
+    assert list(e.tokens()[: len(seq_ref)]) == list(seq_ref)
+    got = lg[n_prompt - 1:]
+    assert np.array_equal(got.view(np.uint32), lg_ref.view(np.uint32))
+    e.close()
+
+
+@gpu
+@pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
+@pytest.mark.parametrize("rpw,img", [(1, 0), (1, 1), (2, 1)])
+def test_gate_up_split_waves_bitexact(wtype, rpw, img):
+    """gate/up with gate and up on separate waves (plan k_split 2), with / without the h image."""
+    shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
+    _check_decode_plan(shape, 9, 6, 128, wtype,
+                       lambda p: {"gate_up": (2, rpw, 0), "down": (p["down"][0], p["down"][1], img)})
+
+
+@gpu
+def test_gate_up_split_waves_tiny_multi_round():
+    """several row tiles per wave pair (rounds > 1: the refill path)."""
+    _check_decode_plan(O.TINY, 7, 10, 128, O.Q4_0, lambda p: {"gate_up": (2, 16, 0)})
