@@ -311,10 +311,10 @@ __device__ __forceinline__ uint2 bytes_to_f16x4(uint32_t v, uint32_t bias_pair) 
 #define GHIP_XWAVES 4
 #endif
 #ifndef GHIP_XRT
-#define GHIP_XRT 4
+#define GHIP_XRT 8
 #endif
 constexpr int XCT = GHIP_XCT;             // 16-token MFMA column tiles per wave
-constexpr int XRT = GHIP_XRT;             // 2-row MFMA row tiles per wave
+constexpr int XRT = GHIP_XRT;             // 2-row MFMA row tiles per wave (W32: XRT/4 8-row groups; 8 measured best)
 constexpr int XW = GHIP_XWAVES;           // waves per workgroup: XWR row groups x XWC token groups
 constexpr int XNT = 64 * XW;
 constexpr int XM = 32, XWR = XM / (2 * XRT), XWC = XW / XWR, XN = XWC * 16 * XCT, XKB = 8;
@@ -343,7 +343,8 @@ __global__ void __launch_bounds__(XNT)
 __attribute__((amdgpu_waves_per_eu(GHIP_XWPE, GHIP_XWPE)))
 #endif
 k_gemm_x(gemm_args g) {
-    static_assert(!W32 || (XRT == 4 && XCT == 2), "W32: waves of 8 rows x 32 tokens");
+    static_assert(!W32 || (XRT % 4 == 0 && XCT == 2), "W32: waves of 8*RG rows x 32 tokens");
+    constexpr int RG = W32 ? XRT / 4 : 1;  // W32: 8-row groups per wave
     // A fragments: [b][row][lane] 16 B (lane l's 4 f16 in half l&1 of the fragment)
     // + a zero region the inactive lanes read at the same strides (no per-lane select)
     __shared__ __attribute__((aligned(16))) uint4 Wf[XKB * XM * 8 + 7 * 16 + 1];
@@ -368,7 +369,8 @@ k_gemm_x(gemm_args g) {
                          : W32  ? &Wf[(wr + ((lane & 31) >> 2)) * 8 + (lane & 3)]
                                 : &Wf[(wr + (l16 >> 3)) * 8 + (l16 & 7)];
     const int a_bstride = a_act ? XM * 8 : 0;
-    const int a_hoff = a_act ? 4 : 0;  // W32: the half-1 lanes' fragments (lane 4 + (lane & 3))
+    const int a_hoff = a_act ? 4 : 0;    // W32: the half-1 lanes' fragments (lane 4 + (lane & 3))
+    const int a_rgoff = a_act ? 64 : 0;  // W32: the next 8-row group
     for (int i = tid; i < 7 * 16 + 1; i += XNT) Wf[XKB * XM * 8 + i] = make_uint4(0u, 0u, 0u, 0u);
 
     float acc[XRT][XCT][4];
@@ -490,35 +492,45 @@ k_gemm_x(gemm_args g) {
 
     // ---- W32 operands and block step ----
     const int n32 = lane & 31, g32 = lane >> 5;
-    float acc32[4][8];
+    float acc32[RG][4][8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int q = 0; q < RG; ++q)
 #pragma unroll
-        for (int l = 0; l < 8; ++l) acc32[j][l] = 0.0f;
-    struct frag32 { xh8 a[2]; xh8 b[2]; float dw[4]; float da; };
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc32[q][j][l] = 0.0f;
+    struct frag32 { xh8 a[RG][2]; xh8 b[2]; float dw[RG][4]; float da; };
     auto ldfrag32 = [&](int b, frag32 &f) {
-        const uint4 *ab = a_ptr + b * a_bstride;
-        f.a[0] = *(const xh8 *)ab;
-        f.a[1] = *(const xh8 *)(ab + a_hoff);
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            const uint4 *ab = a_ptr + b * a_bstride + q * a_rgoff;
+            f.a[q][0] = *(const xh8 *)ab;
+            f.a[q][1] = *(const xh8 *)(ab + a_hoff);
+            const float4 dwq = *(const float4 *)&dws[b][g32][wr / 2 + 4 * q];
+            f.dw[q][0] = dwq.x; f.dw[q][1] = dwq.y; f.dw[q][2] = dwq.z; f.dw[q][3] = dwq.w;
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) f.b[h] = *(const xh8 *)(Xs + (wt + n32) * XS_ROW + b * 64 + h * 32 + g32 * 16);
         f.da = das[b][wt + n32];
-        const float4 dwq = *(const float4 *)&dws[b][g32][wr / 2];
-        f.dw[0] = dwq.x; f.dw[1] = dwq.y; f.dw[2] = dwq.z; f.dw[3] = dwq.w;
     };
     auto block32 = [&](const frag32 &f) {
         const xf16v z = {};
-        const xf16v d0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[0], f.b[0], z, 0, 0, 0);
-        const xf16v d1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[1], f.b[1], z, 0, 0, 0);
+        xf16v d[RG][2];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float d = f.dw[j] * f.da;
+        for (int q = 0; q < RG; ++q)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                acc32[j][i] = __builtin_fmaf(d, d0[4 * j + i], acc32[j][i]);
-                acc32[j][4 + i] = __builtin_fmaf(d, d1[4 * j + i], acc32[j][4 + i]);
+            for (int h = 0; h < 2; ++h) d[q][h] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[q][h], f.b[h], z, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < RG; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float dd = f.dw[q][j] * f.da;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    acc32[q][j][i] = __builtin_fmaf(dd, d[q][0][4 * j + i], acc32[q][j][i]);
+                    acc32[q][j][4 + i] = __builtin_fmaf(dd, d[q][1][4 * j + i], acc32[q][j][4 + i]);
+                }
             }
-        }
     };
 
     gload(0);
@@ -557,14 +569,16 @@ k_gemm_x(gemm_args g) {
     if constexpr (W32) {  // hsum in registers: ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7))
         const int64_t t = t0 + wt + n32;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float *a = acc32[j];
-            float o = ((a[0] + a[4]) + (a[2] + a[6])) + ((a[1] + a[5]) + (a[3] + a[7]));
-            const int64_t r = r0 + wr + 2 * j + g32;
-            if (t >= g.T || r >= g.rows) continue;
-            if (EPI == EPI_ADD) o = o + g.resid[t * g.ldy + r];
-            g.y[t * g.ldy + r] = o;
-        }
+        for (int q = 0; q < RG; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float *a = acc32[q][j];
+                float o = ((a[0] + a[4]) + (a[2] + a[6])) + ((a[1] + a[5]) + (a[3] + a[7]));
+                const int64_t r = r0 + wr + 8 * q + 2 * j + g32;
+                if (t >= g.T || r >= g.rows) continue;
+                if (EPI == EPI_ADD) o = o + g.resid[t * g.ldy + r];
+                g.y[t * g.ldy + r] = o;
+            }
         return;
     }
     // hsum: lane kg even holds lanes 0-3 of (row, token), lane^16 lanes 4-7
