@@ -330,6 +330,9 @@ static_assert(XN * XKB * 64 / 16 % XNT == 0, "token records");
 #ifndef GHIP_X32
 #define GHIP_X32 1
 #endif
+#ifndef GHIP_XMASK
+#define GHIP_XMASK 0  // 1: EXEC-masked A reads for the inactive lanes (measured slower: 99.6 vs 88.0 ms)
+#endif
 // W32: the lane sums from v_mfma_f32_32x32x16_f16 instead (the default).  K = 16 covers half a
 // block, and only the four AVX2 lanes 4h..4h+3 have elements in half h, so MFMA row m = 4*row + i
 // (i = lane & 3 of half h) wastes 3/4 of each A row instead of 7/8: a wave's 8 rows x 32 tokens per
@@ -347,7 +350,10 @@ k_gemm_x(gemm_args g) {
     constexpr int RG = W32 ? XRT / 4 : 1;  // W32: 8-row groups per wave
     // A fragments: [b][row][lane] 16 B (lane l's 4 f16 in half l&1 of the fragment)
     // + a zero region the inactive lanes read at the same strides (no per-lane select)
-    __shared__ __attribute__((aligned(16))) uint4 Wf[XKB * XM * 8 + 7 * 16 + 1];
+    // W32 pads the fragment rows to 9 x 16 B: the 8 active lanes of a ds_read_b128 lane group then
+    // hit distinct banks (rows 2 apart would share them at 8 x 16 B)
+    constexpr int WFR = W32 ? 9 : 8;
+    __shared__ __attribute__((aligned(16))) uint4 Wf[XKB * XM * WFR + 7 * 16 + 1];
     __shared__ __attribute__((aligned(16))) uint8_t Xs[XN * XS_ROW];
     __shared__ __attribute__((aligned(16))) float dws[XKB][2][XM / 2];  // [b][row & 1][row >> 1]
     __shared__ __attribute__((aligned(16))) float das[XKB][XN];
@@ -365,13 +371,13 @@ k_gemm_x(gemm_args g) {
     // W32: MFMA row (lane & 31) = 4 * row + (lane & 3); lane's k group 8*(lane >> 5) .. holds the
     // elements of AVX2 lane 4h + (lane & 3) iff (lane >> 5) == (lane & 3) >> 1
     const bool a_act = W32 ? (lane >> 5) == ((lane & 3) >> 1) : ((l16 & 7) >> 1) == kg;
-    const uint4 *a_ptr = !a_act ? &Wf[XKB * XM * 8]
-                         : W32  ? &Wf[(wr + ((lane & 31) >> 2)) * 8 + (lane & 3)]
+    const uint4 *a_ptr = !a_act ? &Wf[XKB * XM * WFR]
+                         : W32  ? &Wf[(wr + ((lane & 31) >> 2)) * WFR + (lane & 3)]
                                 : &Wf[(wr + (l16 >> 3)) * 8 + (l16 & 7)];
-    const int a_bstride = a_act ? XM * 8 : 0;
-    const int a_hoff = a_act ? 4 : 0;    // W32: the half-1 lanes' fragments (lane 4 + (lane & 3))
-    const int a_rgoff = a_act ? 64 : 0;  // W32: the next 8-row group
-    for (int i = tid; i < 7 * 16 + 1; i += XNT) Wf[XKB * XM * 8 + i] = make_uint4(0u, 0u, 0u, 0u);
+    const int a_bstride = a_act ? XM * WFR : 0;
+    const int a_hoff = a_act ? 4 : 0;          // W32: the half-1 lanes' fragments (lane 4 + (lane & 3))
+    const int a_rgoff = a_act ? 8 * WFR : 0;   // W32: the next 8-row group
+    for (int i = tid; i < 7 * 16 + 1; i += XNT) Wf[XKB * XM * WFR + i] = make_uint4(0u, 0u, 0u, 0u);
 
     float acc[XRT][XCT][4];
 #pragma unroll
@@ -423,7 +429,7 @@ k_gemm_x(gemm_args g) {
             const uint32_t qd[4] = {wq[k].x, wq[k].y, wq[k].z, wq[k].w};
             const uint32_t sd[4] = {ws[k].x, ws[k].y, ws[k].z, ws[k].w};
             auto put = [&](int b, uint2 f) {
-                Wf[(b * XM + row) * 8 + l] = (l & 1) ? make_uint4(0u, 0u, f.x, f.y) : make_uint4(f.x, f.y, 0u, 0u);
+                Wf[(b * XM + row) * WFR + l] = (l & 1) ? make_uint4(0u, 0u, f.x, f.y) : make_uint4(f.x, f.y, 0u, 0u);
             };
             if (WT == T_Q4_0) {
 #pragma unroll
@@ -504,8 +510,14 @@ k_gemm_x(gemm_args g) {
 #pragma unroll
         for (int q = 0; q < RG; ++q) {
             const uint4 *ab = a_ptr + b * a_bstride + q * a_rgoff;
+#if GHIP_XMASK
+            const xh8 zh = {};
+            f.a[q][0] = a_act ? *(const xh8 *)ab : zh;  // inactive lanes: no LDS access (EXEC-masked)
+            f.a[q][1] = a_act ? *(const xh8 *)(ab + a_hoff) : zh;
+#else
             f.a[q][0] = *(const xh8 *)ab;
             f.a[q][1] = *(const xh8 *)(ab + a_hoff);
+#endif
             const float4 dwq = *(const float4 *)&dws[b][g32][wr / 2 + 4 * q];
             f.dw[q][0] = dwq.x; f.dw[q][1] = dwq.y; f.dw[q][2] = dwq.z; f.dw[q][3] = dwq.w;
         }
@@ -540,11 +552,22 @@ k_gemm_x(gemm_args g) {
         if (kb0 + XKB < nb) gload(kb0 + XKB);
         const int nbs = (int)(nb - kb0 < XKB ? nb - kb0 : XKB);
         if constexpr (W32) {
+#if GHIP_XPF
+            frag32 cur;
+            ldfrag32(0, cur);
+            for (int b = 0; b < nbs; ++b) {
+                frag32 nxt;
+                ldfrag32(b + 1 < nbs ? b + 1 : b, nxt);  // next block's operands in flight
+                block32(cur);
+                cur = nxt;
+            }
+#else
             for (int b = 0; b < nbs; ++b) {
                 frag32 cur;
                 ldfrag32(b, cur);
                 block32(cur);
             }
+#endif
             __syncthreads();
             continue;
         }
