@@ -330,6 +330,9 @@ static_assert(XN * XKB * 64 / 16 % XNT == 0, "token records");
 #ifndef GHIP_X32
 #define GHIP_X32 1
 #endif
+#ifndef GHIP_XCOMPACT
+#define GHIP_XCOMPACT 0  // 1: W32 A fragments stored as their 8 nonzero bytes, placed in registers (90.2 vs 87.6 ms: off)
+#endif
 #ifndef GHIP_XMASK
 #define GHIP_XMASK 0  // 1: EXEC-masked A reads for the inactive lanes (measured slower: 99.6 vs 88.0 ms)
 #endif
@@ -353,7 +356,12 @@ k_gemm_x(gemm_args g) {
     // W32 pads the fragment rows to 9 x 16 B: the 8 active lanes of a ds_read_b128 lane group then
     // hit distinct banks (rows 2 apart would share them at 8 x 16 B)
     constexpr int WFR = W32 ? 9 : 8;
-    __shared__ __attribute__((aligned(16))) uint4 Wf[XKB * XM * WFR + 7 * 16 + 1];
+    // compact W32 image: 8 B per (block, row, lane), rows padded to 10 x 8 B (distinct banks for the
+    // 16 active lanes of a ds_read_b64 lane group); the LDS saved fits a third workgroup per CU
+    constexpr bool CW = W32 && GHIP_XCOMPACT;
+    constexpr int WFR2 = 10;
+    __shared__ __attribute__((aligned(16))) uint4 Wf[CW ? 1 : XKB * XM * WFR + 7 * 16 + 1];
+    __shared__ __attribute__((aligned(16))) uint2 Wf2[CW ? XKB * XM * WFR2 + 8 : 1];
     __shared__ __attribute__((aligned(16))) uint8_t Xs[XN * XS_ROW];
     __shared__ __attribute__((aligned(16))) float dws[XKB][2][XM / 2];  // [b][row & 1][row >> 1]
     __shared__ __attribute__((aligned(16))) float das[XKB][XN];
@@ -371,13 +379,21 @@ k_gemm_x(gemm_args g) {
     // W32: MFMA row (lane & 31) = 4 * row + (lane & 3); lane's k group 8*(lane >> 5) .. holds the
     // elements of AVX2 lane 4h + (lane & 3) iff (lane >> 5) == (lane & 3) >> 1
     const bool a_act = W32 ? (lane >> 5) == ((lane & 3) >> 1) : ((l16 & 7) >> 1) == kg;
-    const uint4 *a_ptr = !a_act ? &Wf[XKB * XM * WFR]
+    const uint4 *a_ptr = CW      ? Wf
+                         : !a_act ? &Wf[XKB * XM * WFR]
                          : W32  ? &Wf[(wr + ((lane & 31) >> 2)) * WFR + (lane & 3)]
                                 : &Wf[(wr + (l16 >> 3)) * 8 + (l16 & 7)];
     const int a_bstride = a_act ? XM * WFR : 0;
     const int a_hoff = a_act ? 4 : 0;          // W32: the half-1 lanes' fragments (lane 4 + (lane & 3))
     const int a_rgoff = a_act ? 8 * WFR : 0;   // W32: the next 8-row group
-    for (int i = tid; i < 7 * 16 + 1; i += XNT) Wf[XKB * XM * WFR + i] = make_uint4(0u, 0u, 0u, 0u);
+    if (CW) {
+        for (int i = tid; i < 8; i += XNT) Wf2[XKB * XM * WFR2 + i] = make_uint2(0u, 0u);
+    } else {
+        for (int i = tid; i < 7 * 16 + 1; i += XNT) Wf[XKB * XM * WFR + i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    const uint2 *a_ptr2 = !a_act ? &Wf2[CW ? XKB * XM * WFR2 : 0] : &Wf2[CW ? (wr + ((lane & 31) >> 2)) * WFR2 + (lane & 3) : 0];
+    const int a_bstride2 = a_act ? XM * WFR2 : 0, a_rgoff2 = a_act ? 8 * WFR2 : 0;
+    const bool a_hi = (lane & 1) != 0;  // W32: this lane's 4 elements sit in the upper half of its 8
 
     float acc[XRT][XCT][4];
 #pragma unroll
@@ -429,7 +445,8 @@ k_gemm_x(gemm_args g) {
             const uint32_t qd[4] = {wq[k].x, wq[k].y, wq[k].z, wq[k].w};
             const uint32_t sd[4] = {ws[k].x, ws[k].y, ws[k].z, ws[k].w};
             auto put = [&](int b, uint2 f) {
-                Wf[(b * XM + row) * WFR + l] = (l & 1) ? make_uint4(0u, 0u, f.x, f.y) : make_uint4(f.x, f.y, 0u, 0u);
+                if (CW) Wf2[(b * XM + row) * WFR2 + l] = f;
+                else Wf[(b * XM + row) * WFR + l] = (l & 1) ? make_uint4(0u, 0u, f.x, f.y) : make_uint4(f.x, f.y, 0u, 0u);
             };
             if (WT == T_Q4_0) {
 #pragma unroll
@@ -509,6 +526,19 @@ k_gemm_x(gemm_args g) {
     auto ldfrag32 = [&](int b, frag32 &f) {
 #pragma unroll
         for (int q = 0; q < RG; ++q) {
+            if constexpr (CW) {
+                const uint2 *ab2 = a_ptr2 + b * a_bstride2 + q * a_rgoff2;
+                const uint2 v0 = ab2[0], v1 = ab2[a_hoff];
+                auto place = [&](uint2 v) {
+                    const uint4 u = a_hi ? make_uint4(0u, 0u, v.x, v.y) : make_uint4(v.x, v.y, 0u, 0u);
+                    return __builtin_bit_cast(xh8, u);
+                };
+                f.a[q][0] = place(v0);
+                f.a[q][1] = place(v1);
+                const float4 dwq = *(const float4 *)&dws[b][g32][wr / 2 + 4 * q];
+                f.dw[q][0] = dwq.x; f.dw[q][1] = dwq.y; f.dw[q][2] = dwq.z; f.dw[q][3] = dwq.w;
+                continue;
+            }
             const uint4 *ab = a_ptr + b * a_bstride + q * a_rgoff;
 #if GHIP_XMASK
             const xh8 zh = {};
