@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <string>
 #include <vector>
@@ -353,7 +354,11 @@ int main(int argc, char **argv) {
     FILE *out = fopen(argv[3], "wb");
     std::vector<int32_t> toks;
     std::vector<float> row;
+    // timing as begin_one_round_inference reports it (src/gemma_model.cpp:552-572): prefill, then decode
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_start = now(), t_prefill = t_start;
     for (int step = 0; step <= n_decode; ++step) {  // inference (:231-286)
+        if (step == 1) t_prefill = now();
         const stage st = step == 0 ? PREFILL : DECODE;
         update_kv_cache(m, input, st);
         load_input_tokens_to_tensor(m, input, st);
@@ -368,6 +373,11 @@ int main(int argc, char **argv) {
         toks.push_back(t);
         input.push_back(t);
     }
+    const auto t_end = now();
+    const double pf_ms = std::chrono::duration<double, std::milli>(t_prefill - t_start).count();
+    const double dec_ms = std::chrono::duration<double, std::milli>(t_end - t_prefill).count();
+    fprintf(stderr, "timing prefill_ms %.3f prompt %zu decode_ms %.3f steps %d decode_tok_s %.2f\n", pf_ms,
+            T, dec_ms, n_decode, n_decode > 0 ? n_decode / (dec_ms * 1e-3) : 0.0);
     fwrite(toks.data(), 4, toks.size(), out);
     fclose(out);
     if (gguf) {  // the sequence as text, through the GGUF tokenizer table
