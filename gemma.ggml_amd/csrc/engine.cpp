@@ -161,6 +161,12 @@ struct gemma_engine {
     gemma_hip_config cfg{};
     int device = 0;
     hipStream_t stream = nullptr;
+    // MALL warm-up (GHIP_WARM): while a layer's attention runs on a few CUs, a side-stream kernel
+    // reads that layer's attn-out and gate/up weights so their matvecs stream from the Infinity Cache
+    int warm = 0, warm_grid = 512;
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> ev_fork;
+    hipEvent_t ev_join = nullptr;
     int qw = 0, kvw = 0, qkv_rows = 0;
     tiled_mat embd;
     // token_embd / tied output in Q6_K (llama.cpp's Q4_0 / Q8_0 Gemma files): raw ggml rows, the
@@ -278,6 +284,16 @@ static int tp_gather_bytes(gemma_engine *e, uint32_t *act, int64_t act_bytes, fl
 static inline layer_dev &layer_of(gemma_engine *e, int il, int vr) { return e->layers[(size_t)il * e->n_virtual + vr]; }
 static inline int rank_of(const gemma_engine *e, int vr) { return e->n_virtual > 1 ? vr : e->tp_rank; }
 
+static inline int wfmt_scale(int wt) { return wt == T_Q4_0 ? 16 : 8; }  // scale bytes per row and tile
+
+// join the warm-up side stream back into the engine stream (one join per step / capture)
+static int warm_join(gemma_engine *e) {
+    if (!e->warm || !e->side) return 0;
+    GHIP_CHECK(hipEventRecord(e->ev_join, e->side));
+    GHIP_CHECK(hipStreamWaitEvent(e->stream, e->ev_join, 0));
+    return 0;
+}
+
 static int enqueue_step(gemma_engine *e) {
     const gemma_hip_config &c = e->cfg;
     const int wt = c.wtype;
@@ -323,6 +339,16 @@ static int enqueue_step(gemma_engine *e) {
         t.mode = e->att_mode;
         t.nwg = e->ag.nwg; t.sbuf = e->att_sbuf; t.sync = e->att_sync; t.err = e->att_sync + e->ag.sync_ints;
         t.dbg_t = stamp_region(e, il, 1);
+        if (e->warm && e->side) {  // fork: warm attn-out + gate/up while attention runs
+            const layer_dev &W = layer_of(e, il, 0);
+            const void *ptrs[6] = {W.o.qs, W.o.sc, W.gate.qs, W.gate.sc, W.up.qs, W.up.sc};
+            const int64_t bytes[6] = {W.o.n_rt * W.o.n_bt * 1024, W.o.n_rt * W.o.n_bt * 8 * wfmt_scale(wt),
+                                      W.gate.n_rt * W.gate.n_bt * 1024, W.gate.n_rt * W.gate.n_bt * 8 * wfmt_scale(wt),
+                                      W.up.n_rt * W.up.n_bt * 1024, W.up.n_rt * W.up.n_bt * 8 * wfmt_scale(wt)};
+            GHIP_CHECK(hipEventRecord(e->ev_fork[il], s));
+            GHIP_CHECK(hipStreamWaitEvent(e->side, e->ev_fork[il], 0));
+            if (launch_mall_warm(ptrs, bytes, 6, e->warm_grid, e->side)) return -1;
+        }
         if (launch_attn_decode(t, s)) return -1;
         const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
         if (e->dbg) GHIP_CHECK(hipMemcpyAsync(e->dbg + tap, e->qkv, (size_t)e->qkv_rows * 4, hipMemcpyDeviceToDevice, s));
@@ -395,7 +421,8 @@ static int enqueue_step(gemma_engine *e) {
         k.x = e->xq8k; k.x_col_stride = (E / 256) * 292; k.y = e->logits; k.y_col_stride = c.n_vocab; k.ncols = 1;
         if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
         if (launch_row_argmax(e->logits, c.n_vocab, e->key, 256, s)) return -1;
-        return launch_advance(e->key, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
+        if (launch_advance(e->key, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s)) return -1;
+        return warm_join(e);
     }
     int lg_grid = 0;
     for (int vr = 0; vr < e->n_virtual; ++vr) {
@@ -412,7 +439,10 @@ static int enqueue_step(gemma_engine *e) {
         // TP: one key per rank, its index made global
         if (e->tp_n > 1 && launch_reduce_keys(e->key, lg_grid, (int64_t)rk * e->sh_v, e->rank_keys + rk, s)) return -1;
     }
-    if (e->tp_n == 1) return launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
+    if (e->tp_n == 1) {
+        if (launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s)) return -1;
+        return warm_join(e);
+    }
     if (e->comm) {
         const ncclResult_t nr = ncclAllGather(e->rank_keys + e->tp_rank, e->rank_keys, 1, ncclUint64, e->comm, s);
         if (nr != ncclSuccess) {
@@ -486,6 +516,15 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     if (const char *v = getenv("GHIP_KS_SMALL")) e->ks_small = atoi(v);
     if (const char *v = getenv("GHIP_KS_DOWN")) e->ks_down = atoi(v);
     if (const char *v = getenv("GHIP_GRID_BIG")) e->grid_big = atoi(v);
+    if (const char *v = getenv("GHIP_WARM")) e->warm = atoi(v);
+    if (const char *v = getenv("GHIP_WARM_GRID")) e->warm_grid = atoi(v);
+    if (tp_n > 1) e->warm = 0;  // single-GPU decode only
+    if (e->warm) {
+        GHIP_FATAL(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+        e->ev_fork.resize(c.n_layer);
+        for (hipEvent_t &ev : e->ev_fork) GHIP_FATAL(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        GHIP_FATAL(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+    }
     const int wt = c.wtype;
     const uint64_t seed = c.seed;
     hipStream_t s = e->stream;
@@ -794,6 +833,9 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (e->embd_q6k) (void)hipFree(e->embd_q6k);
+    for (hipEvent_t ev : e->ev_fork) (void)hipEventDestroy(ev);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->side) (void)hipStreamDestroy(e->side);
     if (e->xq8k) (void)hipFree(e->xq8k);
     (void)hipStreamDestroy(e->stream);
     delete e;

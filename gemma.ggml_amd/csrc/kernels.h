@@ -220,6 +220,8 @@ struct rope_row {  // k_advance also publishes the new position's RoPE row: cur 
     float *cur = nullptr;
     int half = 0, ctx = 0;
 };
+// read `n` weight regions with allocating loads (MALL warm-up for a later kernel), `grid` workgroups
+int launch_mall_warm(const void *const *ptrs, const int64_t *bytes, int n, int grid, hipStream_t s);
 int launch_advance(const unsigned long long *keys, int n_parts, int *token, int *pos, int *hist, int hist_cap,
                    const int *n_fixed, const rope_row &r, hipStream_t s);
 

@@ -920,6 +920,30 @@ __global__ void __launch_bounds__(256) k_stream_read(const uint4 *src_, uint64_t
     if (acc == 0x9E3779B9u) *sink = acc;  // never true for the memset pattern: keeps the loads
 }
 
+// MALL warm-up of weights a later kernel will stream (engine side stream, during attention): plain
+// (allocating) loads over up to 6 regions, grid-stride; the XOR keeps the loads alive
+struct warm_regions { const uint4 *p[6]; uint64_t n16[6]; int n; };
+__global__ void __launch_bounds__(256) k_mall_warm(warm_regions r, unsigned *sink) {
+    const uint64_t nth = (uint64_t)gridDim.x * 256;
+    uint32_t acc = 0;
+    for (int k = 0; k < r.n; ++k) {
+        const v4u_t *src = (const v4u_t *)r.p[k];
+        uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+        for (; i + 3 * nth < r.n16[k]; i += 4 * nth) {
+            v4u_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = src[i + u * nth];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+        for (; i < r.n16[k]; i += nth) {
+            const v4u_t v = src[i];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == 0x9E3779B9u && sink) *sink = acc;
+}
+
 __global__ void k_exp_f16_all(uint16_t *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < 65536) out[i] = (uint16_t)exp_f16_of((uint32_t)i);
@@ -1138,6 +1162,18 @@ int launch_exp_f16_all(uint16_t *out, hipStream_t s) {
 
 int launch_reduce_keys(const unsigned long long *keys, int n, int64_t row_base, unsigned long long *out, hipStream_t s) {
     hipLaunchKernelGGL(k_reduce_keys, dim3(1), dim3(256), 0, s, keys, n, row_base, out);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_mall_warm(const void *const *ptrs, const int64_t *bytes, int n, int grid, hipStream_t s) {
+    warm_regions r{};
+    r.n = n < 6 ? n : 6;
+    for (int k = 0; k < r.n; ++k) {
+        r.p[k] = (const uint4 *)ptrs[k];
+        r.n16[k] = (uint64_t)bytes[k] / 16;
+    }
+    hipLaunchKernelGGL(k_mall_warm, dim3((unsigned)grid), dim3(256), 0, s, r, nullptr);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }
