@@ -215,6 +215,32 @@ def main():
         except Exception as ex:  # reported, never fatal to the headline line
             q6o = {"error": str(ex)[:300]}
 
+    # the reference's shipped format (src/app.cpp:36, gemma-2b-it-q4_k_m): K-quant layers (Q4_K q/k/o/
+    # gate/up, Q6_K v/down) and a Q6_K token_embd / output, token by token through the K-quant matvecs
+    kqm = None
+    if args.wtype == "q4_0" and args.q8_steps > 0:
+        try:
+            E, F, qw, kvw, V = (GEMMA_2B[k] for k in ("n_embd", "n_ff", "n_head", "n_head_kv", "n_vocab"))
+            qw, kvw = qw * GEMMA_2B["head_dim"], kvw * GEMMA_2B["head_dim"]
+            q4k = (qw * E + kvw * E + E * qw + 2 * F * E) * 144 // 256
+            q6k = (kvw * E + E * F) * 210 // 256
+            kbytes = GEMMA_2B["n_layer"] * (q4k + q6k) + V * E * 210 // 256
+            ke = G.Engine(GEMMA_2B, n_ctx=args.ctx, wtype=G.GGML_TYPE_Q4_K, device=local_rank)
+            ke.begin(prompt)
+            ke.step(args.prompt + args.warmup, use_graph=True)
+            ke.L.gemma_engine_sync(ke.h)
+            t0 = time.perf_counter()
+            ke.step(args.q8_steps, use_graph=True)
+            ke.L.gemma_engine_sync(ke.h)
+            kdt = time.perf_counter() - t0
+            ke.close()
+            kqm = {"model": "Gemma-2B Q4_K_M layout (Q4_K/Q6_K layers, Q6_K output; the reference's shipped format)",
+                   "tok_s": round(args.q8_steps / kdt, 2), "ms_per_token": round(kdt / args.q8_steps * 1e3, 4),
+                   "steps": args.q8_steps, "token_weight_bytes": kbytes,
+                   "weight_GB_s": round(kbytes * args.q8_steps / kdt / 1e9, 1)}
+        except Exception as ex:  # reported, never fatal to the headline line
+            kqm = {"error": str(ex)[:300]}
+
     # prefill leg (BASELINE config 3): batched prefill of a 2048-token synthetic prompt, logits for
     # every row as the reference computes them.  "exact": bit-identical to the CPU path (the
     # headline prefill_tok_s); "fast": int8/f16 MFMA, fp32 summation order differs
@@ -294,6 +320,7 @@ def main():
             "kquant_matvec": kquant,
             "q8_0_decode": q8,
             "q4_0_q6k_output_decode": q6o,
+            "q4_k_m_decode": kqm,
             "tp_decode": tp,
             "launch_plan": {k: ({"k_split": v[0], "rows_per_wg": v[1], "image": v[2]} if isinstance(v, tuple) else
                                 ("split" if v else "per_head")) for k, v in plan.items()},

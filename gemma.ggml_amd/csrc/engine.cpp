@@ -147,6 +147,17 @@ struct layer_dev {
     tiled_mat qkv, o, gate, up, down;
 };
 
+// K-quant layer matrices (wtype GGML_TYPE_Q4_K: llama.cpp's Q4_K_M files): raw ggml rows, each
+// matrix Q4_K or Q6_K, multiplied by the K-quant matvec against the Q8_K INIT of its input
+struct kq_mat {
+    uint8_t *w = nullptr;
+    int type = 0;
+    int64_t rows = 0, K = 0, rb = 0;
+};
+struct kq_layer {
+    kq_mat q, k, v, o, gate, up, down;
+};
+
 struct gemma_engine;
 static bool att_img_ok(const gemma_engine *e);
 
@@ -172,6 +183,10 @@ struct gemma_engine {
     // token_embd / tied output in Q6_K (llama.cpp's Q4_0 / Q8_0 Gemma files): raw ggml rows, the
     // embedding dequantized by k_embed_q6K and the logits through the K-quant matvec
     int out_type = 0;
+    bool kq = false;              // K-quant layers (kql) instead of the tiled Q4_0 / Q8_0 ones
+    std::vector<kq_layer> kql;
+    uint8_t *kq_x = nullptr;      // Q8_K INIT of the current matvec input (max(E, qw, F) / 256 blocks)
+    float *kq_g = nullptr;        // ffn gate output (n_ff), consumed by the up matvec's gelu*mul epilogue
     uint8_t *embd_q6k = nullptr;
     int64_t embd_row_bytes = 0;
     uint8_t *xq8k = nullptr;  // Q8_K rows of rms_norm(x)*out_norm (decode: 1 row; prefill: T rows)
@@ -294,11 +309,18 @@ static int warm_join(gemma_engine *e) {
     return 0;
 }
 
+static int enqueue_step_kq(gemma_engine *e, const rope_row &rr);
+
 static int enqueue_step(gemma_engine *e) {
     const gemma_hip_config &c = e->cfg;
     const int wt = c.wtype;
     hipStream_t s = e->stream;
     const int E = c.n_embd;
+    if (e->kq) {
+        rope_row rr;
+        rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+        return enqueue_step_kq(e, rr);
+    }
     if (e->out_type == T_Q6_K &&
         launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s))
         return -1;
@@ -453,6 +475,57 @@ static int enqueue_step(gemma_engine *e) {
     return launch_advance(e->rank_keys, e->tp_n, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
 }
 
+// One decode token with K-quant layer matrices (src/gemma_model.cpp:665-747 on a Q4_K_M file):
+// per layer rms_norm*attn_norm -> Q8_K -> Wq, Wk, Wv (K-quant dots) -> attention (the same kernel)
+// -> Q8_K(attn) -> Wo (+inpL) -> rms_norm*ffn_norm -> Q8_K -> Wgate, Wup (gelu(gate)*up epilogue)
+// -> Q8_K(h) -> Wdown (+sa); then the Q6_K tied output.  ggml's INIT and vec_dot order throughout.
+static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
+    const gemma_hip_config &c = e->cfg;
+    hipStream_t s = e->stream;
+    const int E = c.n_embd;
+    auto mv = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in) {
+        kq_args k;
+        k.w = W.w; k.row_bytes = W.rb; k.rows = W.rows; k.nsb = (int)(W.K / 256);
+        k.x = e->kq_x; k.x_col_stride = (W.K / 256) * 292; k.y = y; k.y_col_stride = W.rows; k.ncols = 1;
+        k.resid = resid; k.gate_in = gate_in; k.gelu_tab = e->gelu_tab; k.gelu_clamp = c.gelu_clamp;
+        return launch_matvec_kq(W.type, k, s);
+    };
+    if (launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s)) return -1;
+    for (int il = 0; il < c.n_layer; ++il) {
+        const layer_dev &L = e->layers[il];
+        const kq_layer &K = e->kql[il];
+        if (launch_norm_q8K(e->x, E, L.attn_norm, E, c.eps, 1, e->kq_x, (E / 256) * 292, s)) return -1;
+        if (mv(K.q, e->qkv, nullptr, nullptr) || mv(K.k, e->qkv + e->qw, nullptr, nullptr) ||
+            mv(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr))
+            return -1;
+        attn_args t;
+        t.qkv = e->qkv;
+        t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
+        t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
+        t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.rope_cur = e->rope_cur; t.exp_tab = e->exp_tab;
+        t.pos = e->pos; t.out = e->attn;
+        t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
+        t.q_scale = 1.0f / sqrtf((float)c.head_dim);
+        t.mode = e->att_mode;
+        t.nwg = e->ag.nwg; t.sbuf = e->att_sbuf; t.sync = e->att_sync; t.err = e->att_sync + e->ag.sync_ints;
+        if (launch_attn_decode(t, s)) return -1;
+        if (launch_quant_q8_K(e->attn, e->qw, e->qw, 1, e->kq_x, (e->qw / 256) * 292, s)) return -1;
+        if (mv(K.o, e->sa, e->x, nullptr)) return -1;                       // + inpL (:723)
+        if (launch_norm_q8K(e->sa, E, L.ffn_norm, E, c.eps, 1, e->kq_x, (E / 256) * 292, s)) return -1;
+        if (mv(K.gate, e->kq_g, nullptr, nullptr) || mv(K.up, e->h, nullptr, e->kq_g)) return -1;  // (:446-449)
+        if (launch_quant_q8_K(e->h, c.n_ff, c.n_ff, 1, e->kq_x, (c.n_ff / 256) * 292, s)) return -1;
+        if (mv(K.down, e->x, e->sa, nullptr)) return -1;                    // + sa (:731)
+    }
+    if (launch_norm_q8K(e->x, E, e->out_norm, E, c.eps, 1, e->xq8k, (E / 256) * 292, s)) return -1;
+    kq_args k;
+    k.w = e->embd_q6k; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = E / 256;
+    k.x = e->xq8k; k.x_col_stride = (E / 256) * 292; k.y = e->logits; k.y_col_stride = c.n_vocab; k.ncols = 1;
+    if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
+    if (launch_row_argmax(e->logits, c.n_vocab, e->key, 256, s)) return -1;
+    if (launch_advance(e->key, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s)) return -1;
+    return warm_join(e);
+}
+
 // real weights in ggml row-major layout (a GGUF file's tensors, src/gemma_model.cpp:145-182)
 struct host_weights {
     const void *embd = nullptr;  // token_embd, type cfg.out_type (or wtype)
@@ -460,6 +533,7 @@ struct host_weights {
     struct layer {
         const float *attn_norm = nullptr, *ffn_norm = nullptr;
         const void *q = nullptr, *k = nullptr, *v = nullptr, *o = nullptr, *gate = nullptr, *up = nullptr, *down = nullptr;
+        int tq = 0, tk = 0, tv = 0, to = 0, tg = 0, tu = 0, td = 0;  // K-quant layers: each matrix's type
     };
     std::vector<layer> layers;
 };
@@ -480,12 +554,18 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
                                    const host_weights *hw = nullptr) {
     set_error("");
     const gemma_hip_config &c = *cfg;
+    const bool kq_layers = c.wtype == T_Q4_K;  // K-quant layers (Q4_K / Q6_K per matrix) + Q6_K output
     if (c.head_dim % 32 || c.n_embd % 32 || c.n_ff % 32 || c.n_ctx % 32 || c.n_head % c.n_head_kv ||
-        (c.wtype != T_Q4_0 && c.wtype != T_Q8_0) || (c.out_type != 0 && c.out_type != c.wtype && c.out_type != T_Q6_K)) {
+        (c.wtype != T_Q4_0 && c.wtype != T_Q8_0 && !kq_layers) ||
+        (c.out_type != 0 && c.out_type != c.wtype && c.out_type != T_Q6_K)) {
         set_error("gemma_engine_create: unsupported config");
         return nullptr;
     }
-    if (c.out_type == T_Q6_K && (c.n_embd % 256 || c.n_embd > 4096 || tp_n > 1)) {
+    if (kq_layers && (c.n_embd % 256 || c.n_ff % 256 || (c.n_head * c.head_dim) % 256 || c.n_embd > 4096 || tp_n > 1)) {
+        set_error("gemma_engine_create: K-quant layers need n_embd, n_ff, n_head*head_dim % 256 == 0, n_embd <= 4096, one rank");
+        return nullptr;
+    }
+    if ((c.out_type == T_Q6_K || kq_layers) && (c.n_embd % 256 || c.n_embd > 4096 || tp_n > 1)) {
         set_error("gemma_engine_create: a Q6_K output needs n_embd % 256 == 0, n_embd <= 4096 and one rank");
         return nullptr;
     }
@@ -530,7 +610,8 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     hipStream_t s = e->stream;
     // weights: synthetic generator straight into the tiled layout (matches oracle/gemma_cpu.cpp)
     bool up_fail = false;  // a host-weight upload failed (last_error says which)
-    e->out_type = c.out_type == T_Q6_K ? T_Q6_K : wt;
+    e->kq = kq_layers;
+    e->out_type = (c.out_type == T_Q6_K || kq_layers) ? T_Q6_K : wt;
     if (e->out_type == T_Q6_K) {  // oracle make_kmat(TID_EMBD, Q6_K, 1/sqrt(E)) on the device
         e->embd_row_bytes = (int64_t)c.n_embd / 256 * 210;
         GHIP_FATAL(hipMalloc(&e->embd_q6k, (size_t)(e->embd_row_bytes * c.n_vocab)));
@@ -573,6 +654,36 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         } else {  // norms are replicated: the slot-0 copy serves every virtual rank
             L.attn_norm = layer_of(e, il, 0).attn_norm;
             L.ffn_norm = layer_of(e, il, 0).ffn_norm;
+        }
+        if (kq_layers) {  // raw K-quant rows: uploaded, or the oracle's make_kmat on the device
+            if (e->kql.empty()) e->kql.resize(c.n_layer);
+            kq_layer &K = e->kql[il];
+            const host_weights::layer *H = hw ? &hw->layers[il] : nullptr;
+            auto make = [&](kq_mat &m, int type, int64_t rows, int64_t k, int tid, double stdv, const void *host) {
+                m.type = type;
+                m.rows = rows;
+                m.K = k;
+                m.rb = k / 256 * (type == T_Q4_K ? 144 : 210);
+                if (hipMalloc(&m.w, (size_t)(m.rb * rows)) != hipSuccess) {
+                    set_error("gemma_engine_create: weight alloc failed");
+                    up_fail = true;
+                    return;
+                }
+                if (host) {
+                    up_fail |= hipMemcpy(m.w, host, (size_t)(m.rb * rows), hipMemcpyHostToDevice) != hipSuccess;
+                } else {
+                    launch_synth_kquant(type, m.w, rows, k, tensor_key(seed, tid_layer(il, tid)),
+                                        (float)(stdv / (type == T_Q4_K ? 0.8 : 0.68)), s);
+                }
+            };
+            make(K.q, H ? H->tq : T_Q4_K, e->qw, c.n_embd, L_Q, se, H ? H->q : nullptr);
+            make(K.k, H ? H->tk : T_Q4_K, e->kvw, c.n_embd, L_K, se, H ? H->k : nullptr);
+            make(K.v, H ? H->tv : T_Q6_K, e->kvw, c.n_embd, L_V, se, H ? H->v : nullptr);
+            make(K.o, H ? H->to : T_Q4_K, c.n_embd, e->qw, L_O, 4.0 * sq, H ? H->o : nullptr);
+            make(K.gate, H ? H->tg : T_Q4_K, c.n_ff, c.n_embd, L_GATE, se, H ? H->gate : nullptr);
+            make(K.up, H ? H->tu : T_Q4_K, c.n_ff, c.n_embd, L_UP, se, H ? H->up : nullptr);
+            make(K.down, H ? H->td : T_Q6_K, c.n_embd, c.n_ff, L_DOWN, 4.0 * sf, H ? H->down : nullptr);
+            continue;
         }
         // this rank's rows [r0, r0 + n) of the fused [Wq | Wk | Wv]: the pieces of each source tensor
         const int64_t q0 = (int64_t)tp_rank * e->sh_qkv, qn = e->sh_qkv;
@@ -661,6 +772,11 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         GHIP_FATAL(hipMalloc(&e->h_da, (size_t)c.n_ff / 32 * 4));
     }
     GHIP_FATAL(hipMalloc(&e->logits, (size_t)c.n_vocab * 4));
+    if (kq_layers) {
+        const int64_t kmax = std::max<int64_t>(std::max<int64_t>(c.n_embd, e->qw), c.n_ff);
+        GHIP_FATAL(hipMalloc(&e->kq_x, (size_t)(kmax / 256 * 292)));
+        GHIP_FATAL(hipMalloc(&e->kq_g, (size_t)c.n_ff * 4));
+    }
     GHIP_FATAL(hipMalloc(&e->key, (size_t)e->grid_big * 8));  // per-workgroup argmax keys
     GHIP_FATAL(hipMalloc(&e->pos, 4));
     GHIP_FATAL(hipMalloc(&e->token, 4));
@@ -752,16 +868,44 @@ extern "C" gemma_engine *gemma_engine_create_from_gguf(const char *path, int n_c
         c.n_ff = (int)tg->ne[1];
         c.wtype = (int)tq->type;
         c.out_type = te->type == GGML_TYPE_Q6_K ? T_Q6_K : 0;
-        if ((c.wtype != T_Q4_0 && c.wtype != T_Q8_0) || (te->type != tq->type && te->type != GGML_TYPE_Q6_K))
-            err = "layer matrices must all be Q4_0 or all Q8_0, token_embd that type or Q6_K";
+        if (tq->type == GGML_TYPE_Q4_K || tq->type == GGML_TYPE_Q6_K) {  // K-quant layers (Q4_K_M files)
+            c.wtype = T_Q4_K;
+            if (te->type != GGML_TYPE_Q6_K) err = "K-quant layers need a Q6_K token_embd";
+        } else if ((c.wtype != T_Q4_0 && c.wtype != T_Q8_0) || (te->type != tq->type && te->type != GGML_TYPE_Q6_K)) {
+            err = "layer matrices must all be Q4_0 or all Q8_0 (or Q4_K / Q6_K), token_embd that type or Q6_K";
+        }
     }
-    hw.embd = tensor("token_embd.weight", c.out_type ? T_Q6_K : c.wtype, c.n_embd, c.n_vocab);
+    const bool kqm = c.wtype == T_Q4_K;
+    // K-quant layers: each matrix Q4_K or Q6_K; returns the data and records the type
+    auto ktensor = [&](const std::string &name, int64_t ne0, int64_t ne1, int &type) -> const void * {
+        const void *d = tensor(name, -1, ne0, ne1);
+        if (!d) return nullptr;
+        const int t = (int)ggml_get_tensor(w, name.c_str())->type;
+        if (t != T_Q4_K && t != T_Q6_K) {
+            err = "tensor " + name + ": K-quant layers must be Q4_K or Q6_K";
+            return nullptr;
+        }
+        type = t;
+        return d;
+    };
+    hw.embd = tensor("token_embd.weight", (c.out_type || kqm) ? T_Q6_K : c.wtype, c.n_embd, c.n_vocab);
     hw.out_norm = (const float *)tensor("output_norm.weight", GGML_TYPE_F32, c.n_embd, 1);
     for (int il = 0; il < c.n_layer && err.empty(); ++il) {
         const std::string b = "blk." + std::to_string(il) + ".";
         host_weights::layer L;
         L.attn_norm = (const float *)tensor(b + "attn_norm.weight", GGML_TYPE_F32, c.n_embd, 1);
         L.ffn_norm = (const float *)tensor(b + "ffn_norm.weight", GGML_TYPE_F32, c.n_embd, 1);
+        if (kqm) {
+            L.q = ktensor(b + "attn_q.weight", c.n_embd, qw, L.tq);
+            L.k = ktensor(b + "attn_k.weight", c.n_embd, kvw, L.tk);
+            L.v = ktensor(b + "attn_v.weight", c.n_embd, kvw, L.tv);
+            L.o = ktensor(b + "attn_output.weight", qw, c.n_embd, L.to);
+            L.gate = ktensor(b + "ffn_gate.weight", c.n_embd, c.n_ff, L.tg);
+            L.up = ktensor(b + "ffn_up.weight", c.n_embd, c.n_ff, L.tu);
+            L.down = ktensor(b + "ffn_down.weight", c.n_ff, c.n_embd, L.td);
+            hw.layers.push_back(L);
+            continue;
+        }
         L.q = tensor(b + "attn_q.weight", c.wtype, c.n_embd, qw);
         L.k = tensor(b + "attn_k.weight", c.wtype, c.n_embd, kvw);
         L.v = tensor(b + "attn_v.weight", c.wtype, c.n_embd, kvw);
@@ -833,6 +977,11 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (e->embd_q6k) (void)hipFree(e->embd_q6k);
+    for (kq_layer &K : e->kql)
+        for (kq_mat *m : {&K.q, &K.k, &K.v, &K.o, &K.gate, &K.up, &K.down})
+            if (m->w) (void)hipFree(m->w);
+    if (e->kq_x) (void)hipFree(e->kq_x);
+    if (e->kq_g) (void)hipFree(e->kq_g);
     for (hipEvent_t ev : e->ev_fork) (void)hipEventDestroy(ev);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     if (e->side) (void)hipStreamDestroy(e->side);
@@ -962,6 +1111,14 @@ extern "C" int64_t gemma_engine_tensor(gemma_engine *e, int tid, void *dst, int6
     const int il = (tid - 16) / 16, k = (tid - 16) % 16;
     if (tid < 16 || il >= c.n_layer) return -1;
     layer_dev &L = e->layers[il];
+    if (e->kq && k != L_ATTN_NORM && k != L_FFN_NORM) {  // raw K-quant rows
+        const kq_layer &K = e->kql[il];
+        const kq_mat *m = k == L_Q ? &K.q : k == L_K ? &K.k : k == L_V ? &K.v : k == L_O ? &K.o : k == L_GATE ? &K.gate
+                        : k == L_UP ? &K.up : k == L_DOWN ? &K.down : nullptr;
+        if (!m || cap < m->rb * m->rows) return -1;
+        GHIP_CHECK(hipMemcpy(dst, m->w, (size_t)(m->rb * m->rows), hipMemcpyDeviceToHost));
+        return m->rb * m->rows;
+    }
     switch (k) {
         case L_ATTN_NORM: return copy_f32(L.attn_norm, c.n_embd);
         case L_FFN_NORM: return copy_f32(L.ffn_norm, c.n_embd);
@@ -1033,6 +1190,10 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
             break;
     }
     };
+    if (e->kq) {
+        set_error("gemma_engine_time: K-quant layer engines time their matvecs with gemma_kq_time");
+        return -1.0;
+    }
     if (which == 4 && e->out_type == T_Q6_K) {
         set_error("gemma_engine_time: the logits kernel of a Q6_K output is the K-quant matvec (gemma_kq_time)");
         return -1.0;
@@ -1100,6 +1261,7 @@ static void drop_graph(gemma_engine *e) {
 
 extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
     set_error("");
+    if (e->kq) return 0;  // K-quant layers: no launch plan to measure
     (void)hipSetDevice(e->device);
     const gemma_hip_config &c = e->cfg;
     const int wt = c.wtype;
@@ -1342,6 +1504,10 @@ static int prefill_run(gemma_engine *e, bool exact, float *logits_last, float *l
     }
     if (e->tp_n > 1) {
         set_error("gemma_engine_prefill: the MFMA prefill is single-GPU (row-split engines prefill token by token)");
+        return -1;
+    }
+    if (e->kq) {
+        set_error("gemma_engine_prefill: K-quant layer engines prefill token by token (gemma_engine_step)");
         return -1;
     }
     if (prefill_alloc(e, T)) return -1;

@@ -93,6 +93,10 @@ struct kq_args {  // y[c][r] = vec_dot_{q4_K,q6_K}_q8_K(row r of w, column c of 
     float *y = nullptr;
     int64_t y_col_stride = 0;     // floats between output columns
     int ncols = 1;
+    // epilogue (engine K-quant layers): y = v + resid (ggml_add), or y = gelu(gate_in) * v (ffn_up)
+    const float *resid = nullptr, *gate_in = nullptr;
+    const uint16_t *gelu_tab = nullptr;
+    int gelu_clamp = 0;
 };
 int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s);
 // ggml quantize_row_q8_K of ncols rows of K floats (row stride ldx floats) -> Q8_K rows ld_out bytes apart

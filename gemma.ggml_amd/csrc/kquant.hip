@@ -106,7 +106,17 @@ template <int WT>
 __device__ __forceinline__ void kq_store(const kq_args &a, int col, int64_t row_raw, int l, float acc, float accm) {
     float v = fold8_dpp(acc);  // ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7)) in lane 0 of the 8-group
     if (WT == T_Q4_K) v = v + quad_fold_dpp(accm);  // (m0+m2)+(m1+m3) in lane 0
-    if (l == 0 && row_raw < a.rows) a.y[(int64_t)col * a.y_col_stride + row_raw] = v;
+    if (l == 0 && row_raw < a.rows) {
+        const int64_t o = (int64_t)col * a.y_col_stride + row_raw;
+        if (a.gate_in) {  // gelu(gate) then ggml_mul by up (src/gemma_model.cpp:444-452)
+            const float g = a.gate_in[o];
+            const float gl = (a.gelu_clamp && g <= -10.0f) ? 0.0f : (a.gelu_clamp && g >= 10.0f) ? g : h2f(a.gelu_tab[f2h(g)]);
+            v = gl * v;
+        } else if (a.resid) {
+            v = v + a.resid[o];
+        }
+        a.y[o] = v;
+    }
 }
 
 template <int WT>

@@ -101,3 +101,44 @@ def write_gguf_q6k(m, shape, path):
         T.write_gguf(m, shape, path, 0)
     finally:
         T.GGUFWriter.add_tensor = orig
+
+
+# ---- K-quant layers (llama.cpp Q4_K_M layout: Q4_K q/k/o/gate/up, Q6_K v/down/token_embd) ----------
+KSHAPE = dict(n_layer=2, n_embd=256, n_head=2, n_head_kv=1, head_dim=128, n_ff=512, n_vocab=1024)
+
+
+@gpu
+def test_kquant_engine_synthetic_matches_oracle():
+    m = O.Model(O.make_config(KSHAPE, n_ctx=128, kmix=1))
+    e = G.Engine(KSHAPE, n_ctx=128, wtype=G.GGML_TYPE_Q4_K)
+    for tid in [0, 1] + [16 + il * 16 + k for il in range(2) for k in range(9)]:
+        ref = m.tensor(tid)
+        assert np.array_equal(e.tensor(tid, ref.size), ref), tid
+    _compare(e, m, KSHAPE, 7, 16)
+    with pytest.raises(RuntimeError):  # batched prefill is not provided for K-quant layers
+        e.begin(O.make_prompt(5, KSHAPE["n_vocab"]))
+        e.prefill(5)
+    e.close()
+    m.close()
+
+
+@gpu
+def test_kquant_engine_gemma2b_layer_shapes():
+    shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
+    m = O.Model(O.make_config(shape, n_ctx=256, kmix=1))
+    e = G.Engine(shape, n_ctx=256, wtype=G.GGML_TYPE_Q4_K)
+    _compare(e, m, shape, 13, 6)
+    e.close()
+    m.close()
+
+
+@gpu
+def test_kquant_engine_from_gguf(tmp_path):
+    m = O.Model(O.make_config(KSHAPE, n_ctx=128, kmix=1))
+    path = tmp_path / "k.gguf"
+    write_gguf(m, KSHAPE, path, 1)
+    e = G.Engine.from_gguf(str(path), n_ctx=128)
+    assert e.cfg.wtype == G.GGML_TYPE_Q4_K
+    _compare(e, m, KSHAPE, 9, 12)
+    e.close()
+    m.close()
