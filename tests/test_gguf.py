@@ -176,9 +176,23 @@ def test_engine_from_gguf_rejects_unsupported_layouts(tmp_path):
     """The engine's GGUF loader validates before touching the GPU (runs on the CPU)."""
     import ctypes as C
     L = G.lib()
-    p = _model_file(tmp_path, kmix=1)  # Q4_K / Q6_K layer matrices: the ggml-API path, not the engine
+    # a Q5_K layer matrix (Q4_K_M files never hold one; Q5_K_M files do): rejected with a message
+    E, V, F = 256, 512, 512
+    w = GGUFWriter()
+    for k, v in (("block_count", 1), ("embedding_length", E), ("attention.head_count", 2),
+                 ("attention.head_count_kv", 1), ("attention.key_length", 128)):
+        w.add("gemma." + k, U32, v)
+    w.add_tensor("token_embd.weight", 14, [E, V], np.zeros(V * E // 256 * 210, np.uint8))
+    w.add_tensor("output_norm.weight", 0, [E], np.ones(E, np.float32))
+    GGUF_BLOCK_Q5_K = (13, 176)
+    import gguf_writer
+    gguf_writer.GGML_BLOCK.setdefault(13, (176, 256))
+    w.add_tensor("blk.0.attn_q.weight", GGUF_BLOCK_Q5_K[0], [E, 256], np.zeros(256 * E // 256 * 176, np.uint8))
+    w.add_tensor("blk.0.ffn_gate.weight", 12, [E, F], np.zeros(F * E // 256 * 144, np.uint8))
+    p = str(tmp_path / "q5k.gguf")
+    w.write(p)
     assert not L.gemma_engine_create_from_gguf(p.encode(), 64, 0)
-    assert "Q4_0 or all Q8_0" in G.last_error()
+    assert "Q4_K" in G.last_error(), G.last_error()
     bad = str(tmp_path / "bad.gguf")
     w = GGUFWriter()
     w.add("gemma.block_count", U32, 1)
