@@ -495,9 +495,14 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         const layer_dev &L = e->layers[il];
         const kq_layer &K = e->kql[il];
         if (launch_norm_q8K(e->x, E, L.attn_norm, E, c.eps, 1, e->kq_x, (E / 256) * 292, s)) return -1;
-        if (mv(K.q, e->qkv, nullptr, nullptr) || mv(K.k, e->qkv + e->qw, nullptr, nullptr) ||
-            mv(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr))
+        if (K.k.w == K.q.w + K.q.rb * K.q.rows) {  // q|k in one allocation: one launch for both
+            kq_mat qk = K.q;
+            qk.rows = K.q.rows + K.k.rows;
+            if (mv(qk, e->qkv, nullptr, nullptr)) return -1;
+        } else if (mv(K.q, e->qkv, nullptr, nullptr) || mv(K.k, e->qkv + e->qw, nullptr, nullptr)) {
             return -1;
+        }
+        if (mv(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr)) return -1;
         attn_args t;
         t.qkv = e->qkv;
         t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
@@ -659,12 +664,24 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
             if (e->kql.empty()) e->kql.resize(c.n_layer);
             kq_layer &K = e->kql[il];
             const host_weights::layer *H = hw ? &hw->layers[il] : nullptr;
+            // q and k of one type share one allocation (k's rows right after q's): one launch for q|k
+            const int tq = H ? H->tq : T_Q4_K, tk = H ? H->tk : T_Q4_K;
+            uint8_t *qk_buf = nullptr;
+            if (tq == tk) {
+                const int64_t rb = c.n_embd / 256 * (tq == T_Q4_K ? 144 : 210);
+                if (hipMalloc(&qk_buf, (size_t)(rb * (e->qw + e->kvw))) != hipSuccess) {
+                    set_error("gemma_engine_create: weight alloc failed");
+                    up_fail = true;
+                }
+            }
             auto make = [&](kq_mat &m, int type, int64_t rows, int64_t k, int tid, double stdv, const void *host) {
                 m.type = type;
                 m.rows = rows;
                 m.K = k;
                 m.rb = k / 256 * (type == T_Q4_K ? 144 : 210);
-                if (hipMalloc(&m.w, (size_t)(m.rb * rows)) != hipSuccess) {
+                if (qk_buf && (&m == &K.q || &m == &K.k)) {
+                    m.w = qk_buf + (&m == &K.k ? m.rb * e->qw : 0);
+                } else if (hipMalloc(&m.w, (size_t)(m.rb * rows)) != hipSuccess) {
                     set_error("gemma_engine_create: weight alloc failed");
                     up_fail = true;
                     return;
@@ -979,7 +996,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     if (e->embd_q6k) (void)hipFree(e->embd_q6k);
     for (kq_layer &K : e->kql)
         for (kq_mat *m : {&K.q, &K.k, &K.v, &K.o, &K.gate, &K.up, &K.down})
-            if (m->w) (void)hipFree(m->w);
+            if (m->w && !(m == &K.k && K.q.w && K.k.w == K.q.w + K.q.rb * K.q.rows)) (void)hipFree(m->w);  // k inside q|k
     if (e->kq_x) (void)hipFree(e->kq_x);
     if (e->kq_g) (void)hipFree(e->kq_g);
     for (hipEvent_t ev : e->ev_fork) (void)hipEventDestroy(ev);

@@ -31,20 +31,43 @@ __device__ __forceinline__ uint32_t ld_u32_a2(const uint8_t *p) {
 // d = y.d*f16(x.d); Q4_K also the mins lane k = l & 3 (meaningful in lanes 0..3): prod and dmin
 struct kq_term { int sumi; float d; int prod; float dmin; };
 
+// a super-block's weight bytes for AVX2 lane l, loaded ahead of the arithmetic (kq_terms)
+template <int WT> struct kq_raw;
+template <> struct kq_raw<T_Q4_K> { uint4 h; uint32_t q[4]; };
+template <> struct kq_raw<T_Q6_K> { uint32_t qla[2], qlb[2], qh[2], sc[4]; uint32_t d; };
+
 template <int WT>
-__device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *xs, int s, int l) {
+__device__ __forceinline__ kq_raw<WT> kq_load(const uint8_t *wrow, int s, int l) {
+    kq_raw<WT> r;
+    if constexpr (WT == T_Q4_K) {
+        const uint8_t *blk = wrow + (int64_t)s * 144;
+        r.h = *(const uint4 *)blk;  // d, dmin, scales[12]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r.q[j] = *(const uint32_t *)(blk + 16 + 32 * j + 4 * l);
+    } else {
+        const uint8_t *blk = wrow + (int64_t)s * 210;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            r.qla[j] = ld_u32_a2(blk + 64 * j + 4 * l);
+            r.qlb[j] = ld_u32_a2(blk + 64 * j + 32 + 4 * l);
+            r.qh[j] = ld_u32_a2(blk + 128 + 32 * j + 4 * l);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r.sc[k] = ld_u32_a2(blk + 192 + 4 * k);
+        r.d = *(const uint16_t *)(blk + 208);
+    }
+    return r;
+}
+
+template <int WT>
+__device__ __forceinline__ kq_term kq_terms(const kq_raw<WT> &r, const uint8_t *xs, int s, int l) {
     kq_term t;
     const uint8_t *xb = xs + s * 292;
     const float yd = *(const float *)xb;
     const int8_t *q8 = (const int8_t *)(xb + 4);
-    if (WT == T_Q4_K) {
-        const uint8_t *blk = wrow + (int64_t)s * 144;
-        const uint4 h = *(const uint4 *)blk;  // d, dmin, scales[12]
-        uint32_t q[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = *(const uint32_t *)(blk + 16 + 32 * j + 4 * l);
+    if constexpr (WT == T_Q4_K) {
         // six-bit scales / mins (src/kernals.cl:79-84)
-        const uint32_t u0 = h.y, u1 = h.z, u2 = h.w;
+        const uint32_t u0 = r.h.y, u1 = r.h.z, u2 = r.h.w;
         const uint32_t s03 = u0 & 0x3f3f3f3fu;                                      // sc 0..3
         const uint32_t s47 = (u2 & 0x0f0f0f0fu) | (((u0 >> 6) & 0x03030303u) << 4);  // sc 4..7
         const uint32_t m03 = u1 & 0x3f3f3f3fu;                                      // mins 0..3
@@ -56,11 +79,11 @@ __device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *
             const int sc_lo = (scw >> (16 * (j & 1))) & 0xFF, sc_hi = (scw >> (16 * (j & 1) + 8)) & 0xFF;
             const uint32_t alo = *(const uint32_t *)(q8 + 64 * j + 4 * l);
             const uint32_t ahi = *(const uint32_t *)(q8 + 64 * j + 32 + 4 * l);
-            sumi += sc_lo * sdot4k(q[j] & 0x0F0F0F0Fu, alo) + sc_hi * sdot4k((q[j] >> 4) & 0x0F0F0F0Fu, ahi);
+            sumi += sc_lo * sdot4k(r.q[j] & 0x0F0F0F0Fu, alo) + sc_hi * sdot4k((r.q[j] >> 4) & 0x0F0F0F0Fu, ahi);
         }
         t.sumi = sumi;
-        t.d = yd * pin(h2f(h.x));
-        t.dmin = -yd * pin(h2f(h.x >> 16));
+        t.d = yd * pin(h2f(r.h.x));
+        t.dmin = -yd * pin(h2f(r.h.x >> 16));
         const int16_t *bs = (const int16_t *)(xb + 260);
         const int k = l & 3;
         const int S0 = (int)bs[4 * k] + (int)bs[4 * k + 1], S1 = (int)bs[4 * k + 2] + (int)bs[4 * k + 3];
@@ -68,13 +91,10 @@ __device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *
         const int mn0 = (mw >> (16 * (k & 1))) & 0xFF, mn1 = (mw >> (16 * (k & 1) + 8)) & 0xFF;
         t.prod = mn0 * S0 + mn1 * S1;
     } else {
-        const uint8_t *blk = wrow + (int64_t)s * 210;
         int sumi = 0;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const uint32_t qla = ld_u32_a2(blk + 64 * j + 4 * l);
-            const uint32_t qlb = ld_u32_a2(blk + 64 * j + 32 + 4 * l);
-            const uint32_t qh = ld_u32_a2(blk + 128 + 32 * j + 4 * l);
+            const uint32_t qla = r.qla[j], qlb = r.qlb[j], qh = r.qh[j];
             const uint32_t q6[4] = {(qla & 0x0F0F0F0Fu) | ((qh & 0x03030303u) << 4),
                                     (qlb & 0x0F0F0F0Fu) | (((qh >> 2) & 0x03030303u) << 4),
                                     ((qla >> 4) & 0x0F0F0F0Fu) | (((qh >> 4) & 0x03030303u) << 4),
@@ -83,17 +103,30 @@ __device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *
             for (int i = 0; i < 4; ++i) {
                 const uint32_t av = *(const uint32_t *)(q8 + 128 * j + 32 * i + 4 * l);
                 const int p = sdot4k(q6[i], av) - sdot4k(0x20202020u, av);
-                const int sc = (int)(int8_t)blk[192 + 8 * j + 2 * i + (l >> 2)];
+                const int bi = 8 * j + 2 * i + (l >> 2);  // scale byte 192 + bi
+                const int sc = (int)(int8_t)(uint8_t)(r.sc[bi >> 2] >> (8 * (bi & 3)));
                 sumi += sc * p;
             }
         }
         t.sumi = sumi;
-        t.d = yd * pin(h2f(*(const uint16_t *)(blk + 208)));
+        t.d = yd * pin(h2f(r.d));
         t.prod = 0;
         t.dmin = 0.0f;
     }
     return t;
 }
+
+template <int WT>
+__device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *xs, int s, int l) {
+    return kq_terms<WT>(kq_load<WT>(wrow, s, l), xs, s, l);
+}
+
+// KQ_PF super-blocks' weight loads are issued before any of their arithmetic (one memory round trip
+// per group instead of one per super-block)
+#ifndef GHIP_KQ_PF
+#define GHIP_KQ_PF 4
+#endif
+constexpr int KQ_PF = GHIP_KQ_PF;
 
 __device__ __forceinline__ void stage_q8k(const kq_args &a, uint8_t *xs, int col, int tid, int nth) {
     const uint32_t *src = (const uint32_t *)(a.x + (int64_t)col * a.x_col_stride);
@@ -132,10 +165,17 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
         const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;  // all lanes stay active for the folds
         const uint8_t *wrow = a.w + row * a.row_bytes;
         float acc = 0.0f, accm = 0.0f;
-        for (int s = 0; s < a.nsb; ++s) {
-            const kq_term t = kq_block<WT>(wrow, xs, s, l);
-            acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
-            if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
+        for (int s0 = 0; s0 < a.nsb; s0 += KQ_PF) {
+            kq_raw<WT> r[KQ_PF];
+#pragma unroll
+            for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
+#pragma unroll
+            for (int p = 0; p < KQ_PF; ++p) {
+                if (s0 + p >= a.nsb) break;
+                const kq_term t = kq_terms<WT>(r[p], xs, s0 + p, l);
+                acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
+                if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
+            }
         }
         kq_store<WT>(a, col, row_raw, l, acc, accm);
     }
@@ -160,8 +200,15 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
     const uint8_t *wrow = a.w + row * a.row_bytes;
     float acc = 0.0f, accm = 0.0f;
-    for (int s = wave * seg; s < (wave + 1) * seg; ++s) {
-        const kq_term t = kq_block<WT>(wrow, xs, s, l);
+    for (int s0 = wave * seg; s0 < (wave + 1) * seg; s0 += KQ_PF) {
+    kq_raw<WT> r[KQ_PF];
+#pragma unroll
+    for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < (wave + 1) * seg ? s0 + p : s0, l);
+#pragma unroll
+    for (int p = 0; p < KQ_PF; ++p) {
+        const int s = s0 + p;
+        if (s >= (wave + 1) * seg) break;
+        const kq_term t = kq_terms<WT>(r[p], xs, s, l);
         if (wave == 0) {
             acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
             if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
@@ -173,6 +220,7 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
                 if (l == 0) st_m[s * 8 + rr] = t.dmin;
             }
         }
+    }
     }
     __syncthreads();
     if (wave != 0) return;
