@@ -49,7 +49,7 @@ struct mv_args {
     uint32_t *out_act = nullptr;                   // EPI_GELU_MUL: also write y's Q8_0 image (the
     float *out_da = nullptr;                       //   next matvec's PRO_IMG input), blocks of y
     int ncols = 1;
-    int ablate = 0;  // timing-only ablations (bench): 1 = no prologue, 4 = no carry
+    int ablate = 0;  // timing-only ablations (bench): 1 = no prologue, 4 = no carry, 8 = no gate/up dots
     unsigned long long *dbg_t = nullptr;  // diagnostics: 8 s_memrealtime stamps per workgroup
     // launch geometry precomputed by launch_t (no 64-bit divisions in the kernel prologue):
     // a wave's row-tile count is rt_q + (rt0 < rt_r); ygroups = EPI_GELU_MUL image groups per WG

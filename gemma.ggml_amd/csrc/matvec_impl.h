@@ -694,6 +694,9 @@ __device__ __forceinline__ float carry_chain(const void *st_s, const float *st_d
     return carry_run<2, false>(ps, pd, total, acc);
 }
 
+#ifndef GHIP_NOSCALE
+#define GHIP_NOSCALE 0
+#endif
 #ifndef GHIP_HOSTDIV
 #define GHIP_HOSTDIV 1  // 1: the wave's item count from launch_t's precomputed quotient (no 64-bit division)
 #endif
@@ -755,12 +758,17 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
         // weights are read once per token by one CU: non-temporal loads (MI355X_MICROARCH nt-weights:
         // issued -> landed -18 %, decode layer -5..10 %)
         qd = ld_nt16(qt + q_off);
+#if GHIP_NOSCALE  // timing only: no scale loads (wrong results)
+        sd = make_uint4(0x3c003c00u, 0x3c003c00u, 0x3c003c00u, 0x3c003c00u);
+        (void)st;
+#else
         if (WT == T_Q4_0) {
             sd = ld_nt16(st + s_off);
         } else {
             const uint2 v = ld_nt8(st + s_off);
             sd = make_uint4(v.x, v.y, 0, 0);
         }
+#endif
         ++issued;
         if (issued < n_items) {
             if (NM == 2) {  // gate and up of one block tile back to back (shared act operands)
@@ -818,9 +826,13 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
                 issue(qb[u], sb[u]);
                 issue(qb[u + 1], sb[u + 1]);
                 if (k + u < n_items) {
-                    const act_tile<WT> at = load_act<WT, NSA>(smem, m, cc.bt, l);
-                    acc = tile_dot_a<WT>(q0, s0, at, acc);
-                    acc2 = tile_dot_a<WT>(q1, s1, at, acc2);
+                    if (a.ablate & 8) {  // timing only: the loads without the dot products
+                        acc += __builtin_bit_cast(float, q0.x ^ s0.x ^ q1.y ^ s1.y);
+                    } else {
+                        const act_tile<WT> at = load_act<WT, NSA>(smem, m, cc.bt, l);
+                        acc = tile_dot_a<WT>(q0, s0, at, acc);
+                        acc2 = tile_dot_a<WT>(q1, s1, at, acc2);
+                    }
                     if (cc.bt + 1 == nbt) {
                         const float vg = fold8(acc), vu = fold8(acc2);
                         acc = 0.0f;

@@ -17,7 +17,7 @@ for k in (0, 1, 2, 3, 4):
     out[k] = round(us, 2)
 print(json.dumps(out))
 '''
-for ab in (0, 1, 2, 4, 3, 7):
+for ab in (0, 1, 8, 9, 4):
     env = dict(os.environ, GHIP_ABLATE=str(ab))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
     print("ablate", ab, r.stdout.strip(), r.stderr.strip()[-300:] if r.returncode else "", flush=True)
