@@ -127,6 +127,9 @@ __device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *
 #define GHIP_KQ_PF 4
 #endif
 constexpr int KQ_PF = GHIP_KQ_PF;
+#ifndef GHIP_KQ_EARLY
+#define GHIP_KQ_EARLY 1  // 1: first weight round issued before the Q8_K staging
+#endif
 
 __device__ __forceinline__ void stage_q8k(const kq_args &a, uint8_t *xs, int col, int tid, int nth) {
     const uint32_t *src = (const uint32_t *)(a.x + (int64_t)col * a.x_col_stride);
@@ -157,18 +160,36 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];  // the column's Q8_K blocks
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
     const int col = blockIdx.y;
+    const int64_t n_groups = (a.rows + 7) / 8;
+    const int64_t g0 = (int64_t)blockIdx.x * (KQ_THREADS / 64) + wave;
+    // the first round of weight loads goes out before the Q8_K staging, so its HBM round trip
+    // overlaps the activation copy into LDS (the Q4_0 matvec's ring-before-prologue)
+    kq_raw<WT> r[KQ_PF];
+#if GHIP_KQ_EARLY
+    {
+        const int64_t row0 = g0 * 8 + rr < a.rows ? g0 * 8 + rr : a.rows - 1;
+#pragma unroll
+        for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(a.w + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
+    }
+    bool early = true;
+#else
+    constexpr bool early = false;
+#endif
     stage_q8k(a, xs, col, tid, KQ_THREADS);
     __syncthreads();
-    const int64_t n_groups = (a.rows + 7) / 8;
-    for (int64_t g = (int64_t)blockIdx.x * (KQ_THREADS / 64) + wave; g < n_groups; g += (int64_t)gridDim.x * (KQ_THREADS / 64)) {
+    for (int64_t g = g0; g < n_groups; g += (int64_t)gridDim.x * (KQ_THREADS / 64)) {
         const int64_t row_raw = g * 8 + rr;
         const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;  // all lanes stay active for the folds
         const uint8_t *wrow = a.w + row * a.row_bytes;
         float acc = 0.0f, accm = 0.0f;
         for (int s0 = 0; s0 < a.nsb; s0 += KQ_PF) {
-            kq_raw<WT> r[KQ_PF];
+            if (!early) {
 #pragma unroll
-            for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
+                for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
+            }
+#if GHIP_KQ_EARLY
+            early = false;
+#endif
 #pragma unroll
             for (int p = 0; p < KQ_PF; ++p) {
                 if (s0 + p >= a.nsb) break;
@@ -194,16 +215,29 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     float *st_d = (float *)(st_i + nsb * 64);   // [nsb][8]  per-row d
     int *st_p = (int *)(st_d + nsb * 8);        // [nsb][64] mins products (Q4_K)
     float *st_m = (float *)(st_p + nsb * 64);   // [nsb][8]  per-row dmin (Q4_K)
-    stage_q8k(a, xs, col, tid, 64 * KS);
-    __syncthreads();
     const int64_t row_raw = (int64_t)blockIdx.x * 8 + rr;
     const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
     const uint8_t *wrow = a.w + row * a.row_bytes;
+    // first round of weight loads before the Q8_K staging (as in k_matvec_kq)
+    kq_raw<WT> r[KQ_PF];
+#if GHIP_KQ_EARLY
+#pragma unroll
+    for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, p < seg ? wave * seg + p : wave * seg, l);
+    bool early = true;
+#else
+    constexpr bool early = false;
+#endif
+    stage_q8k(a, xs, col, tid, 64 * KS);
+    __syncthreads();
     float acc = 0.0f, accm = 0.0f;
     for (int s0 = wave * seg; s0 < (wave + 1) * seg; s0 += KQ_PF) {
-    kq_raw<WT> r[KQ_PF];
+    if (!early) {
 #pragma unroll
-    for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < (wave + 1) * seg ? s0 + p : s0, l);
+        for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < (wave + 1) * seg ? s0 + p : s0, l);
+    }
+#if GHIP_KQ_EARLY
+    early = false;
+#endif
 #pragma unroll
     for (int p = 0; p < KQ_PF; ++p) {
         const int s = s0 + p;
