@@ -169,6 +169,45 @@ extern "C" void hpc_set_error_mode(int exit_on_error) { st().exit_on_error = exi
 
 extern "C" int hpc_weight_cache_entries(void) { return (int)(st().weights.size() + st().raw_weights.size()); }
 
+// drops every cached device copy of the host weight at `host` (any type/shape); returns how many.
+// The cache is keyed by the host pointer: a caller that frees or rewrites a src0 buffer calls this
+// first, or a later buffer at the same address would be served the stale device copy.
+extern "C" int hpc_unregister_weight(const void *host) {
+    hpc_state &s = st();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (s.inited) (void)hipStreamSynchronize(s.stream);  // no launch may still read a freed copy
+    int n = 0;
+    for (auto it = s.weights.begin(); it != s.weights.end();) {
+        if (it->first.host == host) {
+            free_tiled(it->second);
+            it = s.weights.erase(it);
+            ++n;
+        } else {
+            ++it;
+        }
+    }
+    for (auto it = s.raw_weights.begin(); it != s.raw_weights.end();) {
+        if (it->first.host == host) {
+            (void)hipFree(it->second);
+            it = s.raw_weights.erase(it);
+            ++n;
+        } else {
+            ++it;
+        }
+    }
+    return n;
+}
+
+extern "C" void hpc_flush_weights(void) {
+    hpc_state &s = st();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (s.inited) (void)hipStreamSynchronize(s.stream);
+    for (auto &kv : s.weights) free_tiled(kv.second);
+    s.weights.clear();
+    for (auto &kv : s.raw_weights) (void)hipFree(kv.second);
+    s.raw_weights.clear();
+}
+
 extern "C" void hpc_set_matvec_ks(int ks) { st().ks = ks > 0 ? ks : 1; }
 
 extern "C" int hpc_register_weight(const void *host, int type, int64_t ne00, int64_t ne01, size_t nb01) {

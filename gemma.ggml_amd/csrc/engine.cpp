@@ -156,6 +156,7 @@ struct kq_mat {
 };
 struct kq_layer {
     kq_mat q, k, v, o, gate, up, down;
+    bool qk_fused = false;  // q and k share one allocation (k's rows right after q's, same type)
 };
 
 struct gemma_engine;
@@ -495,7 +496,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         const layer_dev &L = e->layers[il];
         const kq_layer &K = e->kql[il];
         if (launch_norm_q8K(e->x, E, L.attn_norm, E, c.eps, 1, e->kq_x, (E / 256) * 292, s)) return -1;
-        if (K.k.w == K.q.w + K.q.rb * K.q.rows) {  // q|k in one allocation: one launch for both
+        if (K.qk_fused) {  // q|k in one allocation (same type): one launch for both
             kq_mat qk = K.q;
             qk.rows = K.q.rows + K.k.rows;
             if (mv(qk, e->qkv, nullptr, nullptr)) return -1;
@@ -695,6 +696,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
             };
             make(K.q, H ? H->tq : T_Q4_K, e->qw, c.n_embd, L_Q, se, H ? H->q : nullptr);
             make(K.k, H ? H->tk : T_Q4_K, e->kvw, c.n_embd, L_K, se, H ? H->k : nullptr);
+            K.qk_fused = qk_buf != nullptr;
             make(K.v, H ? H->tv : T_Q6_K, e->kvw, c.n_embd, L_V, se, H ? H->v : nullptr);
             make(K.o, H ? H->to : T_Q4_K, c.n_embd, e->qw, L_O, 4.0 * sq, H ? H->o : nullptr);
             make(K.gate, H ? H->tg : T_Q4_K, c.n_ff, c.n_embd, L_GATE, se, H ? H->gate : nullptr);
@@ -996,7 +998,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     if (e->embd_q6k) (void)hipFree(e->embd_q6k);
     for (kq_layer &K : e->kql)
         for (kq_mat *m : {&K.q, &K.k, &K.v, &K.o, &K.gate, &K.up, &K.down})
-            if (m->w && !(m == &K.k && K.q.w && K.k.w == K.q.w + K.q.rb * K.q.rows)) (void)hipFree(m->w);  // k inside q|k
+            if (m->w && !(m == &K.k && K.qk_fused)) (void)hipFree(m->w);  // k lives inside q's q|k buffer
     if (e->kq_x) (void)hipFree(e->kq_x);
     if (e->kq_g) (void)hipFree(e->kq_g);
     for (hipEvent_t ev : e->ev_fork) (void)hipEventDestroy(ev);
@@ -1014,6 +1016,11 @@ extern "C" int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_
         set_error("gemma_engine_begin: prompt length out of range");
         return -1;
     }
+    for (int i = 0; i < n_prompt; ++i)  // the embedding kernels index token_embd rows unchecked
+        if (prompt[i] < 0 || prompt[i] >= c.n_vocab) {
+            set_error("gemma_engine_begin: token id " + std::to_string(prompt[i]) + " out of range [0, n_vocab)");
+            return -1;
+        }
     (void)hipSetDevice(e->device);
     hipStream_t s = e->stream;
     const size_t kv_bytes = (size_t)c.n_layer * c.n_ctx * e->kvw * 2;
@@ -1058,6 +1065,7 @@ extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_
         set_error("gemma_engine_step: context full");
         return -1;
     }
+    if (n <= 0) return 0;  // nothing to run (no warm-up step, no logits written)
     if (use_graph && !e->graph_exec) {
         // first eager step sets the kernels' LDS attributes before capture
         if (enqueue_step(e)) return -1;

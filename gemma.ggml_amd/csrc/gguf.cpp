@@ -118,9 +118,12 @@ bool read_kv(reader &r, gguf_kv &kv) {
     return r.bytes(kv.data.data(), es);
 }
 
+// SIZE_MAX when the byte count does not fit (a malformed file's dimensions)
 size_t tensor_bytes(const gguf_tensor_info &ti) {
-    size_t n = ggml_impl::type_size(ti.type) * (size_t)(ti.ne[0] / ggml_impl::blck_size(ti.type));
-    for (int i = 1; i < GGML_MAX_DIMS; ++i) n *= (size_t)ti.ne[i];
+    size_t n = ggml_impl::type_size(ti.type);
+    if (__builtin_mul_overflow(n, (size_t)(ti.ne[0] / ggml_impl::blck_size(ti.type)), &n)) return SIZE_MAX;
+    for (int i = 1; i < GGML_MAX_DIMS; ++i)
+        if (__builtin_mul_overflow(n, (size_t)ti.ne[i], &n)) return SIZE_MAX;
     return n;
 }
 
@@ -206,9 +209,11 @@ struct gguf_context *gguf_init_from_file(const char *fname, struct gguf_init_par
     size_t data_bytes = 0;
     for (const gguf_tensor_info &ti : g->infos) {
         if (ti.offset % g->alignment) return bail("tensor " + ti.name + ": offset not aligned");
-        const size_t end = ti.offset + tensor_bytes(ti);
-        if (end > r.size || g->data_offset + end > r.size)
+        // compared by subtraction: offset + bytes must not wrap for an offset near UINT64_MAX
+        const size_t nbytes = tensor_bytes(ti), avail = r.size > g->data_offset ? r.size - g->data_offset : 0;
+        if (ti.offset > avail || nbytes > avail - ti.offset)
             return bail("tensor " + ti.name + ": data past the end of file");
+        const size_t end = ti.offset + nbytes;
         data_bytes = std::max(data_bytes, end);
     }
     if (params.ctx) {

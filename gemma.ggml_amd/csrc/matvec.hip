@@ -20,8 +20,15 @@ int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int gri
         set_error("matvec: grid_x <= 0");
         return -1;
     }
-    if (a.nb % 1 || (pro != PRO_Q8 && (a.nb * 32) % 8)) {
-        set_error("matvec: K must be a multiple of 32");
+    // the tiled weight image: n_bt block tiles of BT blocks cover the nb = K/32 blocks, the padded
+    // tail (< BT blocks) is zero-filled in the activation image
+    const int64_t bt = wtype == T_Q4_0 ? wfmt<T_Q4_0>::BT : wfmt<T_Q8_0>::BT;
+    if (a.nb <= 0 || a.n_bt != (a.nb + bt - 1) / bt || a.n_rt != (a.rows + 7) / 8 || a.ncols <= 0) {
+        set_error("matvec: shape mismatch (n_bt must be ceil(K/32 / BT), n_rt ceil(rows / 8), ncols > 0)");
+        return -1;
+    }
+    if (wtype != T_Q4_0 && wtype != T_Q8_0) {
+        set_error("matvec: weight type must be Q4_0 or Q8_0");
         return -1;
     }
     int r = -1;

@@ -26,8 +26,10 @@ extern "C" {
  * GGML_TYPE_Q6_K (wdata = block_q8_K rows; ggml's AVX2 K-quant lane order) or GGML_TYPE_F16
  * (wdata = fp16 rows).  `vec_dot` is accepted for link compatibility and not called.
  * Quantized src0 is uploaded + re-tiled once and cached by (src0->data, shape) — weights are
- * immutable for the program's lifetime (src/gemma_model.cpp:24-27); F16 src0 (KV-cache views)
- * is uploaded on every call.  Errors: no return value (as the reference); the message is kept
+ * immutable for the program's lifetime (src/gemma_model.cpp:24-27).  CONTRACT: a caller that
+ * frees or rewrites a quantized src0 buffer calls hpc_unregister_weight(ptr) (or
+ * hpc_flush_weights()) first; otherwise a later buffer at the same address gets the stale copy.
+ * F16 src0 (KV-cache views) is uploaded on every call.  Errors: no return value (as the reference); the message is kept
  * for hpc_last_error() and, unless hpc_set_error_mode(0), the process exits(1) like
  * src/hpc.cpp:163-166 / src/opencl.cpp:13-17.                                                   */
 void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, int64_t ne1, int64_t nb1, int64_t nb2,
@@ -42,6 +44,8 @@ int hpc_register_weight(const void *host, int type, int64_t ne00, int64_t ne01, 
 int hpc_last_error(char *buf, size_t len);/* length of the last error message (0 = none)          */
 void hpc_set_error_mode(int exit_on_error);
 int hpc_weight_cache_entries(void);
+int hpc_unregister_weight(const void *host); /* drop the cached device copies of `host`; returns the count */
+void hpc_flush_weights(void);                /* drop every cached device weight                          */
 void hpc_set_matvec_ks(int ks);          /* K-split of the quantized matvec (1/2/4/8; tests) */
 
 /* ---- graph executor (SURVEY §8(b) `hpc_graph_compute(ggml_cgraph*)`): runs a graph built with the

@@ -136,6 +136,10 @@ def test_bad_tensor_infos(tmp_path):
     _expect_error(one(2, (33,), b"\0" * 18), "block size")
     _expect_error(one(0, (4,), b"\0" * 16, offsets=[8]), "not aligned")
     _expect_error(one(0, (1 << 30,), b"\0" * 16), "past the end")
+    # an offset near UINT64_MAX (aligned): offset + bytes wraps; must still be rejected
+    _expect_error(one(0, (4,), b"\0" * 16, offsets=[(1 << 64) - 32]), "past the end")
+    # dimensions whose byte count overflows size_t
+    _expect_error(one(0, (1 << 40, 1 << 40, 1 << 40), b"\0" * 16), "too many elements")
     w = GGUFWriter()
     w.add("dup", U32, 1)
     w.add("dup", U32, 2)
