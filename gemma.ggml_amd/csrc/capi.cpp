@@ -260,7 +260,8 @@ extern "C" void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, 
         a.y = dev_dst; a.y_col_stride = ne01;
         a.ncols = (int)col_num;
         int ks = s.ks;
-        while (ks > 1 && (W->n_bt % ks || matvec_lds_bytes(type, ks, W->n_bt, W->n_bt / ks) > 160 * 1024)) ks >>= 1;
+        if (ks == KS_RR && !matvec_rr_supported(type, W->n_bt)) ks = 8;
+        while (ks > 1 && ks != KS_RR && (W->n_bt % ks || matvec_lds_bytes(type, ks, W->n_bt, W->n_bt / ks) > 160 * 1024)) ks >>= 1;
         const int grid = ks > 1 ? (int)std::min<int64_t>(W->n_rt, 1024) : (int)std::min<int64_t>((W->n_rt + 3) / 4, 1024);
         if (launch_matvec(type, ks, PRO_Q8, EPI_STORE, a, grid, s.stream)) return fail(last_error());
     } else if (type == T_Q4_K || type == T_Q6_K) {

@@ -222,7 +222,7 @@ struct gemma_engine {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     // launch geometry: one plan per matrix class (defaults below; gemma_engine_tune measures)
-    int ks_small = 4, ks_down = 8;
+    int ks_small = KS_RR, ks_down = KS_RR;  // round-pipelined form where the shape allows (pick_ks falls back)
     int grid_big = 2048;
     launch_plan plan[MC_N];
     // prefill scratch (lazily allocated)
@@ -263,6 +263,7 @@ static int mv_grid(const gemma_engine *e, int cls, int64_t n_rt) {
 // largest power-of-two K split <= target that divides the block-tile count and whose LDS image
 // (activation + carry stash) fits the 160 KiB of a CU (Gemma-7B's down, K = 24576, steps to KS 1)
 static int pick_ks(int wtype, int64_t n_bt, int target) {
+    if (target == KS_RR) return matvec_rr_supported(wtype, n_bt) ? KS_RR : pick_ks(wtype, n_bt, 8);
     int ks = target;
     while (ks > 1 && (n_bt % ks || matvec_lds_bytes(wtype, ks, n_bt, n_bt / ks) > 160 * 1024)) ks >>= 1;
     return ks;
@@ -1329,6 +1330,8 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
             const int rmax = cls == MC_LOGITS ? 16 : ks == 1 ? 2 : 4;
             for (int rpw = 1; rpw <= rmax; rpw *= 2) cands.push_back({ks, rpw, e->plan[cls].img});
         }
+        // the round-pipelined form (one workgroup per row tile)
+        if (splits && cls != MC_GU && pick_ks(wt, nbt[cls], KS_RR) == KS_RR) cands.push_back({KS_RR, 1, e->plan[cls].img});
         const launch_plan keep = e->plan[cls];
         launch_plan win = keep;
         for (const launch_plan &p : cands) {

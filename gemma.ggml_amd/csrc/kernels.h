@@ -57,7 +57,11 @@ struct mv_args {
 };
 
 // ks: waves that split one row tile's K range (ordered carry hand-off); 1 = one wave per tile.
+// ks = KS_RR: the round-pipelined form (matvec_rr.hip): 8 loader waves interleaved over K + a carrier
+// wave that runs the chains one round behind the loads; one workgroup per row tile (grid_x ignored).
+constexpr int KS_RR = 9;
 int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int grid_x, hipStream_t s);
+bool matvec_rr_supported(int wtype, int64_t n_bt);
 size_t matvec_lds_bytes(int wtype, int ks, int64_t n_bt, int64_t segment_tiles);
 
 // ---- ggml graph executor kernels (ggml_ops.hip) ----------------------------------------------------

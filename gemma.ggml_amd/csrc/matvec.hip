@@ -7,6 +7,7 @@ int matvec_dispatch_ks1(int wtype, int pro, int epi, const mv_args &a, int g, hi
 int matvec_dispatch_ks2(int wtype, int pro, int epi, const mv_args &a, int g, hipStream_t s);
 int matvec_dispatch_ks4(int wtype, int pro, int epi, const mv_args &a, int g, hipStream_t s);
 int matvec_dispatch_ks8(int wtype, int pro, int epi, const mv_args &a, int g, hipStream_t s);
+int matvec_dispatch_rr(int wtype, int pro, int epi, const mv_args &a, hipStream_t s);
 
 size_t matvec_lds_bytes(int wtype, int ks, int64_t n_bt, int64_t seg) {
     const bool nsa = ks != 8;  // as launch_t
@@ -37,6 +38,7 @@ int launch_matvec(int wtype, int ks, int pro, int epi, const mv_args &a, int gri
         case 2: r = matvec_dispatch_ks2(wtype, pro, epi, a, grid_x, s); break;
         case 4: r = matvec_dispatch_ks4(wtype, pro, epi, a, grid_x, s); break;
         case 8: r = matvec_dispatch_ks8(wtype, pro, epi, a, grid_x, s); break;
+        case KS_RR: r = matvec_dispatch_rr(wtype, pro, epi, a, s); break;  // grid = one workgroup per row tile
         default: set_error("matvec: unsupported KS");
     }
     if (r != 0 && last_error().empty()) set_error("matvec: bad (ks, pro, epi) combination");

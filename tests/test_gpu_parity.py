@@ -104,10 +104,10 @@ def _rand_f32(rng, *shape, scale=1.0):
 
 
 @gpu
-@pytest.mark.parametrize("ks", [1, 2, 4, 8])
+@pytest.mark.parametrize("ks", [1, 2, 4, 8, 9])  # 9 = KS_RR, the round-pipelined form (falls back to 8 where unsupported)
 @pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
 @pytest.mark.parametrize("rows,k,ncols", [(8, 256, 1), (2048, 2048, 1), (256, 16384, 1), (40, 96, 3), (1000, 2048, 5),
-                                          (13, 64, 2), (64, 24576, 1)])
+                                          (13, 64, 2), (64, 24576, 1), (24, 6144, 2), (16, 32768, 1)])
 def test_mul_mat_quant_bitexact(wtype, rows, k, ncols, ks):
     import gemma_hip as G
     rng = np.random.default_rng(rows * 7 + k + ncols)
@@ -245,7 +245,7 @@ def test_tuned_plan_bitexact():
     e = _engine(shape, n_ctx=128)
     plans = [e.tune(iters=4)]
     base = dict(plans[0])
-    for ks in (1, 2, 4, 8):
+    for ks in (1, 2, 4, 8, 9):  # 9 = KS_RR
         for rpw in (1, 2):
             img = (ks + rpw) % 2  # both image settings of attn-out and down across the sweep
             p = dict(base, down=(ks, rpw, img), qkv=(ks if ks <= 4 else 4, rpw, 0), attn_out=(min(ks, 2), 3 - rpw, 1 - img))
@@ -294,3 +294,15 @@ def test_gate_up_split_waves_bitexact(wtype, rpw, img):
 def test_gate_up_split_waves_tiny_multi_round():
     """several row tiles per wave pair (rounds > 1: the refill path)."""
     _check_decode_plan(O.TINY, 7, 10, 128, O.Q4_0, lambda p: {"gate_up": (2, 16, 0)})
+
+
+@gpu
+@pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
+@pytest.mark.parametrize("img", [0, 1])
+def test_round_pipelined_matvecs_gemma2b_bitexact(wtype, img):
+    """qkv, attn-out and down in the round-pipelined form (plan k_split 9 = KS_RR: 8 loader waves
+    interleaved over K, a carrier wave chaining one round behind) at Gemma-2B layer shapes, with
+    and without the producer-written activation images."""
+    shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
+    _check_decode_plan(shape, 9, 6, 128, wtype,
+                       lambda p: {"qkv": (9, 1, 0), "attn_out": (9, 1, img), "down": (9, 1, img)})
