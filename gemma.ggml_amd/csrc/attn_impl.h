@@ -1,0 +1,388 @@
+// attn_impl.h — one token's attention for one query head (the per-head form), shared by the
+// standalone decode kernel (ops.hip k_attn_head) and the fused layer-front kernel (layer_front.hip).
+//
+// RoPE-NEOX (src/gemma_model.cpp:698-716) + q scale (:708) + KV store (:499-518) + KQ (:474) +
+// soft_max_ext (:476) + KQV (:485) + permute/cont (:487-489) with ggml's AVX/F16C vec_dot_f16 order
+//  and the fp16 exp table (A.6).  SC1: the q|k|v input was handed off inside the same
+// launch (sc1 loads) and the output's Q8_0 image is handed on (sc1 stores) — MI355X_MICROARCH
+// §inter-workgroup visibility, row 1 of the sc1 table.
+#pragma once
+
+#include "device_util.h"
+#include "kernels.h"
+
+namespace ghip {
+namespace {
+
+// ---- ggml_vec_dot_f16 order on 32 per-thread accumulators -------------------------
+__device__ __forceinline__ float reduce_f16_acc(const float acc[4][8]) {
+    float x0[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const float a = acc[0][l] + acc[2][l];
+        const float b = acc[1][l] + acc[3][l];
+        x0[l] = a + b;
+    }
+    float t0[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t0[i] = x0[i] + x0[i + 4];
+    const float h0 = t0[0] + t0[1], h1 = t0[2] + t0[3];
+    return h0 + h1;
+}
+
+// 32 fp16 of x (global/LDS) against 32 fp16 of y: one "step" of the AVX loop
+__device__ __forceinline__ void f16_step(float acc[4][8], const uint4 *x4, const uint4 *y4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint4 xv = x4[j], yv = y4[j];
+        const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w}, ys[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            acc[j][2 * w] = __builtin_fmaf(h2f(xs[w]), h2f(ys[w]), acc[j][2 * w]);
+            acc[j][2 * w + 1] = __builtin_fmaf(h2f(xs[w] >> 16), h2f(ys[w] >> 16), acc[j][2 * w + 1]);
+        }
+    }
+}
+
+#ifndef GHIP_ATT_THREADS
+#define GHIP_ATT_THREADS 1024
+#endif
+constexpr int ATT_THREADS = GHIP_ATT_THREADS;
+constexpr int ATT_QUADS = ATT_THREADS / 4;  // one KQ (position, head) or KQV (dim, head) pair per quad
+constexpr int ATT_VW = 256;                 // V positions staged in LDS per dimension row (n_kv <= 256)
+constexpr int ATT_STG = 2;                  // staging uint4 per thread for each of K and V
+constexpr int ATT_MAXWG = 256;              // co-resident workgroups (in-kernel hand-off)
+
+// ggml_vec_dot_f16 with accumulator row j = t4 held by lane t4 of a quad: fold the
+// quad exactly as sum0+=sum2, sum1+=sum3, sum0+=sum1 (xor-2 then xor-1), then halves and hadds.
+__device__ __forceinline__ float quad_reduce_f16(const float acc[8]) {
+    float x0[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) x0[l] = quad_fold_dpp(acc[l]);
+    float t0[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t0[i] = x0[i] + x0[i + 4];
+    const float h0 = t0[0] + t0[1], h1 = t0[2] + t0[3];
+    return h0 + h1;
+}
+
+// acc = fmaf((float)x16, (float)y16, acc) in ONE instruction: v_fma_mix_f32 converts its f16
+// operands exactly and rounds the fused result once — the F16C/FMA step of ggml_vec_dot_f16.
+__device__ __forceinline__ float fma_mix_lo(uint32_t x, uint32_t y, float acc) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(r) : "v"(x), "v"(y), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ float fma_mix_hi(uint32_t x, uint32_t y, float acc) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "=v"(r) : "v"(x), "v"(y), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ void f16_step8(float acc[8], uint4 xv, uint4 yv) {
+    const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w}, ys[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        acc[2 * w] = fma_mix_lo(xs[w], ys[w], acc[2 * w]);
+        acc[2 * w + 1] = fma_mix_hi(xs[w], ys[w], acc[2 * w + 1]);
+    }
+}
+
+// positions per KQ block (PS) and dims per KQV workgroup (DS): quads = PS*G and DS*G <= 64, and
+// the staged K rows (PS*hd halfs) and V rows (DS*ATT_VW halfs) fit ATT_STG uint4 per thread
+struct attn_split {
+    int ps, ds;
+};
+__host__ __device__ inline attn_split attn_split_of(int G, int hd) {
+    // KQV slices of at most 32 dims: one Q8_0 block of each head's output per workgroup (image)
+    int ps = ATT_QUADS / G, ds = ATT_QUADS / G < 32 ? ATT_QUADS / G : 32;
+    const int cap = ATT_STG * ATT_THREADS * 8;  // halfs
+    if (ps * hd > cap) ps = cap / hd;
+    if (ds * ATT_VW > cap) ds = cap / ATT_VW;
+    return {ps, ds};
+}
+
+// Cross-workgroup hand-off (MI355X_MICROARCH §inter-workgroup visibility, row 1 of the sc1 table):
+// every byte handed off is stored and loaded with global sc1 accesses; each storing wave drains
+// vmcnt before the workgroup barrier, then one lane adds to the counter; the consumer polls the
+// counter with an sc1 load and joins a barrier before any of its sc1 loads.
+typedef __attribute__((address_space(1))) float gfloat_t;
+typedef __attribute__((address_space(1))) int gint_t;
+__device__ __forceinline__ void st_sc1(float *p, float v) {
+    __hip_atomic_store((gfloat_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float *p) {
+    return __hip_atomic_load((const gfloat_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_sc1_i(const int *p) {
+    return __hip_atomic_load((const gint_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+
+typedef __attribute__((address_space(1))) uint32_t guint_t;
+__device__ __forceinline__ void st_sc1_u(uint32_t *p, uint32_t v) {
+    __hip_atomic_store((guint_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1_u(const uint32_t *p) {
+    return __hip_atomic_load((const guint_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool SC1>
+__device__ __forceinline__ float4 ld4(const float *p) {
+    if (!SC1) return *(const float4 *)p;
+    return make_float4(ld_sc1(p), ld_sc1(p + 1), ld_sc1(p + 2), ld_sc1(p + 3));
+}
+template <bool SC1>
+__device__ __forceinline__ float ld1(const float *p) {
+    return SC1 ? ld_sc1(p) : *p;
+}
+// image_put_quad with write-through (sc1) stores (device_util.h)
+__device__ __forceinline__ void image_put_quad_sc1(uint32_t *act, float *da, int64_t b, int q, const float v[8]) {
+    float amax = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    amax = fmaxf(amax, dpp_f<0xB1>(amax));
+    amax = fmaxf(amax, dpp_f<0x4E>(amax));
+    const float d = amax / 127.f;
+    const uint32_t d16 = f2h(d);
+    const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        const int l = 2 * q + hh;
+        int qi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qi[k] = (int)__builtin_rintf(v[4 * hh + k] * id);
+        const uint32_t packed = (uint32_t)(qi[0] & 0xFF) | ((uint32_t)(qi[1] & 0xFF) << 8) |
+                                ((uint32_t)(qi[2] & 0xFF) << 16) | ((uint32_t)(qi[3] & 0xFF) << 24);
+        st_sc1_u(act + ((b >> 2) * 8 + l) * 4 + (b & 3), packed);
+    }
+    if (q == 0) st_sc1(da + b, h2f(d16));
+}
+
+constexpr int AH_THREADS = 1024;  // per-head form: 256 quads = 256 KQ positions / KQV dims per pass
+#ifndef GHIP_AH_PF
+#define GHIP_AH_PF 4
+#endif
+constexpr int AH_KPF = GHIP_AH_PF;  // K steps (of 32 elements) prefetched per lane: hd <= 256
+constexpr int AH_VPF = GHIP_AH_PF;  // V steps (of 32 positions) prefetched per lane: n_kv <= 256
+
+#define AH_STAMP(i)                                                                                         \
+    do {                                                                                                    \
+        if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[(int64_t)h * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+// K/V rows of the first pass (no dependence on this token's q|k|v): KPF K steps of 32 elements for
+// position `quad`, VPF V steps of 32 positions for dimension `quad`, and the published position
+template <int KPF, int VPF>
+struct attn_pre {
+    uint4 k[KPF], v[VPF];
+    int pos_v;
+};
+template <int NTH, int KPF, int VPF>
+__device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, attn_pre<KPF, VPF> &p) {
+    const int hd = a.hd, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
+    const int G = a.H / a.Hkv, kvh = h / G, kvw = a.Hkv * hd;
+    p.pos_v = ((const int *)a.rope_cur)[hd];  // published with the row (k_advance / begin)
+    {
+        const int j = quad < a.ctx ? quad : 0;  // no dependency on pos: rows >= pos are masked
+        const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
+#pragma unroll
+        for (int s = 0; s < KPF; ++s) p.k[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
+    }
+    const int d0 = quad < hd ? quad : 0;
+    const uint16_t *vrow0 = a.vc + ((int64_t)kvh * hd + d0) * a.ctx;
+#pragma unroll
+    for (int s = 0; s < VPF; ++s) p.v[s] = *(const uint4 *)(vrow0 + (s * 32 < a.ctx ? s * 32 : 0) + t4 * 8);
+}
+
+// One token's attention for query head h by one NTH-thread workgroup (SURVEY A.4/A.6 order).
+// PRE: the K/V prefetch `pre` was issued by the caller (the fused kernel issues it before waiting
+// for q|k|v); otherwise it is issued here, after the RoPE inputs (issue order = wait order).
+template <int NTH, bool SC1, int KPF = AH_KPF, int VPF = AH_VPF, bool PRE = false>
+__device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, const attn_pre<KPF, VPF> *pre = nullptr) {
+    const int hd = a.hd, half = hd / 2, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
+    const int lane = tid & 63, wave = tid >> 6, nwave = NTH / 64;
+    const int G = a.H / a.Hkv, kvh = h / G;
+    AH_STAMP(0);
+    const int kvw = a.Hkv * hd;
+    const float *qh = a.qkv + (int64_t)h * hd;
+    const float *kh = a.qkv + (int64_t)a.H * hd + (int64_t)kvh * hd;
+    const float *vh = a.qkv + (int64_t)a.H * hd + kvw + (int64_t)kvh * hd;
+    const float *cs = a.rope_cur, *sn = a.rope_cur + half;
+    // ---- early loads (issue order = wait order): RoPE inputs + pos, then K rows, then V rows
+    // RoPE inputs: only the waves holding a pair load them (every load instruction costs the CU's
+    // load path ~16 clk whatever its addresses; a wave-uniform branch skips the others)
+    const int n4 = half / 4, i4 = (tid < n4 ? tid : 0) * 4;
+    float4 qa{}, qb{}, ka{}, kb{}, ca{}, sa{};
+    if (wave * 64 < n4) {
+        qa = ld4<SC1>(qh + i4); qb = ld4<SC1>(qh + i4 + half);
+        ka = ld4<SC1>(kh + i4); kb = ld4<SC1>(kh + i4 + half);
+        ca = *(const float4 *)(cs + i4); sa = *(const float4 *)(sn + i4);
+    }
+    attn_pre<KPF, VPF> own;
+    if (!PRE) attn_prefetch<NTH, KPF, VPF>(a, h, own);
+    const attn_pre<KPF, VPF> &P = PRE ? *pre : own;
+    const int pos_v = P.pos_v;
+    const uint4 *kpre = P.k, *vpre = P.v;
+    const int d0 = quad < hd ? quad : 0;
+    const float vx0 = ld1<SC1>(vh + d0);
+    const int pos = __builtin_amdgcn_readfirstlane(pos_v);
+    const int n_total = pos + 1;
+    int n_kv = 32 * (n_total / 32 + 1);  // src/gemma_model.cpp:429
+    if (n_kv > a.ctx) n_kv = a.ctx;
+
+    uint16_t *q16 = (uint16_t *)smem;  // hd
+    uint16_t *k16 = q16 + hd;          // hd (this token's k, post-rope)
+    float *S = (float *)(smem + ((2 * hd * 2 + 15) & ~15));  // ctx
+    uint16_t *P16 = (uint16_t *)(S + a.ctx);                 // ctx
+
+    // RoPE NEOX on q (then * q_scale) and on k; f32 -> f16 (ggml_cpy / MUL_MAT INIT conversions)
+    auto rope4 = [&](float4 x0v, float4 x1v, float scale, bool scaled, uint16_t *lo, uint16_t *hi) {
+        const float x0s[4] = {x0v.x, x0v.y, x0v.z, x0v.w}, x1s[4] = {x1v.x, x1v.y, x1v.z, x1v.w};
+        const float cs4[4] = {ca.x, ca.y, ca.z, ca.w}, sn4[4] = {sa.x, sa.y, sa.z, sa.w};
+        uint32_t l2[2] = {0, 0}, h2[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float x0 = x0s[k], x1 = x1s[k], c = cs4[k], s = sn4[k];
+            const float p0 = x0 * c, p1 = x1 * s, p2 = x0 * s, p3 = x1 * c;
+            const float r0 = p0 - p1, r1 = p2 + p3;
+            const uint32_t a0 = scaled ? f2h(r0 * scale) : f2h(r0), a1 = scaled ? f2h(r1 * scale) : f2h(r1);
+            l2[k >> 1] |= a0 << (16 * (k & 1));
+            h2[k >> 1] |= a1 << (16 * (k & 1));
+        }
+        *(uint2 *)lo = make_uint2(l2[0], l2[1]);
+        *(uint2 *)hi = make_uint2(h2[0], h2[1]);
+    };
+    if (tid < n4) {
+        rope4(qa, qb, a.q_scale, true, q16 + i4, q16 + i4 + half);
+        rope4(ka, kb, 1.0f, false, k16 + i4, k16 + i4 + half);
+    }
+    __syncthreads();
+    AH_STAMP(1);
+    // this token's cache entries (src/gemma_model.cpp:506-517), by the group's first head; readers
+    // in this launch use k16 / the v values instead
+    if (h % G == 0) {
+        for (int i = tid; i < hd; i += NTH) a.kc[(int64_t)pos * kvw + (int64_t)kvh * hd + i] = k16[i];
+        for (int d = quad; d < hd; d += NTH / 4)
+            if (t4 == 0) a.vc[((int64_t)kvh * hd + d) * a.ctx + pos] = f2h(d == d0 ? vx0 : ld1<SC1>(vh + d));
+    }
+    // ---- KQ (vec_dot_f16 over hd per kv position) + mask (j > pos -> -inf), scale 1.0
+    for (int j0 = 0; j0 < n_kv; j0 += NTH / 4) {
+        const int j = j0 + quad;
+        float acc[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+        if (j == pos) {
+            for (int s = 0; s * 32 < hd; ++s)
+                f16_step8(acc, *(const uint4 *)(k16 + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
+        } else if (j0 == 0) {
+#pragma unroll
+            for (int s = 0; s < KPF; ++s)
+                if (s * 32 < hd) f16_step8(acc, kpre[s], *(const uint4 *)(q16 + s * 32 + t4 * 8));
+            const uint16_t *krow = a.kc + (int64_t)(j < a.ctx ? j : 0) * kvw + (int64_t)kvh * hd;
+            for (int s = KPF; s * 32 < hd; ++s)
+                f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
+        } else {
+            const int jc = j < pos ? j : 0;  // j > pos is masked below
+            const uint16_t *krow = a.kc + (int64_t)jc * kvw + (int64_t)kvh * hd;
+            for (int s = 0; s * 32 < hd; ++s)
+                f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
+        }
+        const float kq = quad_reduce_f16(acc);
+        if (t4 == 0 && j < n_kv) {
+            const float w = (j > pos) ? -INFINITY : kq * 1.0f + 0.0f;
+            S[j] = w;
+            if (a.dbg_w) a.dbg_w[(int64_t)h * a.ctx + j] = w;
+        }
+    }
+    __syncthreads();
+    AH_STAMP(2);
+    // ---- soft_max_ext: every wave reduces the whole row (DPP) and writes P16 for its
+    // own slice j = 64*wave + lane + NTH*m: one barrier for the whole softmax
+    float mx = -INFINITY;
+    for (int j = lane; j < n_kv; j += 64) mx = fmaxf(mx, S[j]);
+    mx = wave_max(mx);
+    unsigned long long isum = 0;
+    float mine[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int j = lane, k = 0; j < n_kv; j += 64, ++k) {
+        const float w = S[j];
+        float e = 0.0f;
+        if (w != -INFINITY) e = h2f(exp_f16_of(f2h(w - mx)));
+        // e is fp16 in [0,1]: an exact multiple of 2^-24, so the integer sum is the exact sum
+        isum += (unsigned long long)(e * 16777216.0f);
+        const int r = k - wave;
+        if (r >= 0 && r % nwave == 0) {
+            const int m = r / nwave;
+            if (m == 0) mine[0] = e; else if (m == 1) mine[1] = e; else if (m == 2) mine[2] = e; else if (m == 3) mine[3] = e;
+        }
+    }
+    const unsigned long long tot = wave_sum_u64(isum);
+    const double sum = (double)tot * (1.0 / 16777216.0);
+    const float inv = (float)(1.0 / sum);
+    if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
+    for (int j = tid, m = 0; j < n_kv; j += NTH, ++m) {
+        float e;
+        if (m < 4) {
+            e = m == 0 ? mine[0] : m == 1 ? mine[1] : m == 2 ? mine[2] : mine[3];
+        } else {  // long rows: recompute (same table lookup, same value)
+            const float w = S[j];
+            e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
+        }
+        P16[j] = f2h(e * inv);
+        if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
+    }
+    __syncthreads();
+    AH_STAMP(3);
+    // ---- KQV: out[d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16); lane t4 runs accumulator j = t4
+    for (int d = quad; d < hd; d += NTH / 4) {
+        float acc[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+        const uint16_t *vr = a.vc + ((int64_t)kvh * hd + d) * a.ctx;
+        const float vx = d == d0 ? vx0 : ld1<SC1>(vh + d);
+        for (int st = 0, s = 0; st < n_kv; st += 32, ++s) {
+            const int e0 = st + t4 * 8;
+            uint4 xv;
+            if (d == d0 && s < VPF) {
+                xv = vpre[0];  // statically-indexed pick from the early loads
+#pragma unroll
+                for (int k = 1; k < VPF; ++k)
+                    if (s == k) xv = vpre[k];
+            } else {
+                xv = *(const uint4 *)(vr + e0);
+            }
+            if (pos >= e0 && pos < e0 + 8) {  // this token's V: its cache write may not be visible
+                const uint32_t hv = f2h(vx), sh = 16 * ((pos - e0) & 1);
+                const uint32_t msk = ~(0xFFFFu << sh);
+                switch ((pos - e0) >> 1) {
+                    case 0: xv.x = (xv.x & msk) | (hv << sh); break;
+                    case 1: xv.y = (xv.y & msk) | (hv << sh); break;
+                    case 2: xv.z = (xv.z & msk) | (hv << sh); break;
+                    default: xv.w = (xv.w & msk) | (hv << sh); break;
+                }
+            }
+            f16_step8(acc, xv, *(const uint4 *)(P16 + e0));
+        }
+        const float o = quad_reduce_f16(acc);
+        if (t4 == 0) {
+            a.out[(int64_t)h * hd + d] = o;
+            if (a.out_act) ((float *)smem)[d] = o;  // q16|k16 (hd floats) are dead after KQ
+        }
+    }
+    if (a.out_act) {
+        // this head's hd/32 blocks of the Q8_0 activation image of `out` (attn-out's PRO_IMG input;
+        // the same quantize_row_q8_0 the consumer would run, DESIGN.md §Activation image)
+        __syncthreads();
+        if (tid < hd / 8) {
+            const float *o = (const float *)smem + (tid >> 2) * 32 + (tid & 3) * 8;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = o[j];
+            if (SC1) image_put_quad_sc1(a.out_act, a.out_da, (int64_t)h * (hd / 32) + (tid >> 2), tid & 3, v);
+            else image_put_quad(a.out_act, nullptr, a.out_da, (int64_t)h * (hd / 32) + (tid >> 2), tid & 3, v);
+        }
+    }
+    AH_STAMP(4);
+}
+
+
+}  // namespace
+}  // namespace ghip

@@ -213,6 +213,12 @@ struct gemma_engine {
     float *x = nullptr, *qkv = nullptr, *attn = nullptr, *sa = nullptr, *h = nullptr, *logits = nullptr;
     // Q8_0 activation images written by their producers (attention, gate/up) for attn-out and down
     // (DESIGN.md §Activation image); null when a shape does not allow them (then PRO_F32)
+    // fused layer front (layer_front.hip): qkv -> attention -> attn-out in one launch per layer;
+    // hand-off counters [n_layer][16] zeroed once per token (memset node), sticky timeout word
+    int fuse_front = 0;  // measured: 727 vs 672 us/token (the in-launch hand-offs cost as much as the
+                         // launch boundaries they replace; DESIGN.md perf log) — kept as an option
+    unsigned *front_cnt = nullptr;
+    int *front_err = nullptr;
     uint32_t *att_act = nullptr, *h_act = nullptr;
     float *att_da = nullptr, *h_da = nullptr;
     unsigned long long *key = nullptr;
@@ -326,7 +332,42 @@ static int enqueue_step(gemma_engine *e) {
     if (e->out_type == T_Q6_K &&
         launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s))
         return -1;
+    const bool front_ok = e->front_cnt && e->fuse_front && e->tp_n == 1 && e->n_virtual == 1 && !e->warm &&
+                          e->att_mode == ATTN_PER_HEAD && e->att_act && e->plan[MC_QKV].ks == KS_RR &&
+                          e->plan[MC_O].ks == KS_RR && e->plan[MC_O].img;
+    if (front_ok) GHIP_CHECK(hipMemsetAsync(e->front_cnt, 0, (size_t)c.n_layer * 16 * 32 * 4, s));
     for (int il = 0; il < c.n_layer; ++il) {
+        // fused front (layers > 0, or a Q6_K embedding that ran before layer 0): one launch for
+        // K1 + K2 + K3 below, same arithmetic (layer_front.hip)
+        if (front_ok && (il > 0 || e->out_type == T_Q6_K)) {
+            const layer_dev &L = e->layers[il];
+            front_args f;
+            f.q.qs = L.qkv.qs; f.q.sc = L.qkv.sc; f.q.rows = L.qkv.rows; f.q.n_rt = L.qkv.n_rt; f.q.n_bt = L.qkv.n_bt;
+            f.q.nb = L.qkv.nb; f.q.norm_w = L.attn_norm; f.q.eps = c.eps; f.q.x = e->x; f.q.y = e->qkv;
+            attn_args &t = f.t;
+            t.qkv = e->qkv;
+            t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
+            t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
+            t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.rope_cur = e->rope_cur; t.exp_tab = e->exp_tab;
+            t.pos = e->pos; t.out = e->attn; t.out_act = e->att_act; t.out_da = e->att_da;
+            t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
+            t.q_scale = 1.0f / sqrtf((float)c.head_dim);
+            t.mode = ATTN_PER_HEAD;
+            f.o.qs = L.o.qs; f.o.sc = L.o.sc; f.o.rows = L.o.rows; f.o.n_rt = L.o.n_rt; f.o.n_bt = L.o.n_bt; f.o.nb = L.o.nb;
+            f.o.x = e->att_act; f.o.x_da = e->att_da; f.o.y = e->sa; f.o.resid = e->x;
+            f.cnt = e->front_cnt + (size_t)il * 16 * 32;  // 16 counters of 128 B
+            f.err = e->front_err;
+            f.dbg_t = stamp_region(e, il, 0);
+            if (layer_front_supported(wt, f.q, f.t, f.o)) {
+                if (launch_layer_front(wt, f, s)) return -1;
+                const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
+                if (e->dbg) GHIP_CHECK(hipMemcpyAsync(e->dbg + tap, e->qkv, (size_t)e->qkv_rows * 4, hipMemcpyDeviceToDevice, s));
+                if (e->dbg)
+                    GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows, e->attn, (size_t)e->qw * 4, hipMemcpyDeviceToDevice, s));
+                goto ffn;
+            }
+        }
+        {
         // K1: [embed | rms_norm*attn_norm] + quantize -> Wq|Wk|Wv   (:677-696); each rank its rows
         for (int vr = 0; vr < e->n_virtual; ++vr) {
             layer_dev &L = layer_of(e, il, vr);
@@ -392,6 +433,8 @@ static int enqueue_step(gemma_engine *e) {
                 return -1;
         }
         if (tp_gather(e, e->sa, e->sh_e)) return -1;
+        }
+    ffn:
         // K4: rms_norm*ffn_norm + quantize -> gate & up -> gelu(gate)*up  (:724, :446-449)
         const bool h_img = e->h_act && e->plan[MC_DOWN].img;
         for (int vr = 0; vr < e->n_virtual; ++vr) {
@@ -431,7 +474,8 @@ static int enqueue_step(gemma_engine *e) {
         }
         if (tp_gather(e, e->x, e->sh_e)) return -1;
         if (e->dbg)
-            GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows + e->qw, e->x, (size_t)E * 4, hipMemcpyDeviceToDevice, s));
+            GHIP_CHECK(hipMemcpyAsync(e->dbg + (size_t)il * (e->qkv_rows + e->qw + E) + e->qkv_rows + e->qw, e->x,
+                                      (size_t)E * 4, hipMemcpyDeviceToDevice, s));
     }
     // K6: rms_norm*output_norm + quantize -> tied output -> logits + argmax  (:736-740, :532-546)
     // K7: token feedback (greedy_sample -> input.push_back, :282-285), position += 1; the prompt is
@@ -786,6 +830,11 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     if (e->qw % 128 == 0) {  // whole 4-block groups
         GHIP_FATAL(hipMalloc(&e->att_act, (size_t)e->qw));
         GHIP_FATAL(hipMalloc(&e->att_da, (size_t)e->qw / 32 * 4));
+        GHIP_FATAL(hipMalloc(&e->front_cnt, (size_t)c.n_layer * 16 * 32 * 4));
+        GHIP_FATAL(hipMalloc(&e->front_err, 64));
+        GHIP_FATAL(hipMemset(e->front_cnt, 0, (size_t)c.n_layer * 16 * 32 * 4));
+        GHIP_FATAL(hipMemset(e->front_err, 0, 64));
+        if (const char *v = getenv("GHIP_FUSE_FRONT")) e->fuse_front = atoi(v);
     }
     if (e->sh_ff % 128 == 0) {  // every rank's shard is whole 4-block groups
         GHIP_FATAL(hipMalloc(&e->h_act, (size_t)c.n_ff));
@@ -816,7 +865,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         // default launch plan (the shapes of every rank's shards are equal)
         const layer_dev &L0 = e->layers[0];
         e->plan[MC_QKV] = {pick_ks(wt, L0.qkv.n_bt, e->ks_small), 1, 0};
-        e->plan[MC_O] = {pick_ks(wt, L0.o.n_bt, e->ks_small), 1, 0};
+        e->plan[MC_O] = {pick_ks(wt, L0.o.n_bt, e->ks_small), 1, e->att_act ? 1 : 0};  // the image feeds the fused front
         e->plan[MC_GU] = {1, 1, 0};
         e->plan[MC_DOWN] = {pick_ks(wt, L0.down.n_bt, e->ks_down), 1, 0};
         e->plan[MC_LOGITS] = {1, 1, 0};
@@ -991,7 +1040,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
             (void)hipFree(L.ffn_norm);
         }
     }
-    void *bufs[] = {e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
+    void *bufs[] = {e->front_cnt, e->front_err, e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
                     e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf.X, e->pf.SA, e->pf.QKV, e->pf.ATT, e->pf.G, e->pf.U,
                     e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.XH, e->pf.keys};
     for (void *p : bufs)
@@ -1384,6 +1433,31 @@ extern "C" int gemma_engine_plan(gemma_engine *e, int *out, int cap) {
     }
     if (n < cap) out[n++] = e->att_mode;  // attention form: 0 per head, 1 split
     return n;
+}
+
+// fused layer front on/off (tests, A/B); returns the sticky hand-off timeout word (0 = none seen)
+extern "C" int gemma_engine_set_fuse(gemma_engine *e, int fuse_front) {
+    if (fuse_front >= 0) {
+        e->fuse_front = fuse_front;
+        drop_graph(e);
+    }
+    int err = 0;
+    if (e->front_err) (void)hipMemcpy(&err, e->front_err, 4, hipMemcpyDeviceToHost);
+    if (getenv("GHIP_FRONT_DUMP") && e->front_err) {
+        int w[8];
+        (void)hipMemcpy(w, e->front_err, 32, hipMemcpyDeviceToHost);
+        fprintf(stderr, "front_err: flag %d site %d value %d target %d max_polls %d\n", w[0], w[1], w[2], w[3], w[4]);
+    }
+    if (getenv("GHIP_FRONT_DUMP") && e->front_cnt) {  // diagnostics: the hand-off counters
+        std::vector<unsigned> v((size_t)e->cfg.n_layer * 16 * 32);
+        (void)hipMemcpy(v.data(), e->front_cnt, v.size() * 4, hipMemcpyDeviceToHost);
+        for (int il = 0; il < e->cfg.n_layer; ++il) {
+            fprintf(stderr, "front_cnt[%d]:", il);
+            for (int k = 0; k < 16; ++k) fprintf(stderr, " %u", v[((size_t)il * 16 + k) * 32]);
+            fprintf(stderr, "\n");
+        }
+    }
+    return err;
 }
 
 extern "C" int gemma_engine_set_plan(gemma_engine *e, const int *in, int n) {

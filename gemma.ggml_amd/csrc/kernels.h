@@ -210,6 +210,19 @@ struct attn_args {
     int *sync = nullptr;
     int *err = nullptr;
 };
+// the front half of a decode layer in one launch (layer_front.hip): qkv (rr, PRO_NORM, EPI_STORE)
+// -> per-head attention -> attn-out (rr, PRO_IMG from the attention's image, EPI_ADD)
+struct front_args {
+    mv_args q;
+    attn_args t;
+    mv_args o;
+    unsigned *cnt = nullptr;  // this layer's hand-off counters [16], zero before the launch
+    int *err = nullptr;       // sticky: a hand-off poll timed out
+    unsigned long long *dbg_t = nullptr;  // diagnostics (stamps build): 16 s_memrealtime per workgroup
+};
+bool layer_front_supported(int wtype, const mv_args &q, const attn_args &t, const mv_args &o);
+int launch_layer_front(int wtype, const front_args &f, hipStream_t s);
+
 struct attn_geom {
     int nwg = 0, grid = 0;
     int img = 0;  // the split form can write the output's Q8_0 image (32-dim KQV slices)

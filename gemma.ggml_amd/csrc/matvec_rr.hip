@@ -15,70 +15,10 @@
 //   * a 9th wave, the carrier, runs the 64 chains through round r-1 while the loaders convert
 //     round r — the chain is consumed as the data lands and ends one round after the last load.
 // One s_barrier per round; no vmcnt(0) drain (loads stay in flight across the barriers).
-#include "matvec_impl.h"
+#include "matvec_rr.h"
 
 namespace ghip {
 namespace {
-
-constexpr int RR_NL = 8;                  // loader waves
-constexpr int RR_NTH = 64 * (RR_NL + 1);  // + the carrier wave
-constexpr int RF_NS = 4;                  // flag form: stash slots (rounds the loaders may run ahead)
-
-// LDS barrier that does not drain the wave's outstanding global loads: LDS stores complete
-// (lgkmcnt), then s_barrier.  (__syncthreads() would also wait for every in-flight load.)
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// stash slot geometry: per lane a run of the round's 8*BT terms (s), per row 8*BT d values.
-// Lane stride 144 B (36 dwords): the 16-B stores of 8 lanes and the b128 reads of 16 lanes hit
-// distinct banks; row stride of d 8*BT+4 floats.  A slot ends with slack for the carry ring's
-// over-reads (up to 4 chunks past a run).
-template <int WT> struct rr_geom {
-    static constexpr int BT = wfmt<WT>::BT;
-    static constexpr int RUN = 8 * BT;                      // blocks per round
-    static constexpr int SBP = RUN + 4;                     // s stride (f32): 272 B (Q4_0) / 144 B (Q8_0), = 4 dwords mod 32
-    static constexpr int SBPD = RUN + 4;                    // d stride (f32)
-    static constexpr size_t S_BYTES = 64 * SBP * 4 + 256;
-    static constexpr size_t D_BYTES = 8 * SBPD * 4 + 256;
-    static constexpr size_t SLOT = S_BYTES + D_BYTES;
-};
-
-// exact (d, (float)isum) terms of one tile for this thread's (row, lane): the operands of the BT
-// fmaf steps tile_dot<WT, false> would apply, stored for the carrier (s as f32: the carrier's
-// chain is then LDS reads + fmaf only)
-template <int WT>
-__device__ __forceinline__ void tile_terms(uint4 q, uint4 scv, const uint8_t *smem, const lds_map &m, int64_t bt, int l,
-                                           float *st_s, float *st_d, int j0) {
-    const act_tile<WT> t = load_act<WT, true>(smem, m, bt, l);
-    const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
-    if constexpr (WT == T_Q4_0) {
-        const uint32_t sv[4] = {scv.x, scv.y, scv.z, scv.w};
-        float dd[8], ss[8];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const uint32_t lo = qv[p] & 0x0F0F0F0Fu, hi = (qv[p] >> 4) & 0x0F0F0F0Fu;
-            ss[2 * p] = (float)sdot4(lo, t.av[2 * p], (int)t.nv[2 * p]);
-            ss[2 * p + 1] = (float)sdot4(hi, t.av[2 * p + 1], (int)t.nv[2 * p + 1]);
-            dd[2 * p] = mix_lo(sv[p], t.dav[2 * p]);
-            dd[2 * p + 1] = mix_hi(sv[p], t.dav[2 * p + 1]);
-        }
-        *(float4 *)(st_s + j0) = make_float4(ss[0], ss[1], ss[2], ss[3]);
-        *(float4 *)(st_s + j0 + 4) = make_float4(ss[4], ss[5], ss[6], ss[7]);
-        if (l == 0) {
-            *(float4 *)(st_d + j0) = make_float4(dd[0], dd[1], dd[2], dd[3]);
-            *(float4 *)(st_d + j0 + 4) = make_float4(dd[4], dd[5], dd[6], dd[7]);
-        }
-    } else {
-        const uint32_t sv[2] = {scv.x, scv.y};
-        float dd[4], ss[4];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            ss[p] = (float)sdot4(qv[p], t.av[p], 0);
-            dd[p] = (p & 1) ? mix_hi(sv[p >> 1], t.dav[p]) : mix_lo(sv[p >> 1], t.dav[p]);
-        }
-        *(float4 *)(st_s + j0) = make_float4(ss[0], ss[1], ss[2], ss[3]);
-        if (l == 0) *(float4 *)(st_d + j0) = make_float4(dd[0], dd[1], dd[2], dd[3]);
-    }
-}
 
 template <int WT, int PRO, int EPI, int NR, int R, int DD>
 __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
@@ -171,107 +111,11 @@ __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
 }
 
 
-// Flag form: the same work with the loaders decoupled from the carrier.  A ring of RF_NS stash slots;
-// loader waves stash round r into slot r % RF_NS as soon as its tile has landed and then bump the
-// slot's LDS counter; the carrier polls the counter (8 arrivals per round) and runs the chains; the
-// loaders only wait when RF_NS rounds ahead of the carrier.  No workgroup barrier after the prologue.
-__device__ __forceinline__ unsigned lds_load_relaxed(const unsigned *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// bounded LDS spin: a wave of this workgroup is the producer, so only a bug can stall it; past the
-// bound the kernel computes garbage instead of hanging the GPU
-__device__ __forceinline__ void lds_wait_geq(const unsigned *p, unsigned target) {
-    for (int it = 0; it < (1 << 20) && lds_load_relaxed(p) < target; ++it) __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");  // the stash reads stay behind the poll
-}
-
-template <int WT, int PRO, int EPI, int NR, int R, int DD>
-__global__ void __launch_bounds__(RR_NTH) k_matvec_rf(mv_args a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    using G = rr_geom<WT>;
-    constexpr int BT = G::BT, SB = wfmt<WT>::SCALE_BYTES;
-    constexpr bool NSA = true;
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int rr = lane >> 3, l = lane & 7;
-    const int col = blockIdx.y;
-    const int64_t rt = blockIdx.x;
-    const lds_map m = make_lds_map<WT, NSA>(1, a.n_bt, a.n_bt, 0);
-    const size_t slot0 = (m.total + 15) & ~(size_t)15;
-    unsigned *cnt = (unsigned *)(smem + slot0 + RF_NS * G::SLOT);  // [RF_NS] arrivals, [RF_NS] = rounds consumed
-    const bool loader = wave < RR_NL;
-    unsigned long long *stp = GHIP_STAMPS && a.dbg_t ? a.dbg_t + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 : nullptr;
-    if (GHIP_STAMPS && stp && tid == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
-    if (tid <= RF_NS) cnt[tid] = 0;
-
-    act_regs<R> ar;
-    prefetch_activation<WT, PRO, R, RR_NTH>(a, col, ar);
-    if (!(a.ablate & 1)) build_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar);
-    if (GHIP_STAMPS && stp && tid == 0) stp[10] = __builtin_amdgcn_s_memrealtime();
-
-    constexpr int D = DD < NR ? DD : NR;
-    uint4 qb[D], sb[D];
-    const uint32_t q_off = (uint32_t)lane * 16u, s_off = (uint32_t)rr * SB;
-    auto issue = [&](int r) {
-        const int64_t tile = rt * a.n_bt + wave + RR_NL * r;
-        qb[r % D] = ld_nt16(a.qs + tile * 1024 + q_off);
-        if (WT == T_Q4_0) {
-            sb[r % D] = ld_nt16(a.sc + tile * 8 * SB + s_off);
-        } else {
-            const uint2 v = ld_nt8(a.sc + tile * 8 * SB + s_off);
-            sb[r % D] = make_uint4(v.x, v.y, 0, 0);
-        }
-    };
-    if (loader) {
-#pragma unroll
-        for (int r = 0; r < D; ++r) issue(r);
-    }
-    if (GHIP_STAMPS && stp && tid == 0) stp[11] = __builtin_amdgcn_s_memrealtime();
-    lds_barrier();  // the activation image (and the zeroed counters) visible to every wave
-    if (GHIP_STAMPS && stp && tid == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
-
-    auto slot_s = [&](int r) { return (float *)(smem + slot0 + (size_t)(r % RF_NS) * G::SLOT); };
-    auto slot_d = [&](int r) { return (float *)(smem + slot0 + (size_t)(r % RF_NS) * G::SLOT + G::S_BYTES); };
-    if (loader) {
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            if (r >= RF_NS) lds_wait_geq(cnt + RF_NS, (unsigned)(r - RF_NS + 1));  // slot free again
-            float *st = slot_s(r) + (size_t)lane * G::SBP;
-            float *sd = slot_d(r) + (size_t)rr * G::SBPD;
-            const uint4 q = qb[r % D], sc = sb[r % D];
-            tile_terms<WT>(q, sc, smem, m, wave + RR_NL * r, l, st, sd, wave * BT);
-            if (r + D < NR) issue(r + D);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stash is in LDS before the arrival
-            if (lane == 0) __hip_atomic_fetch_add(cnt + (r % RF_NS), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (GHIP_STAMPS && stp && lane == 0 && wave == 0 && r < 8) stp[2 + r] = __builtin_amdgcn_s_memrealtime();
-            if (GHIP_STAMPS && stp && lane == 0 && wave == RR_NL - 1 && r == NR - 1) stp[15] = __builtin_amdgcn_s_memrealtime();
-        }
-        return;
-    }
-    // the carrier
-    __builtin_amdgcn_s_setprio(3);
-    float acc = 0.0f;
-#pragma unroll 1
-    for (int r = 0; r < NR; ++r) {
-        lds_wait_geq(cnt + (r % RF_NS), (unsigned)(RR_NL * (r / RF_NS + 1)));
-        const float4 *pd = (const float4 *)(slot_d(r) + (size_t)rr * G::SBPD);
-        const uint4 *ps = (const uint4 *)(slot_s(r) + (size_t)lane * G::SBP);
-        acc = carry_ring<false>(ps, pd, G::RUN / 4, acc);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the slot done before freeing it
-        if (lane == 0) __hip_atomic_fetch_add(cnt + RF_NS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (GHIP_STAMPS && stp && lane == 0 && r == 5) stp[12] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (GHIP_STAMPS && stp && lane == 0) stp[13] = __builtin_amdgcn_s_memrealtime();
-    const float v = fold8(acc);
-    unsigned long long best = 0;
-    if (l == 0) epilogue<EPI>(a, col, rt * 8 + rr, v, 0.0f, best);
-    if (GHIP_STAMPS && stp && lane == 0) stp[14] = __builtin_amdgcn_s_memrealtime();
-}
-
 template <int WT, int PRO, int EPI, int NR>
 int launch_rr_t(const mv_args &a, hipStream_t s) {
     constexpr int R = (PRO == PRO_F32 || PRO == PRO_NORM) && NR * wfmt<WT>::BT * 8 > 144 ? 4 : 1;
     const lds_map m = make_lds_map<WT, true>(1, a.n_bt, a.n_bt, 0);
-    size_t lds = ((m.total + 15) & ~(size_t)15) + 2 * rr_geom<WT>::SLOT;
+    const size_t lds = ((m.total + 15) & ~(size_t)15) + 2 * rr_geom<WT>::SLOT;
     if (lds > 160 * 1024) {
         set_error("matvec(rr): LDS image too large");
         return -1;
@@ -285,13 +129,7 @@ int launch_rr_t(const mv_args &a, hipStream_t s) {
     // 4 7.9, 2 8.2 — four keep the CU's memory queue full without stalling the first round's issue
     static const int dd_env = getenv("GHIP_RR_D") ? atoi(getenv("GHIP_RR_D")) : 4;
     const int dd = (PRO == PRO_IMG || PRO == PRO_F32) && EPI == EPI_ADD && NR >= 8 && dd_env ? dd_env : 64;
-    static const bool flags = getenv("GHIP_RR_FLAGS") && atoi(getenv("GHIP_RR_FLAGS"));
-    const size_t lds_f = ((m.total + 15) & ~(size_t)15) + RF_NS * rr_geom<WT>::SLOT + 64;
-    const bool use_f = flags && NR >= 2 && lds_f <= 160 * 1024;
-    if (use_f) lds = lds_f;
-    const void *fn = use_f ? (dd == 4 ? (const void *)k_matvec_rf<WT, PRO, EPI, NR, R, 4>
-                                      : (const void *)k_matvec_rf<WT, PRO, EPI, NR, R, 64>)
-                   : dd == 2 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 2>
+    const void *fn = dd == 2 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 2>
                    : dd == 4 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 4>
                    : dd == 6 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 6>
                              : (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 64>;

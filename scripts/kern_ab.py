@@ -14,7 +14,7 @@ for spec in sys.argv[1:]:
     p = dict(base)
     for item in spec.split(";"):
         k, v = item.split("=")
-        p[k] = tuple(int(t) for t in v.split(","))
+        p[k] = int(v) if k == "attention" else tuple(int(t) for t in v.split(","))
     e.set_plan(p)
     res = {}
     for k in [k for k in IDS if k in spec] + ["step"]:

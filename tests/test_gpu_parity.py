@@ -306,3 +306,27 @@ def test_round_pipelined_matvecs_gemma2b_bitexact(wtype, img):
     shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
     _check_decode_plan(shape, 9, 6, 128, wtype,
                        lambda p: {"qkv": (9, 1, 0), "attn_out": (9, 1, img), "down": (9, 1, img)})
+
+
+@gpu
+@pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
+@pytest.mark.parametrize("fuse", [1, 0])
+def test_fused_layer_front_gemma2b_bitexact(wtype, fuse):
+    """qkv -> attention -> attn-out as ONE launch per layer (layer_front.hip: in-launch sc1 hand-offs
+    over sharded counters) against the oracle, and the unfused launches; no hand-off may time out."""
+    O.lib().orc_set_threads(16)
+    shape = dict(O.GEMMA_2B, n_layer=3, n_vocab=8192)
+    m = O.Model(O.make_config(shape, n_ctx=256, wtype=wtype))
+    prompt = O.make_prompt(9, shape["n_vocab"])
+    seq_ref, lg_ref = m.generate(prompt, 40)
+    e = _engine(shape, n_ctx=256, wtype=wtype)
+    p = e.plan()
+    p.update(qkv=(9, 1, 0), attn_out=(9, 1, 1), attention=0)
+    e.set_plan(p)
+    e.set_fuse(fuse)
+    e.begin(prompt)
+    lg = e.step(len(prompt) + 40, want_logits=True, use_graph=True)
+    assert e.set_fuse(-1) == 0, "an in-launch hand-off timed out"
+    assert list(e.tokens()[: len(seq_ref)]) == list(seq_ref)
+    assert np.array_equal(lg[len(prompt) - 1:].view(np.uint32), lg_ref.view(np.uint32))
+    e.close()
