@@ -101,6 +101,37 @@ def cpu_baseline(n_prompt=128, n_decode=48, threads=4):
             "affinity_cpus": allowed, "runs": runs}
 
 
+# MFMA dense peaks (MI355X_MICROARCH §Matrix cores): BF16/F16 ~2.5 PF; I8 = 2x the BF16 rate per clock
+MFMA_PEAK_TOPS = {"i8": 5000.0, "f16": 2500.0}
+GEMMA_2B_MACS_PER_TOKEN = 2506096640  # every weight of the 18 layers + the tied output
+
+
+def prefill_roofline(T, prefill):
+    """Prefill against the MFMA roofline: algorithmic ops = 2*T*MACs/token for the weight
+    GEMMs (logits for every row, src/gemma_model.cpp:740) + the full masked attention, 18 layers x
+    (KQ + KQV) x 2 flops x 8 heads x 256 x T^2; plus the PMC MFMA/LDS utilisation of the exact GEMM
+    from the committed profile (profiles/r02/pmc_prefill.json, scripts/pmc_prefill.sh)."""
+    gemm_ops = 2.0 * T * GEMMA_2B_MACS_PER_TOKEN
+    attn_ops = 18 * 4 * 8 * 256 * float(T) * T
+    out = {"bound": "mfma", "unit": "TOP/s", "algo_ops": gemm_ops + attn_ops, "gemm_ops": gemm_ops, "attn_ops": attn_ops,
+           "peak_i8_dense": MFMA_PEAK_TOPS["i8"], "peak_f16_dense": MFMA_PEAK_TOPS["f16"]}
+    for name in ("exact", "fast"):
+        if name in prefill:
+            a = out["algo_ops"] / (prefill[name]["ms"] * 1e-3) / 1e12
+            out[name] = {"achieved": round(a, 1), "frac_i8": round(a / MFMA_PEAK_TOPS["i8"], 4),
+                         "frac_f16": round(a / MFMA_PEAK_TOPS["f16"], 4)}
+    out["achieved"] = out["exact"]["achieved"]
+    out["peak"] = MFMA_PEAK_TOPS["i8"]
+    out["frac"] = out["exact"]["frac_i8"]
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02", "pmc_prefill.json")) as f:
+            pmc = json.load(f)
+        out["pmc_exact_gemm"] = {k: pmc[k] for k in ("mfma_util", "lds_busy", "lds_bank_conflict_frac", "note")}
+    except Exception:
+        out["pmc_exact_gemm"] = None
+    return out
+
+
 def load_traffic(kernel_id):
     """HBM bytes per launch of the roofline kernel from the committed PMC summary (or None)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -296,6 +327,7 @@ def main():
                                    "path (DESIGN.md Prefill)")
         prefill["tok_s"] = prefill["exact"]["tok_s"]
         prefill["ms"] = prefill["exact"]["ms"]
+        prefill["roofline"] = prefill_roofline(args.prefill, prefill)
 
     # K-quant leg: Q4_K / Q6_K x Q8_K matvec alone at Gemma-2B shapes, cold weights
     kquant = {}
