@@ -38,9 +38,52 @@ def main():
         if world > 1:
             dist.barrier()
 
+    import hashlib
+
+    import numpy as np
+    n_check, prompt = 20, make_prompt(16, GEMMA_7B["n_vocab"])
+
+    def row_hashes(lg):
+        return np.frombuffer(b"".join(hashlib.sha1(r.tobytes()).digest()[:8] for r in lg), dtype=np.uint8).copy()
+
+    # reference (rank 0): the UNSPLIT engine on one GPU, same synthetic weights and prompt; the first
+    # 16 rows are the prompt positions (teacher-forced, so they vary with the input tokens), then 4
+    # greedy steps.  Its logits hashes are broadcast; every rank compares its own gathered logits.
+    # At N = 1 the split under test is 8 virtual ranks on one GPU (the same shards and key merge).
+    ref = torch.zeros(n_check * 8, dtype=torch.uint8)
+    tok_s_1 = None
+    margin = None
+    if rank == 0:
+        re_ = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank)
+        re_.begin(prompt)
+        lg = re_.step(n_check, want_logits=True, use_graph=True)
+        ref = torch.from_numpy(row_hashes(lg))
+        top2 = np.sort(lg, axis=1)[:, -2:]
+        margin = float(np.min((top2[:, 1] - top2[:, 0]) / np.maximum(np.abs(top2[:, 1]), 1e-30)))
+        re_.L.gemma_engine_sync(re_.h)
+        t1 = time.perf_counter()
+        re_.step(steps, use_graph=True)
+        re_.L.gemma_engine_sync(re_.h)
+        tok_s_1 = steps / (time.perf_counter() - t1)
+        re_.close()
+    if world > 1:
+        dist.broadcast(ref, 0)
+    split = (world, rank, rid) if world > 1 else (8, 0, None)
+    ce = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=split)
+    ce.begin(prompt)
+    got = row_hashes(ce.step(n_check, want_logits=True, use_graph=True))
+    ce.close()
+    bad = torch.tensor([int(np.sum(got.reshape(n_check, 8) != ref.numpy().reshape(n_check, 8), axis=1).astype(bool).sum())])
+    if world > 1:
+        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+    if int(bad.item()) != 0:
+        if rank == 0:
+            print(json.dumps({"error": f"row-split logits differ from the unsplit engine: {int(bad.item())} rows over all ranks"}), flush=True)
+        sys.exit(3)
+
     te = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=(world, rank, rid))
     plan = te.tune(6) if tune else te.plan()
-    te.begin(make_prompt(16, GEMMA_7B["n_vocab"]))
+    te.begin(prompt)
     te.step(16 + 4, use_graph=True)
     sync()
     t0 = time.perf_counter()
@@ -55,9 +98,17 @@ def main():
     toks = list(te.tokens())
     te.close()
     if rank == 0:
-        print(json.dumps({"model": "Gemma-7B " + wtype_s.upper(), "ranks": world, "tok_s": round(steps / dt, 2),
+        tok_s = steps / dt
+        print(json.dumps({"model": "Gemma-7B " + wtype_s.upper(), "ranks": world, "tok_s": round(tok_s, 2),
                           "ms_per_token": round(dt / steps * 1e3, 4), "steps": steps,
                           "parallelism": f"row-split tp{world} (RCCL all-gather x4/layer)" if world > 1 else "1 GPU",
+                          "tok_s_unsplit_1gpu": round(tok_s_1, 2),
+                          "speedup_vs_1gpu": round(tok_s / tok_s_1, 3),
+                          "strong_scaling_efficiency": round(tok_s / tok_s_1 / world, 3),
+                          "parity_check": {"rows": n_check, "mismatched_rows_all_ranks": 0,
+                                           "reference": "unsplit 1-GPU engine (rank 0), logits sha1 per row",
+                                           "split_checked": f"{world} RCCL ranks" if world > 1 else "8 virtual ranks",
+                                           "min_top1_top2_rel_margin": round(margin, 6)},
                           "tokens_head": [int(t) for t in toks[16:24]], "launch_plan": plan}), flush=True)
     if world > 1:
         dist.barrier()
