@@ -177,6 +177,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--prefill", type=int, default=2048, help="prefill leg prompt length (0 = skip)")
+    ap.add_argument("--ggml-steps", type=int, default=64, help="decode steps of the ggml-API drop-in leg (0 = skip)")
     ap.add_argument("--no-tune", action="store_true", help="default launch plan instead of the measured one")
     ap.add_argument("--tp-steps", type=int, default=48, help="Gemma-7B row-split decode leg steps (0 = skip)")
     ap.add_argument("--q8-steps", type=int, default=48, help="Gemma-2B Q8_0 decode leg steps (0 = skip)")
@@ -329,6 +330,30 @@ def main():
         prefill["ms"] = prefill["exact"]["ms"]
         prefill["roofline"] = prefill_roofline(args.prefill, prefill)
 
+    # ggml-API drop-in leg: the reference's graph code (tests/ggml_driver, restating
+    # src/gemma_model.cpp) driving ggml_graph_compute_with_ctx on a Gemma-2B Q4_0 GGUF of the same
+    # synthetic weights; timed like src/gemma_model.cpp:552-572 (graph build + compute + greedy sample)
+    ggml_leg = None
+    if args.ggml_steps > 0 and rank == 0 and world == 1:
+        import re
+        import subprocess
+        import tempfile
+        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+            try:
+                r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ggml_path_bench.py"), str(args.ggml_steps), td],
+                                   capture_output=True, text=True, timeout=600)
+                mt = re.search(r"prefill_ms ([0-9.]+) prompt (\d+) decode_ms ([0-9.]+) steps (\d+) decode_tok_s ([0-9.]+)", r.stdout)
+                if mt:
+                    ggml_leg = {"decode_tok_s": float(mt.group(5)), "prefill_tok_s": round(int(mt.group(2)) / float(mt.group(1)) * 1e3, 1),
+                                "prompt": int(mt.group(2)), "steps": int(mt.group(4)),
+                                "path": "ggml_graph_compute_with_ctx recognises the Gemma graph and runs the device-resident engine "
+                                        "over the graph's weights and KV-cache mirrors (ggml_api.cpp try_fast); includes the "
+                                        "reference loop's host graph build and greedy sample"}
+                else:
+                    ggml_leg = {"error": (r.stderr or r.stdout)[-300:]}
+            except Exception as ex:  # reported, never fatal to the headline line
+                ggml_leg = {"error": str(ex)[:300]}
+
     # K-quant leg: Q4_K / Q6_K x Q8_K matvec alone at Gemma-2B shapes, cold weights
     kquant = {}
     for t, name in ((G.GGML_TYPE_Q4_K, "q4_K"), (G.GGML_TYPE_Q6_K, "q6_K")):
@@ -384,6 +409,8 @@ def main():
             "q4_0_q6k_output_decode": q6o,
             "q4_k_m_decode": kqm,
             "tp_decode": tp,
+            "ggml_path": ggml_leg,
+            "ggml_path_decode_tok_s": ggml_leg.get("decode_tok_s") if ggml_leg else None,
             "launch_plan": {k: ({"k_split": v[0], "rows_per_wg": v[1], "image": v[2]} if isinstance(v, tuple) else
                                 ("split" if v else "per_head")) for k, v in plan.items()},
             "prefill_serial_tok_s": round(args.prompt / prefill_serial_s, 2),

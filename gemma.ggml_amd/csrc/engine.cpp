@@ -19,6 +19,7 @@
 
 #include "../../include/gemma_hpc.h"
 #include "../../include/ggml.h"
+#include "engine_ext.h"
 #include "kernels.h"
 
 namespace ghip {
@@ -141,6 +142,7 @@ static tiled_mat sub_rows(const tiled_mat &m, int64_t r0, int64_t n) {
 }  // namespace ghip
 
 using namespace ghip;
+using ghip::host_weights;
 
 struct layer_dev {
     float *attn_norm = nullptr, *ffn_norm = nullptr;
@@ -195,6 +197,8 @@ struct gemma_engine {
     float *out_norm = nullptr;
     std::vector<layer_dev> layers;
     uint16_t *kc = nullptr, *vc = nullptr;  // [L][ctx][kvw], [L][kvw][ctx]
+    std::vector<uint16_t *> kc_ext, vc_ext;  // external per-layer caches (ggml executor), else empty
+    float *ext_stage = nullptr;               // pinned logits row (ggml executor path)
     int att_mode = ATTN_PER_HEAD;
     // row-split tensor parallelism: this rank's contiguous row range of every
     // matrix; activations are full vectors, each matvec writes its shard in place and an in-place
@@ -306,6 +310,13 @@ static int tp_gather_bytes(gemma_engine *e, uint32_t *act, int64_t act_bytes, fl
 // layer il's shards of (virtual) rank slot vr, and the rank that slot stands for
 static inline layer_dev &layer_of(gemma_engine *e, int il, int vr) { return e->layers[(size_t)il * e->n_virtual + vr]; }
 static inline int rank_of(const gemma_engine *e, int vr) { return e->n_virtual > 1 ? vr : e->tp_rank; }
+// layer il's caches: K [ctx][kvw], V [kvw][ctx]
+static inline uint16_t *kc_of(const gemma_engine *e, int il) {
+    return e->kc_ext.empty() ? e->kc + (size_t)il * e->cfg.n_ctx * e->kvw : e->kc_ext[il];
+}
+static inline uint16_t *vc_of(const gemma_engine *e, int il) {
+    return e->vc_ext.empty() ? e->vc + (size_t)il * e->cfg.n_ctx * e->kvw : e->vc_ext[il];
+}
 
 static inline int wfmt_scale(int wt) { return wt == T_Q4_0 ? 16 : 8; }  // scale bytes per row and tile
 
@@ -346,8 +357,8 @@ static int enqueue_step(gemma_engine *e) {
             f.q.nb = L.qkv.nb; f.q.norm_w = L.attn_norm; f.q.eps = c.eps; f.q.x = e->x; f.q.y = e->qkv;
             attn_args &t = f.t;
             t.qkv = e->qkv;
-            t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
-            t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
+            t.kc = kc_of(e, il);
+            t.vc = vc_of(e, il);
             t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.rope_cur = e->rope_cur; t.exp_tab = e->exp_tab;
             t.pos = e->pos; t.out = e->attn; t.out_act = e->att_act; t.out_da = e->att_da;
             t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
@@ -393,8 +404,8 @@ static int enqueue_step(gemma_engine *e) {
         // K2: rope + scale + kv store + KQ + softmax + KQV  (:698-718, :454-518); replicated
         attn_args t;
         t.qkv = e->qkv;
-        t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
-        t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
+        t.kc = kc_of(e, il);
+        t.vc = vc_of(e, il);
         t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.rope_cur = e->rope_cur; t.exp_tab = e->exp_tab;
         t.pos = e->pos; t.out = e->attn;
         const bool att_img = e->att_act && att_img_ok(e) && e->plan[MC_O].img;
@@ -551,8 +562,8 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         if (mv(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr)) return -1;
         attn_args t;
         t.qkv = e->qkv;
-        t.kc = e->kc + (size_t)il * c.n_ctx * e->kvw;
-        t.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
+        t.kc = kc_of(e, il);
+        t.vc = vc_of(e, il);
         t.rope_cos = e->rope_cos; t.rope_sin = e->rope_sin; t.rope_cur = e->rope_cur; t.exp_tab = e->exp_tab;
         t.pos = e->pos; t.out = e->attn;
         t.H = c.n_head; t.Hkv = c.n_head_kv; t.hd = c.head_dim; t.ctx = c.n_ctx;
@@ -578,16 +589,6 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
 }
 
 // real weights in ggml row-major layout (a GGUF file's tensors, src/gemma_model.cpp:145-182)
-struct host_weights {
-    const void *embd = nullptr;  // token_embd, type cfg.out_type (or wtype)
-    const float *out_norm = nullptr;
-    struct layer {
-        const float *attn_norm = nullptr, *ffn_norm = nullptr;
-        const void *q = nullptr, *k = nullptr, *v = nullptr, *o = nullptr, *gate = nullptr, *up = nullptr, *down = nullptr;
-        int tq = 0, tk = 0, tv = 0, to = 0, tg = 0, tu = 0, td = 0;  // K-quant layers: each matrix's type
-    };
-    std::vector<layer> layers;
-};
 
 // rows [r0, r0 + dst.rows) of a host row-major Q4_0 / Q8_0 matrix into the tiled layout
 static int upload_rows(const tiled_mat &dst, const void *host, int64_t r0, hipStream_t s) {
@@ -602,7 +603,8 @@ static int upload_rows(const tiled_mat &dst, const void *host, int64_t r0, hipSt
 }
 
 static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int tp_n, int tp_rank, const void *nccl_id,
-                                   const host_weights *hw = nullptr) {
+                                   const host_weights *hw = nullptr, const std::vector<uint16_t *> *kc_ext = nullptr,
+                                   const std::vector<uint16_t *> *vc_ext = nullptr) {
     set_error("");
     const gemma_hip_config &c = *cfg;
     const bool kq_layers = c.wtype == T_Q4_K;  // K-quant layers (Q4_K / Q6_K per matrix) + Q6_K output
@@ -793,10 +795,15 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     }
     // caches, tables, activations
     const size_t kv_elems = (size_t)c.n_layer * c.n_ctx * e->kvw;
-    GHIP_FATAL(hipMalloc(&e->kc, kv_elems * 2));
-    GHIP_FATAL(hipMalloc(&e->vc, kv_elems * 2));
-    GHIP_FATAL(hipMemsetAsync(e->kc, 0, kv_elems * 2, s));
-    GHIP_FATAL(hipMemsetAsync(e->vc, 0, kv_elems * 2, s));
+    if (kc_ext && vc_ext) {
+        e->kc_ext = *kc_ext;
+        e->vc_ext = *vc_ext;
+    } else {
+        GHIP_FATAL(hipMalloc(&e->kc, kv_elems * 2));
+        GHIP_FATAL(hipMalloc(&e->vc, kv_elems * 2));
+        GHIP_FATAL(hipMemsetAsync(e->kc, 0, kv_elems * 2, s));
+        GHIP_FATAL(hipMemsetAsync(e->vc, 0, kv_elems * 2, s));
+    }
     std::vector<uint16_t> et, gt;
     build_f16_tables(et, gt);
     std::vector<float> rc, rs;
@@ -1030,6 +1037,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     (void)hipStreamSynchronize(e->stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->rank_keys) (void)hipFree(e->rank_keys);
+    if (e->ext_stage) (void)hipHostFree(e->ext_stage);
     drop_graph(e);
     free_tiled(e->embd);
     for (size_t i = 0; i < e->layers.size(); ++i) {
@@ -1073,9 +1081,10 @@ extern "C" int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_
         }
     (void)hipSetDevice(e->device);
     hipStream_t s = e->stream;
-    const size_t kv_bytes = (size_t)c.n_layer * c.n_ctx * e->kvw * 2;
-    GHIP_CHECK(hipMemsetAsync(e->kc, 0, kv_bytes, s));
-    GHIP_CHECK(hipMemsetAsync(e->vc, 0, kv_bytes, s));
+    for (int il = 0; il < c.n_layer; ++il) {
+        GHIP_CHECK(hipMemsetAsync(kc_of(e, il), 0, (size_t)c.n_ctx * e->kvw * 2, s));
+        GHIP_CHECK(hipMemsetAsync(vc_of(e, il), 0, (size_t)c.n_ctx * e->kvw * 2, s));
+    }
     GHIP_CHECK(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
     GHIP_CHECK(hipMemcpyAsync(e->hist, prompt, (size_t)n_prompt * 4, hipMemcpyHostToDevice, s));
     GHIP_CHECK(hipMemsetAsync(e->pos, 0, 4, s));
@@ -1548,7 +1557,7 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
         if (gemm(L.qkv, EPI_STORE, nullptr, p.QKV, e->qkv_rows)) return -1;
         ropekv_args r;
         r.qkv = p.QKV; r.ldqkv = e->qkv_rows; r.rope_cos = e->rope_cos; r.rope_sin = e->rope_sin; r.q16 = p.Q16;
-        r.kc = e->kc + (size_t)il * c.n_ctx * e->kvw; r.vc = e->vc + (size_t)il * c.n_ctx * e->kvw;
+        r.kc = kc_of(e, il); r.vc = vc_of(e, il);
         r.H = c.n_head; r.Hkv = c.n_head_kv; r.hd = c.head_dim; r.ctx = c.n_ctx; r.p0 = 0;
         r.q_scale = 1.0f / sqrtf((float)c.head_dim);
         if (launch_rope_kv_prefill(r, T, s)) return -1;
@@ -1830,4 +1839,60 @@ extern "C" int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps, int 
     (void)hipFree(d);
     if (r == 0) e->host_pos = T;
     return r;
+}
+
+// ---- the ggml executor's fast path (engine_ext.h) ------------------------------------------------
+gemma_engine *gemma_engine_create_ext(const gemma_hip_config *cfg, int device, const host_weights &hw,
+                                      const std::vector<uint16_t *> &kc, const std::vector<uint16_t *> &vc) {
+    if ((int)kc.size() != cfg->n_layer || (int)vc.size() != cfg->n_layer) {
+        set_error("gemma_engine_create_ext: one K and one V cache per layer");
+        return nullptr;
+    }
+    return engine_create(cfg, device, 1, 0, nullptr, &hw, &kc, &vc);
+}
+
+// the device state a decode step reads: hist[pos] = token, *pos, the RoPE row of pos (k_advance
+// publishes it between steps of a device-fed sequence; here the host feeds every token)
+static int ext_set_position(gemma_engine *e, int token, int pos) {
+    const gemma_hip_config &c = e->cfg;
+    rope_row rr;
+    rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+    // n_fixed past the history: k_advance must not overwrite hist (the host supplies every token)
+    return launch_set_position(token, pos, e->pos, e->hist, e->nfix, c.n_ctx + 1, rr, e->stream);
+}
+
+int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) {
+    set_error("");
+    const gemma_hip_config &c = e->cfg;
+    if (pos < 0 || pos + 1 >= c.n_ctx || token < 0 || token >= c.n_vocab) {
+        set_error("gemma_engine_ext_decode: token or position out of range");
+        return -1;
+    }
+    (void)hipSetDevice(e->device);
+    if (ext_set_position(e, token, pos)) return -1;
+    if (!e->graph_exec) {  // first step eager (sets the kernels' LDS attributes), then capture
+        if (enqueue_step(e)) return -1;
+        if (ensure_graph(e)) return -1;
+    } else {
+        GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
+    }
+    // logits through a pinned staging row (a pageable device-to-host copy stages through the driver)
+    const size_t lb = (size_t)c.n_vocab * 4;
+    if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, lb, hipHostMallocDefault));
+    GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
+    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    memcpy(logits, e->ext_stage, lb);
+    e->host_pos = pos + 1;
+    return 0;
+}
+
+int gemma_engine_ext_prefill(gemma_engine *e, const int32_t *tokens, int T, float *logits_all) {
+    if (gemma_engine_begin(e, tokens, T)) return -1;
+    if (e->kq || e->cfg.wtype == T_Q4_K) {  // K-quant layers: token by token
+        for (int i = 0; i < T; ++i)
+            if (gemma_engine_ext_decode(e, tokens[i], i, logits_all + (size_t)i * e->cfg.n_vocab)) return -1;
+        return 0;
+    }
+    std::vector<float> last(e->cfg.n_vocab);
+    return gemma_engine_prefill(e, last.data(), logits_all) < 0 ? -1 : 0;
 }

@@ -22,6 +22,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <chrono>
+#include <cmath>
 #include <map>
 #include <mutex>
 #include <set>
@@ -31,6 +34,7 @@
 #include <vector>
 
 #include "../../include/gemma_hpc.h"
+#include "engine_ext.h"
 #include "ggml_impl.h"
 #include "kernels.h"
 
@@ -415,6 +419,255 @@ int run_node(run_state &rs, ggml_tensor *n) {
     }
 }
 
+// ---- the Gemma graph fast path -------------------------------------------------------------------
+// build_compute_graph (src/gemma_model.cpp:665-747) emits one fixed graph per call.  When the graph
+// handed to the executor is exactly that graph (verified op by op, every parameter, and the host
+// inputs: tokens, positions, the causal mask, the KV write position), it runs on the
+// device-resident engine (fused kernels, one hipGraph per decode token, engine.cpp) over the same
+// host weights and over the executor's own device mirrors of the graph's KV-cache tensors, and the
+// last node's logits are copied back like the generic path does.  Same arithmetic, same bits
+// (tests/test_gpu_ggml_graph.py runs both paths).  Anything else runs node by node below.
+struct gemma_match {
+    gemma_hip_config cfg{};
+    host_weights hw;
+    std::vector<ggml_tensor *> kc, vc;  // cache roots per layer
+    std::vector<int32_t> tokens;
+    int T = 0;
+    int pos0 = 0;
+};
+
+bool op_is(const ggml_tensor *t, int op) { return t && t->op == op; }
+bool is_leaf_w(const ggml_tensor *t) { return t && t->op == GGML_OP_NONE && !t->view_src && t->data; }
+const ggml_tensor *skip_views(const ggml_tensor *t) {  // through RESHAPE / VIEW / PERMUTE / TRANSPOSE
+    while (t && (t->op == GGML_OP_RESHAPE || t->op == GGML_OP_VIEW || t->op == GGML_OP_PERMUTE || t->op == GGML_OP_TRANSPOSE))
+        t = t->src[0];
+    return t;
+}
+
+// norm * w: MUL(RMS_NORM(x), w) -> x, w, eps
+bool match_norm(const ggml_tensor *t, const ggml_tensor **x, const float **w, float *eps) {
+    if (!op_is(t, GGML_OP_MUL) || !op_is(t->src[0], GGML_OP_RMS_NORM) || !is_leaf_w(t->src[1]) ||
+        t->src[1]->type != GGML_TYPE_F32)
+        return false;
+    *x = t->src[0]->src[0];
+    *w = (const float *)t->src[1]->data;
+    *eps = get_f32(t->src[0], 0);
+    return true;
+}
+
+bool match_gemma(ggml_cgraph *g, gemma_match &m, std::string &why) {
+    auto fail = [&](const char *w) {
+        why = w;
+        return false;
+    };
+    const ggml_tensor *last = g->nodes[g->n_nodes - 1];
+    if (!op_is(last, GGML_OP_MUL_MAT) || !is_leaf_w(last->src[0])) return fail("last node");
+    const ggml_tensor *embd = last->src[0];
+    const ggml_tensor *x;
+    const float *onorm;
+    float eps;
+    if (!match_norm(last->src[1], &x, &onorm, &eps)) return fail("output norm");
+    gemma_hip_config &c = m.cfg;
+    c.n_embd = (int)embd->ne[0];
+    c.n_vocab = (int)embd->ne[1];
+    c.eps = eps;
+    m.hw.embd = embd->data;
+    m.hw.out_norm = onorm;
+    // cache stores: root -> the CPY node writing it
+    std::unordered_map<const ggml_tensor *, const ggml_tensor *> store;
+    for (int i = 0; i < g->n_nodes; ++i)
+        if (op_is(g->nodes[i], GGML_OP_CPY)) store[root_of(g->nodes[i]->src[1])] = g->nodes[i];
+    std::vector<host_weights::layer> rev;
+    const ggml_tensor *posv = nullptr, *maskv = nullptr;
+    int wtype = -1, hd = 0, H = 0, Hkv = 0, nff = 0, kvhead = -1, gclamp = -1;
+    float base = 0.f;
+    while (op_is(x, GGML_OP_ADD)) {
+        host_weights::layer L;
+        // x = down(gelu(gate(n2)) * up(n2)) + sa
+        const ggml_tensor *dn = x->src[0], *sa = x->src[1];
+        if (!op_is(dn, GGML_OP_MUL_MAT) || !is_leaf_w(dn->src[0]) || !op_is(dn->src[1], GGML_OP_MUL)) return fail("ffn down");
+        const ggml_tensor *gm = dn->src[1];
+        if (!op_is(gm->src[0], GGML_OP_GELU) || !op_is(gm->src[1], GGML_OP_MUL_MAT)) return fail("gelu*up");
+        const ggml_tensor *gt = gm->src[0]->src[0], *ut = gm->src[1];
+        if (!op_is(gt, GGML_OP_MUL_MAT) || !is_leaf_w(gt->src[0]) || !is_leaf_w(ut->src[0]) || gt->src[1] != ut->src[1])
+            return fail("gate/up");
+        const int gc = gm->src[0]->op_params[0];
+        if (gclamp >= 0 && gc != gclamp) return fail("gelu variants");
+        gclamp = gc;
+        const ggml_tensor *sx;
+        if (!match_norm(gt->src[1], &sx, &L.ffn_norm, &eps) || sx != sa || eps != c.eps) return fail("ffn norm");
+        L.gate = gt->src[0]->data; L.up = ut->src[0]->data; L.down = dn->src[0]->data;
+        nff = (int)gt->src[0]->ne[1];
+        // sa = Wo(cont(permute(kqv))) + inpL
+        if (!op_is(sa, GGML_OP_ADD) || !op_is(sa->src[0], GGML_OP_MUL_MAT) || !is_leaf_w(sa->src[0]->src[0])) return fail("attn out");
+        L.o = sa->src[0]->src[0]->data;
+        const ggml_tensor *inp = sa->src[1];
+        const ggml_tensor *cont = sa->src[0]->src[1];
+        if (!op_is(cont, GGML_OP_CONT) || !op_is(cont->src[0], GGML_OP_PERMUTE)) return fail("kqv merge");
+        const ggml_tensor *kqv = cont->src[0]->src[0];
+        if (!op_is(kqv, GGML_OP_MUL_MAT) || !op_is(kqv->src[0], GGML_OP_VIEW) || !op_is(kqv->src[1], GGML_OP_SOFT_MAX))
+            return fail("kqv");
+        const ggml_tensor *sm = kqv->src[1];
+        if (sm->src[2] || get_f32(sm, 0) != 1.0f || get_f32(sm, 1) != 0.0f || !op_is(sm->src[1], GGML_OP_VIEW)) return fail("softmax");
+        if (maskv && sm->src[1] != maskv) return fail("mask");
+        maskv = sm->src[1];
+        const ggml_tensor *kq = sm->src[0];
+        if (!op_is(kq, GGML_OP_MUL_MAT) || !op_is(kq->src[0], GGML_OP_VIEW) || !op_is(kq->src[1], GGML_OP_PERMUTE)) return fail("kq");
+        const ggml_tensor *qs = kq->src[1]->src[0];
+        if (!op_is(qs, GGML_OP_SCALE) || !op_is(qs->src[0], GGML_OP_ROPE)) return fail("q scale");
+        const ggml_tensor *qr = qs->src[0];
+        const ggml_tensor *qm = skip_views(qr->src[0]);
+        if (!op_is(qm, GGML_OP_MUL_MAT) || !is_leaf_w(qm->src[0])) return fail("q proj");
+        const ggml_tensor *n1 = qm->src[1];
+        const ggml_tensor *n1x;
+        if (!match_norm(n1, &n1x, &L.attn_norm, &eps) || n1x != inp || eps != c.eps) return fail("attn norm");
+        L.q = qm->src[0]->data;
+        hd = (int)qr->ne[0];
+        H = (int)qr->ne[1];
+        if (qr->op_params[1] != hd || qr->op_params[2] != 2 || get_f32(qr, 6) != 1.0f || get_f32(qr, 7) != 0.0f ||
+            get_f32(qr, 8) != 1.0f)
+            return fail("rope params");
+        if (get_f32(qs, 0) != 1.0f / sqrtf((float)hd)) return fail("q scale value");
+        if (posv && qr->src[1] != posv) return fail("positions");
+        posv = qr->src[1];
+        base = get_f32(qr, 5);
+        // caches and their stores
+        const ggml_tensor *kroot = root_of((ggml_tensor *)kq->src[0]), *vroot = root_of((ggml_tensor *)kqv->src[0]);
+        auto ks = store.find(kroot), vs = store.find(vroot);
+        if (ks == store.end() || vs == store.end()) return fail("kv store");
+        const ggml_tensor *kr = ks->second->src[0];  // rope(reshape(k proj))
+        if (!op_is(kr, GGML_OP_ROPE) || kr->src[1] != posv || kr->op_params[2] != 2 || get_f32(kr, 5) != base) return fail("k rope");
+        const ggml_tensor *km = skip_views(kr->src[0]);
+        const ggml_tensor *vm = skip_views(vs->second->src[0]);
+        if (!op_is(km, GGML_OP_MUL_MAT) || km->src[1] != n1 || !op_is(vm, GGML_OP_MUL_MAT) || vm->src[1] != n1) return fail("k/v proj");
+        L.k = km->src[0]->data;
+        L.v = vm->src[0]->data;
+        Hkv = (int)kr->ne[1];
+        const int64_t kvw = (int64_t)Hkv * hd;
+        if (kroot->type != GGML_TYPE_F16 || vroot->type != GGML_TYPE_F16 || ggml_nelements(kroot) % kvw) return fail("cache type");
+        const int64_t off_k = (int64_t)((char *)ks->second->src[1]->data - (char *)kroot->data);
+        const int kh = (int)(off_k / (kvw * 2));
+        if (kvhead >= 0 && kh != kvhead) return fail("kv head");
+        kvhead = kh;
+        const int types[7] = {(int)qm->src[0]->type, (int)km->src[0]->type, (int)vm->src[0]->type, (int)sa->src[0]->src[0]->type,
+                              (int)gt->src[0]->type, (int)ut->src[0]->type, (int)dn->src[0]->type};
+        for (int t : types)
+            if (t != types[0] || (wtype >= 0 && t != wtype)) return fail("mixed layer types");
+        wtype = types[0];
+        rev.push_back(L);
+        m.kc.push_back((ggml_tensor *)kroot);
+        m.vc.push_back((ggml_tensor *)vroot);
+        x = inp;
+    }
+    // x0 = get_rows(token_embd, tokens) * sqrt(E)
+    if (!op_is(x, GGML_OP_SCALE) || !op_is(x->src[0], GGML_OP_GET_ROWS) || x->src[0]->src[0] != embd ||
+        get_f32(x, 0) != sqrtf((float)c.n_embd))
+        return fail("embedding");
+    if (rev.empty() || !posv || !maskv) return fail("no layers");
+    std::reverse(rev.begin(), rev.end());
+    std::reverse(m.kc.begin(), m.kc.end());
+    std::reverse(m.vc.begin(), m.vc.end());
+    m.hw.layers = rev;
+    if (wtype != GGML_TYPE_Q4_0 && wtype != GGML_TYPE_Q8_0) return fail("layer type (fast path: Q4_0 / Q8_0)");
+    if ((int)embd->type != wtype && embd->type != GGML_TYPE_Q6_K) return fail("token_embd type");
+    c.n_layer = (int)rev.size();
+    c.n_head = H; c.n_head_kv = Hkv; c.head_dim = hd; c.n_ff = nff;
+    c.n_ctx = (int)(ggml_nelements(m.kc[0]) / ((int64_t)Hkv * hd));
+    c.wtype = wtype;
+    c.out_type = embd->type == GGML_TYPE_Q6_K ? T_Q6_K : 0;
+    c.rope_base = base;
+    c.gelu_clamp = gclamp;
+    // host inputs: tokens, positions, mask (the engine derives the causal mask and n_kv itself)
+    const ggml_tensor *tok = x->src[0]->src[1];
+    m.T = (int)tok->ne[0];
+    if (tok->type != GGML_TYPE_I32 || posv->ne[0] != m.T || posv->type != GGML_TYPE_I32) return fail("inputs");
+    m.tokens.assign((const int32_t *)tok->data, (const int32_t *)tok->data + m.T);
+    const int32_t *pv = (const int32_t *)posv->data;
+    m.pos0 = pv[0];
+    for (int i = 0; i < m.T; ++i)
+        if (pv[i] != m.pos0 + i) return fail("positions not consecutive");
+    if (m.T > 1 && m.pos0 != 0) return fail("multi-token graph not starting at 0");
+    if (kvhead != m.pos0) return fail("kv head != position");
+    const int64_t kv_n = maskv->ne[0];
+    if (kv_n != std::min<int64_t>(c.n_ctx, 32 * ((m.pos0 + m.T) / 32 + 1)) || maskv->ne[1] != m.T || maskv->type != GGML_TYPE_F32)
+        return fail("n_kv");
+    for (int i = 0; i < m.T; ++i) {
+        const float *row = (const float *)((const char *)maskv->data + (size_t)i * maskv->nb[1]);
+        for (int64_t j = 0; j < kv_n; ++j) {
+            const bool masked = j > m.pos0 + i;
+            if (masked ? !(row[j] == -INFINITY) : row[j] != 0.0f) return fail("mask not causal");
+        }
+    }
+    if (last->ne[1] != m.T || !last->data || !is_contiguous(last)) return fail("output rows");
+    return true;
+}
+
+struct fast_engine {
+    gemma_engine *e = nullptr;
+    const void *key_embd = nullptr, *key_q0 = nullptr;
+    int n_ctx = 0, n_layer = 0;
+    std::vector<const void *> kv_keys;
+};
+fast_engine &fast() {
+    static fast_engine f;
+    return f;
+}
+
+// 1 = ran on the engine, 0 = not the Gemma graph (run generically), -1 = error
+double now_us() {
+    return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e-3;
+}
+
+int try_fast(ggml_cgraph *g) {
+    static const bool on = !getenv("GHIP_GGML_FAST") || atoi(getenv("GHIP_GGML_FAST"));
+    static const bool prof = getenv("GHIP_GGML_FAST_PROF") != nullptr;
+    if (!on || g->n_nodes < 8) return 0;
+    const double t0 = prof ? now_us() : 0.0;
+    gemma_match m;
+    std::string why;
+    if (!match_gemma(g, m, why)) {
+        if (getenv("GHIP_GGML_FAST_WHY")) fprintf(stderr, "[gemma_hip] ggml fast path not taken: %s\n", why.c_str());
+        return 0;
+    }
+    executor &ex_ = ex();
+    // the caches' device mirrors (device-authoritative: the graph writes them)
+    std::vector<uint16_t *> kc, vc;
+    std::vector<const void *> kv_keys;
+    for (int il = 0; il < m.cfg.n_layer; ++il) {
+        if (sync_leaf(m.kc[il], true) || sync_leaf(m.vc[il], true)) return -1;
+        kc.push_back((uint16_t *)ex_.leaves[m.kc[il]->data].dev);
+        vc.push_back((uint16_t *)ex_.leaves[m.vc[il]->data].dev);
+        kv_keys.push_back(kc.back());
+        kv_keys.push_back(vc.back());
+    }
+    GHIP_CHECK(hipStreamSynchronize(ex_.stream));
+    fast_engine &f = fast();
+    if (!f.e || f.key_embd != m.hw.embd || f.key_q0 != m.hw.layers[0].q || f.n_ctx != m.cfg.n_ctx ||
+        f.n_layer != m.cfg.n_layer || f.kv_keys != kv_keys) {
+        if (f.e) gemma_engine_free(f.e);
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        f.e = gemma_engine_create_ext(&m.cfg, dev, m.hw, kc, vc);
+        if (!f.e) return -1;
+        f.key_embd = m.hw.embd;
+        f.key_q0 = m.hw.layers[0].q;
+        f.n_ctx = m.cfg.n_ctx;
+        f.n_layer = m.cfg.n_layer;
+        f.kv_keys = kv_keys;
+    }
+    ggml_tensor *last = g->nodes[g->n_nodes - 1];
+    const double t1 = prof ? now_us() : 0.0;
+    const int rc = m.T == 1 ? gemma_engine_ext_decode(f.e, m.tokens[0], m.pos0, (float *)last->data)
+                            : gemma_engine_ext_prefill(f.e, m.tokens.data(), m.T, (float *)last->data);
+    if (rc) return -1;
+    if (prof) fprintf(stderr, "[gemma_hip] fast path T=%d: match+sync %.1f us, engine %.1f us\n", m.T, t1 - t0, now_us() - t1);
+    for (int il = 0; il < m.cfg.n_layer; ++il) {
+        ex_.leaves[m.kc[il]->data].valid = true;
+        ex_.leaves[m.vc[il]->data].valid = true;
+    }
+    return 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -454,6 +707,7 @@ void ggml_free(struct ggml_context *ctx) {
     }
     for (ggml_tensor *t : ctx->tensors) delete t;
     for (ggml_cgraph *g : ctx->graphs) {
+        delete (std::unordered_set<ggml_tensor *> *)g->visited;
         delete[] g->nodes;
         delete[] g->leafs;
         delete g;
@@ -669,6 +923,7 @@ struct ggml_cgraph *ggml_new_graph(struct ggml_context *ctx) {
     g->leafs = new ggml_tensor *[kGraphSize];
     g->grads = nullptr;
     g->n_nodes = g->n_leafs = 0;
+    g->visited = new std::unordered_set<ggml_tensor *>();
     ctx->graphs.push_back(g);
     return g;
 }
@@ -689,10 +944,9 @@ static void visit(ggml_cgraph *g, std::unordered_set<ggml_tensor *> &seen, ggml_
 }
 
 void ggml_build_forward_expand(struct ggml_cgraph *g, struct ggml_tensor *t) {
-    std::unordered_set<ggml_tensor *> seen;
-    for (int i = 0; i < g->n_nodes; ++i) seen.insert(g->nodes[i]);
-    for (int i = 0; i < g->n_leafs; ++i) seen.insert(g->leafs[i]);
-    visit(g, seen, t);
+    // the graph keeps its visited set: rebuilding it from nodes + leafs on every call made the
+    // reference's per-layer expands quadratic (~2.5 ms of host time per Gemma-2B decode graph)
+    visit(g, *(std::unordered_set<ggml_tensor *> *)g->visited, t);
 }
 
 enum ggml_status ggml_graph_compute_with_ctx(struct ggml_context *ctx, struct ggml_cgraph *g, int n_threads) {
@@ -703,6 +957,8 @@ enum ggml_status ggml_graph_compute_with_ctx(struct ggml_context *ctx, struct gg
     set_error("");
     if (ensure_init()) return GGML_STATUS_FAILED;
     if (g->n_nodes == 0) return GGML_STATUS_SUCCESS;
+    const int fr = try_fast(g);  // the Gemma graph: the device-resident engine
+    if (fr != 0) return fr > 0 ? GGML_STATUS_SUCCESS : GGML_STATUS_FAILED;
     // leaves the graph writes into (ggml_cpy destinations): device-authoritative
     std::unordered_set<const void *> written;
     for (int i = 0; i < g->n_nodes; ++i)

@@ -245,6 +245,7 @@ struct rope_row {  // k_advance also publishes the new position's RoPE row: cur 
 int launch_mall_warm(const void *const *ptrs, const int64_t *bytes, int n, int grid, hipStream_t s);
 int launch_advance(const unsigned long long *keys, int n_parts, int *token, int *pos, int *hist, int hist_cap,
                    const int *n_fixed, const rope_row &r, hipStream_t s);
+int launch_set_position(int token, int p, int *pos, int *hist, int *n_fixed, int fixed, const rope_row &r, hipStream_t s);
 
 // ---- generic ggml-op kernels used by the C-ABI and the ggml-compatible executor ----------------
 int launch_mul_mat_f16(const uint16_t *src0, int64_t nb01_elems, int64_t ne01, const uint16_t *src1,

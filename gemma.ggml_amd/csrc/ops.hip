@@ -700,6 +700,23 @@ __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys,
     }
 }
 
+// host-fed position (the ggml executor's engine path): hist[p] = token, *pos = p, *n_fixed past the
+// history (k_advance leaves hist alone), the RoPE row of p — kernel arguments instead of four
+// pageable host copies
+__global__ void __launch_bounds__(256) k_set_position(int token, int p, int *pos, int *hist, int *n_fixed, int fixed,
+                                                      rope_row r) {
+    if (threadIdx.x == 0) {
+        hist[p] = token;
+        *pos = p;
+        *n_fixed = fixed;
+        ((int *)r.cur)[2 * r.half] = p;
+    }
+    for (int i = threadIdx.x; i < r.half; i += 256) {
+        r.cur[i] = r.cos[(int64_t)p * r.half + i];
+        r.cur[r.half + i] = r.sin[(int64_t)p * r.half + i];
+    }
+}
+
 // C-ABI F16 mul_mat (KQ/KQV shapes): one thread per (row, col), vec_dot_f16 order
 __global__ void k_mul_mat_f16(const uint16_t *src0, int64_t nb01e, int64_t ne01, const uint16_t *src1, int64_t rse,
                               int64_t ncols, int64_t K, float *dst) {
@@ -877,6 +894,12 @@ int launch_mall_warm(const void *const *ptrs, const int64_t *bytes, int n, int g
 int launch_advance(const unsigned long long *keys, int n_parts, int *token, int *pos, int *hist, int hist_cap,
                    const int *n_fixed, const rope_row &r, hipStream_t s) {
     hipLaunchKernelGGL(k_advance, dim3(1), dim3(256), 0, s, keys, n_parts, token, pos, hist, hist_cap, n_fixed, r);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_set_position(int token, int p, int *pos, int *hist, int *n_fixed, int fixed, const rope_row &r, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_position, dim3(1), dim3(256), 0, s, token, p, pos, hist, n_fixed, fixed, r);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -124,6 +124,7 @@ struct ggml_cgraph {
     struct ggml_tensor **nodes;
     struct ggml_tensor **grads;
     struct ggml_tensor **leafs;
+    void *visited; /* the graph's visited-node set (ggml's visited_hash_table role): O(1) per expand */
 };
 
 typedef struct ggml_backend_buffer_type *ggml_backend_buffer_type_t;

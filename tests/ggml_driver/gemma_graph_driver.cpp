@@ -356,20 +356,29 @@ int main(int argc, char **argv) {
     std::vector<float> row;
     // timing as begin_one_round_inference reports it (src/gemma_model.cpp:552-572): prefill, then decode
     auto now = [] { return std::chrono::steady_clock::now(); };
+    const bool bench = getenv("DRIVER_BENCH") && atoi(getenv("DRIVER_BENCH"));
     auto t_start = now(), t_prefill = t_start;
     for (int step = 0; step <= n_decode; ++step) {  // inference (:231-286)
         if (step == 1) t_prefill = now();
         const stage st = step == 0 ? PREFILL : DECODE;
+        const auto p0 = now();
         update_kv_cache(m, input, st);
         load_input_tokens_to_tensor(m, input, st);
         ggml_cgraph *g = build_compute_graph(m, input, st);
+        const auto p1 = now();
         // src/gemma_model.cpp:237 calls ggml_graph_compute_with_ctx; hpc_graph_compute is the same executor
         if (ggml_graph_compute_with_ctx(m.compute_ctx, g, 1) != GGML_STATUS_SUCCESS) {
             fprintf(stderr, "graph compute failed\n");
             return 1;
         }
+        const auto p2 = now();
         const int32_t t = greedy_sample(g->nodes[g->n_nodes - 1], row);
-        fwrite(row.data(), 4, row.size(), out);
+        const auto p3 = now();
+        if (getenv("DRIVER_PROF"))
+            fprintf(stderr, "step %d: build %.1f us compute %.1f us sample %.1f us\n", step,
+                    std::chrono::duration<double, std::micro>(p1 - p0).count(), std::chrono::duration<double, std::micro>(p2 - p1).count(),
+                    std::chrono::duration<double, std::micro>(p3 - p2).count());
+        if (!bench) fwrite(row.data(), 4, row.size(), out);  // (bench mode: the timed loop is the reference's)
         toks.push_back(t);
         input.push_back(t);
     }

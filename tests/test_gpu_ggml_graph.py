@@ -69,7 +69,9 @@ def write_gguf(m, shape, path, kmix):
     w.write(str(path))
 
 
-def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0):
+def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fast=1):
+    """fast=1: the executor recognises the Gemma graph and runs the device-resident engine over the
+    graph's weights and KV-cache mirrors (ggml_api.cpp try_fast); fast=0: node by node."""
     m = O.Model(O.make_config(shape, n_ctx=ctx, wtype=wtype, kmix=kmix))
     wpath, ppath, opath = tmp_path / ("m.gguf" if gguf else "w.bin"), tmp_path / "p.bin", tmp_path / "o.bin"
     if gguf:
@@ -89,8 +91,11 @@ def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0):
         args = [DRIVER, str(wpath), str(ppath), str(opath)] + [str(shape[k]) for k in
                 ("n_layer", "n_embd", "n_head", "n_head_kv", "head_dim", "n_ff", "n_vocab")] + [str(ctx), str(wtype),
                                                                                               str(n_decode)]
-    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, GHIP_GGML_FAST=str(fast), GHIP_GGML_FAST_WHY="1")
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
+    if fast and not kmix:  # the Gemma graph must take the engine path (K-quant layers: node by node)
+        assert "fast path not taken" not in r.stderr, r.stderr[-500:]
     raw = np.fromfile(opath, dtype=np.float32)
     V = shape["n_vocab"]
     logits = raw[: (n_decode + 1) * V].reshape(n_decode + 1, V)
@@ -115,33 +120,39 @@ def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0):
 
 
 @gpu
-def test_ggml_graph_tiny_q4_0(tmp_path):
-    _run(tmp_path, dict(O.TINY), O.Q4_0, 20, 4, 128)
+@pytest.mark.parametrize("fast", [1, 0])
+def test_ggml_graph_tiny_q4_0(tmp_path, fast):
+    _run(tmp_path, dict(O.TINY), O.Q4_0, 20, 4, 128, fast=fast)
 
 
 @gpu
-def test_ggml_graph_gqa_q8_0(tmp_path):
-    _run(tmp_path, dict(O.TINY, n_head=4, n_head_kv=2), O.Q8_0, 37, 3, 128)
+@pytest.mark.parametrize("fast", [1, 0])
+def test_ggml_graph_gqa_q8_0(tmp_path, fast):
+    _run(tmp_path, dict(O.TINY, n_head=4, n_head_kv=2), O.Q8_0, 37, 3, 128, fast=fast)
 
 
 @gpu
-def test_ggml_graph_gemma2b_layers(tmp_path):
+@pytest.mark.parametrize("fast", [1, 0])
+def test_ggml_graph_gemma2b_layers(tmp_path, fast):
     shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
-    _run(tmp_path, shape, O.Q4_0, 40, 2, 128)
+    _run(tmp_path, shape, O.Q4_0, 40, 2, 128, fast=fast)
 
 
 @gpu
-def test_ggml_graph_gguf_q4_0(tmp_path):
-    _run(tmp_path, dict(O.TINY), O.Q4_0, 20, 4, 128, gguf=True)
+@pytest.mark.parametrize("fast", [1, 0])
+def test_ggml_graph_gguf_q4_0(tmp_path, fast):
+    _run(tmp_path, dict(O.TINY), O.Q4_0, 20, 4, 128, gguf=True, fast=fast)
 
 
 @gpu
-def test_ggml_graph_gguf_kquant_mix_tiny(tmp_path):
+@pytest.mark.parametrize("fast", [1, 0])
+def test_ggml_graph_gguf_kquant_mix_tiny(tmp_path, fast):
     shape = dict(n_layer=2, n_embd=256, n_head=2, n_head_kv=1, head_dim=128, n_ff=512, n_vocab=1024)
-    _run(tmp_path, shape, O.Q4_0, 23, 4, 128, gguf=True, kmix=1)
+    _run(tmp_path, shape, O.Q4_0, 23, 4, 128, gguf=True, kmix=1, fast=fast)
 
 
 @gpu
-def test_ggml_graph_gguf_kquant_mix_gemma2b_layers(tmp_path):
+@pytest.mark.parametrize("fast", [1, 0])
+def test_ggml_graph_gguf_kquant_mix_gemma2b_layers(tmp_path, fast):
     shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
-    _run(tmp_path, shape, O.Q4_0, 33, 2, 128, gguf=True, kmix=1)
+    _run(tmp_path, shape, O.Q4_0, 33, 2, 128, gguf=True, kmix=1, fast=fast)
