@@ -10,6 +10,7 @@
 
 #include "device_util.h"
 #include "kernels.h"
+#include "q8k.h"
 
 namespace ghip {
 namespace {
@@ -364,7 +365,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         const float o = quad_reduce_f16(acc);
         if (t4 == 0) {
             a.out[(int64_t)h * hd + d] = o;
-            if (a.out_act) ((float *)smem)[d] = o;  // q16|k16 (hd floats) are dead after KQ
+            if (a.out_act || a.out_q8k) ((float *)smem)[d] = o;  // q16|k16 (hd floats) are dead after KQ
         }
     }
     if (a.out_act) {
@@ -378,6 +379,16 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             for (int j = 0; j < 8; ++j) v[j] = o[j];
             if (SC1) image_put_quad_sc1(a.out_act, a.out_da, (int64_t)h * (hd / 32) + (tid >> 2), tid & 3, v);
             else image_put_quad(a.out_act, nullptr, a.out_da, (int64_t)h * (hd / 32) + (tid >> 2), tid & 3, v);
+        }
+    }
+    if (a.out_q8k) {
+        // this head's 256 outputs are one Q8_K super-block of `out` (the K-quant attn-out's INIT,
+        // quantize_row_q8_K as k_quant_q8_K runs it); launch_attn_decode checks hd == 256
+        __syncthreads();
+        if (tid < 64) {
+            const float4 v = *(const float4 *)((const float *)smem + tid * 4);
+            const float xv[4] = {v.x, v.y, v.z, v.w};
+            q8K_store(xv, tid, a.out_q8k + (int64_t)h * 292);
         }
     }
     AH_STAMP(4);

@@ -189,6 +189,12 @@ struct gemma_engine {
     bool kq = false;              // K-quant layers (kql) instead of the tiled Q4_0 / Q8_0 ones
     std::vector<kq_layer> kql;
     uint8_t *kq_x = nullptr;      // Q8_K INIT of the current matvec input (max(E, qw, F) / 256 blocks)
+    // hand-off mode (kq_fuse == 2): the Q8_K images each producer writes for its consumer, one
+    // buffer per hand-off so no launch overwrites the image it reads (kq_x = the attn-norm image,
+    // kq_xa = attention output, kq_xf = ffn-norm image, kq_xh = gelu(gate)*up); counters zeroed once
+    uint8_t *kq_xa = nullptr, *kq_xf = nullptr, *kq_xh = nullptr;
+    unsigned *kq_cnt = nullptr;
+    int kq_cnt_cap = 0;
     float *kq_g = nullptr;        // ffn gate output (n_ff), consumed by the up matvec's gelu*mul epilogue
     uint8_t *embd_q6k = nullptr;
     int64_t embd_row_bytes = 0;
@@ -219,6 +225,11 @@ struct gemma_engine {
     // (DESIGN.md §Activation image); null when a shape does not allow them (then PRO_F32)
     // fused layer front (layer_front.hip): qkv -> attention -> attn-out in one launch per layer;
     // hand-off counters [n_layer][16] zeroed once per token (memset node), sticky timeout word
+    // K-quant layers: kq_fuse = the plan for where ggml's Q8_K INIT runs (enqueue_step_kq: 0 launches,
+    // 1 consumer prologues, 2 producer hand-offs, 3 norms in prologues + quantizations handed off);
+    // kq_dual: gate+up in one launch
+    int kq_fuse = 3, kq_dual = 1;
+    int kq_abl = 0;  // GHIP_KQ_ABL: hand-off timing ablation (kq_args::q8_abl; wrong results)
     int fuse_front = 0;  // measured: 727 vs 672 us/token (the in-launch hand-offs cost as much as the
                          // launch boundaries they replace; DESIGN.md perf log) — kept as an option
     unsigned *front_cnt = nullptr;
@@ -540,26 +551,75 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
     const gemma_hip_config &c = e->cfg;
     hipStream_t s = e->stream;
     const int E = c.n_embd;
-    auto mv = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in) {
+    // Where ggml's Q8_K INIT of each matvec input runs (all write the same bytes):
+    //   LAUNCH   a k_norm_q8K / k_quant_q8_K launch;
+    //   PROLOGUE the consumer's prologue from f32 (KQP_NORM / KQP_F32, every workgroup);
+    //   HANDOFF  the producer's tail (kq_handoff; attention: each head's super-block).
+    // Images: A = attn-norm(x) -> q|k, v; B = attention out -> o; C = ffn-norm(sa) -> gate/up;
+    // D = gelu(gate)*up -> down; each in its own buffer.  e->kq_fuse picks the plan:
+    //   0 all LAUNCH; 1 all PROLOGUE; 2 all HANDOFF (measured: the norm tails cost more than a
+    //   launch); 3 (default) norms PROLOGUE, quantizations HANDOFF.
+    enum { LAUNCH, PROLOGUE, HANDOFF };
+    static const int plan[4][4] = {{LAUNCH, LAUNCH, LAUNCH, LAUNCH},
+                                   {PROLOGUE, PROLOGUE, PROLOGUE, PROLOGUE},
+                                   {HANDOFF, HANDOFF, HANDOFF, HANDOFF},
+                                   {PROLOGUE, HANDOFF, PROLOGUE, HANDOFF}};
+    const int mode = e->kq_fuse >= 0 && e->kq_fuse <= 3 ? e->kq_fuse : 3;
+    int srcA = plan[mode][0], srcB = plan[mode][1], srcC = plan[mode][2], srcD = plan[mode][3];
+    if (E > 2048) {  // the norm hand-off holds <= 2048 values in one wave
+        if (srcA == HANDOFF) srcA = PROLOGUE;
+        if (srcC == HANDOFF) srcC = PROLOGUE;
+    }
+    if (srcB == HANDOFF && !(e->att_mode == ATTN_PER_HEAD && c.head_dim == 256)) srcB = LAUNCH;
+    struct img {
+        int src;
+        uint8_t *x;  // the Q8_K image (LAUNCH / HANDOFF)
+        int pro;     // PROLOGUE: mode and f32 input
+        const float *xf, *norm_w;
+    };
+    struct out {
+        int mode = KQO_NONE;  // a HANDOFF this launch writes
+        uint8_t *q8 = nullptr;
+        const float *norm = nullptr;
+    };
+    auto mv = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in, const img &in, const out &o,
+                  const kq_mat *up) {
         kq_args k;
         k.w = W.w; k.row_bytes = W.rb; k.rows = W.rows; k.nsb = (int)(W.K / 256);
-        k.x = e->kq_x; k.x_col_stride = (W.K / 256) * 292; k.y = y; k.y_col_stride = W.rows; k.ncols = 1;
+        k.x = in.x; k.x_col_stride = (W.K / 256) * 292; k.y = y; k.y_col_stride = W.rows; k.ncols = 1;
         k.resid = resid; k.gate_in = gate_in; k.gelu_tab = e->gelu_tab; k.gelu_clamp = c.gelu_clamp;
+        k.eps = c.eps;
+        if (in.src == PROLOGUE) {
+            k.pro = in.pro; k.xf = in.xf; k.xf_col_stride = W.K; k.norm_w = in.norm_w;
+        }
+        if (o.mode != KQO_NONE) {
+            k.q8_mode = o.mode; k.q8_out = o.q8; k.q8_norm = o.norm; k.q8_cnt = e->kq_cnt; k.q8_cnt_cap = e->kq_cnt_cap;
+            k.q8_abl = e->kq_abl;
+        }
+        if (up) k.w2 = up->w;
         return launch_matvec_kq(W.type, k, s);
+    };
+    auto launch_img = [&](const img &in, int K) {
+        if (in.src != LAUNCH) return 0;
+        if (in.norm_w) return launch_norm_q8K(in.xf, K, in.norm_w, K, c.eps, 1, in.x, (K / 256) * 292, s);
+        return launch_quant_q8_K(in.xf, K, K, 1, in.x, (K / 256) * 292, s);
     };
     if (launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s)) return -1;
     for (int il = 0; il < c.n_layer; ++il) {
         const layer_dev &L = e->layers[il];
         const kq_layer &K = e->kql[il];
-        if (launch_norm_q8K(e->x, E, L.attn_norm, E, c.eps, 1, e->kq_x, (E / 256) * 292, s)) return -1;
+        // layer 0's image A has no producing down: a launch when the plan hands it off
+        const img in_a{srcA == HANDOFF && il == 0 ? LAUNCH : srcA, e->kq_x, KQP_NORM, e->x, L.attn_norm};
+        if (launch_img(in_a, E)) return -1;
         if (K.qk_fused) {  // q|k in one allocation (same type): one launch for both
             kq_mat qk = K.q;
             qk.rows = K.q.rows + K.k.rows;
-            if (mv(qk, e->qkv, nullptr, nullptr)) return -1;
-        } else if (mv(K.q, e->qkv, nullptr, nullptr) || mv(K.k, e->qkv + e->qw, nullptr, nullptr)) {
+            if (mv(qk, e->qkv, nullptr, nullptr, in_a, out{}, nullptr)) return -1;
+        } else if (mv(K.q, e->qkv, nullptr, nullptr, in_a, out{}, nullptr) ||
+                   mv(K.k, e->qkv + e->qw, nullptr, nullptr, in_a, out{}, nullptr)) {
             return -1;
         }
-        if (mv(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr)) return -1;
+        if (mv(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr, in_a, out{}, nullptr)) return -1;
         attn_args t;
         t.qkv = e->qkv;
         t.kc = kc_of(e, il);
@@ -570,15 +630,43 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         t.q_scale = 1.0f / sqrtf((float)c.head_dim);
         t.mode = e->att_mode;
         t.nwg = e->ag.nwg; t.sbuf = e->att_sbuf; t.sync = e->att_sync; t.err = e->att_sync + e->ag.sync_ints;
+        if (srcB == HANDOFF) t.out_q8k = e->kq_xa;  // each head's 256 outputs are one super-block
         if (launch_attn_decode(t, s)) return -1;
-        if (launch_quant_q8_K(e->attn, e->qw, e->qw, 1, e->kq_x, (e->qw / 256) * 292, s)) return -1;
-        if (mv(K.o, e->sa, e->x, nullptr)) return -1;                       // + inpL (:723)
-        if (launch_norm_q8K(e->sa, E, L.ffn_norm, E, c.eps, 1, e->kq_x, (E / 256) * 292, s)) return -1;
-        if (mv(K.gate, e->kq_g, nullptr, nullptr) || mv(K.up, e->h, nullptr, e->kq_g)) return -1;  // (:446-449)
-        if (launch_quant_q8_K(e->h, c.n_ff, c.n_ff, 1, e->kq_x, (c.n_ff / 256) * 292, s)) return -1;
-        if (mv(K.down, e->x, e->sa, nullptr)) return -1;                    // + sa (:731)
+        const img in_b{srcB, e->kq_xa, KQP_F32, e->attn, nullptr};
+        if (launch_img(in_b, e->qw)) return -1;
+        out o_c;
+        if (srcC == HANDOFF) {
+            o_c.mode = KQO_NORM; o_c.q8 = e->kq_xf; o_c.norm = L.ffn_norm;
+        }
+        if (mv(K.o, e->sa, e->x, nullptr, in_b, o_c, nullptr)) return -1;  // + inpL (:723)
+        const img in_c{srcC, e->kq_xf, KQP_NORM, e->sa, L.ffn_norm};
+        if (launch_img(in_c, E)) return -1;
+        out o_d;
+        if (srcD == HANDOFF) {
+            o_d.mode = KQO_QUANT; o_d.q8 = e->kq_xh;
+        }
+        if (K.gate.type == K.up.type && K.gate.rows == K.up.rows && K.gate.K == K.up.K && e->kq_dual) {
+            // gate and up in one launch, gelu(gate)*up in registers (:446-449)
+            if (mv(K.gate, e->h, nullptr, nullptr, in_c, o_d, &K.up)) return -1;
+        } else if (mv(K.gate, e->kq_g, nullptr, nullptr, in_c, out{}, nullptr) ||
+                   mv(K.up, e->h, nullptr, e->kq_g, in_c, o_d, nullptr)) {
+            return -1;
+        }
+        const img in_d{srcD, e->kq_xh, KQP_F32, e->h, nullptr};
+        if (launch_img(in_d, c.n_ff)) return -1;
+        // down (+ sa, :731); under a HANDOFF plan for A it writes the next layer's image A (or the
+        // output norm's)
+        out o_a;
+        if (srcA == HANDOFF) {
+            o_a.mode = KQO_NORM;
+            o_a.q8 = il + 1 < c.n_layer ? e->kq_x : e->xq8k;
+            o_a.norm = il + 1 < c.n_layer ? e->layers[il + 1].attn_norm : e->out_norm;
+        }
+        if (mv(K.down, e->x, e->sa, nullptr, in_d, o_a, nullptr)) return -1;
     }
-    if (launch_norm_q8K(e->x, E, e->out_norm, E, c.eps, 1, e->xq8k, (E / 256) * 292, s)) return -1;
+    // the tied output's INIT: handed over by the last down, else its own launch (256k rows over
+    // thousands of workgroups would each redo the norm in a prologue)
+    if (srcA != HANDOFF && launch_norm_q8K(e->x, E, e->out_norm, E, c.eps, 1, e->xq8k, (E / 256) * 292, s)) return -1;
     kq_args k;
     k.w = e->embd_q6k; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = E / 256;
     k.x = e->xq8k; k.x_col_stride = (E / 256) * 292; k.y = e->logits; k.y_col_stride = c.n_vocab; k.ncols = 1;
@@ -834,6 +922,9 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     GHIP_FATAL(hipMalloc(&e->attn, (size_t)e->qw * 4));
     GHIP_FATAL(hipMalloc(&e->sa, (size_t)c.n_embd * 4));
     GHIP_FATAL(hipMalloc(&e->h, (size_t)c.n_ff * 4));
+    if (const char *v = getenv("GHIP_KQ_FUSE")) e->kq_fuse = atoi(v);
+    if (const char *v = getenv("GHIP_KQ_DUAL")) e->kq_dual = atoi(v);
+    if (const char *v = getenv("GHIP_KQ_ABL")) e->kq_abl = atoi(v);
     if (e->qw % 128 == 0) {  // whole 4-block groups
         GHIP_FATAL(hipMalloc(&e->att_act, (size_t)e->qw));
         GHIP_FATAL(hipMalloc(&e->att_da, (size_t)e->qw / 32 * 4));
@@ -850,7 +941,14 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     GHIP_FATAL(hipMalloc(&e->logits, (size_t)c.n_vocab * 4));
     if (kq_layers) {
         const int64_t kmax = std::max<int64_t>(std::max<int64_t>(c.n_embd, e->qw), c.n_ff);
-        GHIP_FATAL(hipMalloc(&e->kq_x, (size_t)(kmax / 256 * 292)));
+        const size_t img = (size_t)(kmax / 256 * 292 + 255) & ~(size_t)255;
+        GHIP_FATAL(hipMalloc(&e->kq_x, 4 * img));
+        e->kq_xa = e->kq_x + img;
+        e->kq_xf = e->kq_x + 2 * img;
+        e->kq_xh = e->kq_x + 3 * img;
+        e->kq_cnt_cap = (int)std::max<int64_t>(c.n_ff / 256, 1);
+        GHIP_FATAL(hipMalloc(&e->kq_cnt, (size_t)e->kq_cnt_cap * 128));
+        GHIP_FATAL(hipMemset(e->kq_cnt, 0, (size_t)e->kq_cnt_cap * 128));
         GHIP_FATAL(hipMalloc(&e->kq_g, (size_t)c.n_ff * 4));
     }
     GHIP_FATAL(hipMalloc(&e->key, (size_t)e->grid_big * 8));  // per-workgroup argmax keys
@@ -1059,6 +1157,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
             if (m->w && !(m == &K.k && K.qk_fused)) (void)hipFree(m->w);  // k lives inside q's q|k buffer
     if (e->kq_x) (void)hipFree(e->kq_x);
     if (e->kq_g) (void)hipFree(e->kq_g);
+    if (e->kq_cnt) (void)hipFree(e->kq_cnt);
     for (hipEvent_t ev : e->ev_fork) (void)hipEventDestroy(ev);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     if (e->side) (void)hipStreamDestroy(e->side);

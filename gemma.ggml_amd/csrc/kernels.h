@@ -101,7 +101,29 @@ struct kq_args {  // y[c][r] = vec_dot_{q4_K,q6_K}_q8_K(row r of w, column c of 
     const float *resid = nullptr, *gate_in = nullptr;
     const uint16_t *gelu_tab = nullptr;
     int gelu_clamp = 0;
+    // fused INIT (no separate Q8_K launch): pro = KQP_F32 quantizes f32 columns xf, KQP_NORM
+    // quantizes rms_norm(xf)*norm_w (k_norm_q8K's bytes); KQP_COPY reads the Q8_K columns x
+    int pro = 0;
+    const float *xf = nullptr;
+    int64_t xf_col_stride = 0;    // floats
+    const float *norm_w = nullptr;
+    float eps = 0.f;
+    // fused ffn gate/up: w = gate, w2 = up (same type and shape), y = gelu(gate) * up
+    const uint8_t *w2 = nullptr;
+    // producer-side INIT of the NEXT matvec (y stored write-through, then a per-wave count):
+    // q8_mode = KQO_QUANT: each 256-row super-block of y quantized to Q8_K by the wave completing it;
+    // KQO_NORM: rms_norm(y)*q8_norm (eps) quantized by the wave completing the whole column.
+    // q8_out: Q8_K columns ((rows/256)*292 B apart); q8_cnt: zero-initialised counters, 32 u32 apart,
+    // q8_cnt_cap of them per launch (left zero)
+    int q8_mode = 0;
+    uint8_t *q8_out = nullptr;
+    unsigned *q8_cnt = nullptr;
+    int q8_cnt_cap = 0;
+    const float *q8_norm = nullptr;
+    int q8_abl = 0;  // timing ablation only (wrong bytes): 1 no tail work, 2 no counting, 4 plain stores
 };
+enum kq_prologue_mode { KQP_COPY = 0, KQP_F32 = 1, KQP_NORM = 2 };
+enum kq_handoff_mode { KQO_NONE = 0, KQO_QUANT = 1, KQO_NORM = 2 };
 int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s);
 // ggml quantize_row_q8_K of ncols rows of K floats (row stride ldx floats) -> Q8_K rows ld_out bytes apart
 int launch_quant_q8_K(const float *x, int64_t ldx, int64_t K, int ncols, uint8_t *out, int64_t ld_out,
@@ -196,6 +218,7 @@ struct attn_args {
     float *out;             // [H*hd]
     uint32_t *out_act = nullptr;  // per-head mode: also out's Q8_0 image (attn-out's PRO_IMG input)
     float *out_da = nullptr;
+    uint8_t *out_q8k = nullptr;   // per-head mode, hd == 256: out's Q8_K image (one super-block per head)
     int H, Hkv, hd, ctx;
     float q_scale;
     float *dbg_w = nullptr;      // optional debug taps: [H][ctx] scores, [H][ctx] fp16 P, [H] inv

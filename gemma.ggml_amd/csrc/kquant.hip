@@ -13,6 +13,7 @@
 
 #include "device_util.h"
 #include "kernels.h"
+#include "q8k.h"
 
 namespace ghip {
 namespace {
@@ -137,6 +138,230 @@ __device__ __forceinline__ void stage_q8k(const kq_args &a, uint8_t *xs, int col
     for (int i = tid; i < a.nsb * 73; i += nth) dst[i] = src[i];
 }
 
+// The column's Q8_K image in LDS = ggml's INIT for K-quant src0, fused into the matvec (no separate
+// k_norm_q8K / k_quant_q8_K launch): KQP_COPY copies precomputed Q8_K rows (x); KQP_F32 runs
+// quantize_row_q8_K on f32 xf (k_quant_q8_K: one wave per super-block); KQP_NORM first applies
+// rms_norm(xf)*norm_w with k_norm_q8K's exact double-sum order (partials of 4 consecutive squares,
+// the pairwise tree h = (n+1)/2), so the bytes equal the separate kernels'.
+// Two halves: kq_pro_load issues every f32 load of this wave's super-blocks (wave w takes
+// w, w+nw, ...; at most XJ of them; surplus slots load a clamped block and are ignored) BEFORE the
+// weight prologue loads, so one counted wait covers them and the serial load -> quantize round
+// trips of a per-block loop are gone; kq_pro_build quantizes from registers into LDS.
+template <int XJ>
+struct kq_pro_regs {
+    float4 x[XJ], w[XJ];
+};
+
+template <int XJ>
+__device__ __forceinline__ void kq_pro_load(const kq_args &a, int col, int wave, int nw, int lane, kq_pro_regs<XJ> &r) {
+    if (a.pro == KQP_COPY) return;
+    const float *x = a.xf + (int64_t)col * a.xf_col_stride;
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+        const int sb = min(wave + nw * j, a.nsb - 1);
+        r.x[j] = *(const float4 *)(x + (int64_t)sb * 256 + lane * 4);
+        if (a.pro == KQP_NORM) r.w[j] = *(const float4 *)(a.norm_w + (int64_t)sb * 256 + lane * 4);
+    }
+}
+
+template <int XJ>
+__device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col, int tid, int nth,
+                             const kq_pro_regs<XJ> &r) {
+    if (a.pro == KQP_COPY) {
+        stage_q8k(a, xs, col, tid, nth);
+        return;
+    }
+    const int nw = nth >> 6, lane = tid & 63, wave = tid >> 6;
+    float scale = 1.0f;
+    if (a.pro == KQP_NORM) {
+#pragma unroll
+        for (int j = 0; j < XJ; ++j) {
+            const int sb = wave + nw * j;
+            if (sb < a.nsb) {
+                double part = 0.0;
+                part += (double)(r.x[j].x * r.x[j].x);
+                part += (double)(r.x[j].y * r.x[j].y);
+                part += (double)(r.x[j].z * r.x[j].z);
+                part += (double)(r.x[j].w * r.x[j].w);
+                red[sb * 64 + lane] = part;
+            }
+        }
+        __syncthreads();
+        int n = a.nsb * 64;
+        while (n > 64) {  // cross-wave levels through LDS
+            const int h = (n + 1) >> 1;
+            for (int i = tid; i + h < n; i += nth) red[i] += red[i + h];
+            __syncthreads();
+            n = h;
+        }
+        if (wave == 0) {  // the last levels (n <= 64) in wave 0's registers: the same adds
+            double v = lane < n ? red[lane] : 0.0;
+            while (n > 1) {
+                const int h = (n + 1) >> 1;
+                const double o = __shfl_down(v, h);
+                if (lane + h < n) v += o;
+                n = h;
+            }
+            if (lane == 0) red[0] = v;
+        }
+        __syncthreads();
+        const float mean = (float)(red[0] / (double)(a.nsb * 256));
+        scale = 1.0f / sqrtf(mean + a.eps);
+    }
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+        const int sb = wave + nw * j;
+        if (sb < a.nsb) {  // wave-uniform
+            float y[4] = {r.x[j].x, r.x[j].y, r.x[j].z, r.x[j].w};
+            if (a.pro == KQP_NORM) {
+                y[0] = pin(y[0] * scale) * r.w[j].x;
+                y[1] = pin(y[1] * scale) * r.w[j].y;
+                y[2] = pin(y[2] * scale) * r.w[j].z;
+                y[3] = pin(y[3] * scale) * r.w[j].w;
+            }
+            q8K_store(y, lane, xs + (int64_t)sb * 292);
+        }
+    }
+}
+
+__device__ __forceinline__ double *kq_red(uint8_t *xs, int nsb) {
+    return (double *)(xs + (((size_t)nsb * 292 + 15) & ~(size_t)15));
+}
+
+// write-through (sc1) global accesses for the in-launch hand-off (MI355X_MICROARCH sc1 table row 1,
+// the pattern attn_impl.h documents): values read back inside the launch are stored and loaded sc1
+typedef __attribute__((address_space(1))) float kq_gfloat;
+typedef __attribute__((address_space(1))) unsigned kq_guint;
+__device__ __forceinline__ void kq_st_sc1(float *p, float v) {
+    __hip_atomic_store((kq_gfloat *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 kq_ld4_sc1(const float *p, bool plain = false) {
+    if (plain) return *(const float4 *)p;
+    return make_float4(__hip_atomic_load((const kq_gfloat *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __hip_atomic_load((const kq_gfloat *)p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __hip_atomic_load((const kq_gfloat *)p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __hip_atomic_load((const kq_gfloat *)p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void kq_put(const kq_args &a, int64_t o, float v) {
+    if (a.q8_mode != KQO_NONE && !(a.q8_abl & 4)) kq_st_sc1(a.y + o, v);
+    else a.y[o] = v;
+}
+
+// Producer-side INIT of the next matvec (kq_args::q8_mode), run by each wave after its rows of group
+// g are stored write-through: the wave drains its stores and counts the group on its super-block's
+// counter (32 groups); the wave completing a super-block quantizes it (KQO_QUANT) or, for KQO_NORM,
+// counts the super-block on the column's counter, and the wave completing the column runs the norm
+// and writes all its super-blocks — the bytes k_quant_q8_K / k_norm_q8K write, without their
+// launches.  Two counter levels keep each address to <= 32 atomics (one counter per column took
+// 256 serialised atomics).  Completing waves reset their counters (the next launch starts at zero).
+// Counters: per column, nsb_y super-block slots then the column slot, 32 u32 (128 B) apart.
+__device__ __forceinline__ bool kq_count(unsigned *cnt, unsigned target, int lane) {
+    unsigned old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add((kq_guint *)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != target - 1) return false;
+    if (lane == 0) __hip_atomic_store((kq_guint *)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// k_norm_q8K's sum over the column: partial p = the squares of elements 4p..4p+3 (p = j*64 + lane,
+// held as part[j]), then the pairwise tree h = (n+1)/2 — levels whose halves are whole 64-partial
+// rows combine registers, the last six (n <= 64) combine lanes; anything else goes through `lds`
+// (free: every dot loop of the grid has finished).  Returns the total in every lane.
+__device__ __forceinline__ double kq_tree(double part[8], int J, int lane, double *lds) {
+    int n = J * 64;
+    bool regs = true;
+    while (n > 64) {
+        const int h = (n + 1) >> 1;
+        if (regs && h % 64 == 0) {
+            const int jh = h / 64, jn = n / 64;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j + jh < jn) part[j] += part[j + jh];
+        } else {
+            if (regs) {  // spill the live rows once, finish the wide levels in LDS
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j * 64 < n) lds[j * 64 + lane] = part[j];
+                regs = false;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            for (int i = lane; i + h < n; i += 64) lds[i] += lds[i + h];
+        }
+        n = h;
+    }
+    double v = part[0];
+    if (!regs) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        v = lane < n ? lds[lane] : 0.0;
+    }
+    while (n > 1) {
+        const int h = (n + 1) >> 1;
+        const double o = __shfl_down(v, h);
+        if (lane + h < n) v += o;
+        n = h;
+    }
+    return __shfl(v, 0);
+}
+
+__device__ __forceinline__ void kq_handoff(const kq_args &a, int col, int64_t g, int lane, uint8_t *lds) {
+    if (a.q8_abl & 2) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int nsb_y = (int)(a.rows / 256);
+    const bool quant = a.q8_mode == KQO_QUANT;
+    const int idx = (int)(g / 32);
+    unsigned *cnt = a.q8_cnt + (int64_t)col * (quant ? nsb_y : nsb_y + 1) * 32;
+    if (!kq_count(cnt + idx * 32, 32u, lane)) return;
+    if ((a.q8_abl & 1) || ((a.q8_abl & 16) && !quant) || ((a.q8_abl & 32) && quant)) return;
+    const float *y = a.y + (int64_t)col * a.y_col_stride;
+    uint8_t *out = a.q8_out + (int64_t)col * nsb_y * 292;
+    if (quant) {
+        const float4 v = kq_ld4_sc1(y + (int64_t)idx * 256 + lane * 4, a.q8_abl & 8);
+        const float xv[4] = {v.x, v.y, v.z, v.w};
+        q8K_store(xv, lane, out + (int64_t)idx * 292);
+        return;
+    }
+    if (!kq_count(cnt + nsb_y * 32, (unsigned)nsb_y, lane)) return;
+    // nsb_y <= 8 (launch_matvec_kq checks): the column in registers
+    float4 xv[8], wv[8];
+    double part[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int sb = min(k, nsb_y - 1);
+        xv[k] = kq_ld4_sc1(y + (int64_t)sb * 256 + lane * 4, a.q8_abl & 8);
+        wv[k] = *(const float4 *)(a.q8_norm + (int64_t)sb * 256 + lane * 4);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        double p = 0.0;
+        p += (double)(xv[k].x * xv[k].x);
+        p += (double)(xv[k].y * xv[k].y);
+        p += (double)(xv[k].z * xv[k].z);
+        p += (double)(xv[k].w * xv[k].w);
+        part[k] = p;
+    }
+    const double sum = kq_tree(part, nsb_y, lane, (double *)lds);
+    const float mean = (float)(sum / (double)a.rows);
+    const float scale = 1.0f / sqrtf(mean + a.eps);
+    float yv[8][4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        yv[k][0] = pin(xv[k].x * scale) * wv[k].x;
+        yv[k][1] = pin(xv[k].y * scale) * wv[k].y;
+        yv[k][2] = pin(xv[k].z * scale) * wv[k].z;
+        yv[k][3] = pin(xv[k].w * scale) * wv[k].w;
+    }
+    if (nsb_y == 8) {
+        q8K_store_n<8>(yv, lane, out);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (k < nsb_y) q8K_store(yv[k], lane, out + (int64_t)k * 292);
+    }
+}
+
 // fold the 8 lanes (and the 4 mins lanes) of each row; lane 0 of the 8-group stores
 template <int WT>
 __device__ __forceinline__ void kq_store(const kq_args &a, int col, int64_t row_raw, int l, float acc, float accm) {
@@ -151,11 +376,27 @@ __device__ __forceinline__ void kq_store(const kq_args &a, int col, int64_t row_
         } else if (a.resid) {
             v = v + a.resid[o];
         }
-        a.y[o] = v;
+        kq_put(a, o, v);
     }
 }
 
+// gate and up of one row: y = gelu(gate) * up (src/gemma_model.cpp:444-452), the gate's value
+// rounded exactly as the separate launches stored and re-read it
 template <int WT>
+__device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t row_raw, int l, float acc, float accm,
+                                            float acc2, float accm2) {
+    float g = fold8_dpp(acc), u = fold8_dpp(acc2);
+    if (WT == T_Q4_K) {
+        g = g + quad_fold_dpp(accm);
+        u = u + quad_fold_dpp(accm2);
+    }
+    if (l == 0 && row_raw < a.rows) {
+        const float gl = (a.gelu_clamp && g <= -10.0f) ? 0.0f : (a.gelu_clamp && g >= 10.0f) ? g : h2f(a.gelu_tab[f2h(g)]);
+        kq_put(a, (int64_t)col * a.y_col_stride + row_raw, gl * u);
+    }
+}
+
+template <int WT, bool DUAL, int XJ>
 __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];  // the column's Q8_K blocks
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
@@ -164,28 +405,39 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
     const int64_t g0 = (int64_t)blockIdx.x * (KQ_THREADS / 64) + wave;
     // the first round of weight loads goes out before the Q8_K staging, so its HBM round trip
     // overlaps the activation copy into LDS (the Q4_0 matvec's ring-before-prologue)
-    kq_raw<WT> r[KQ_PF];
+    // DUAL (ffn gate and up in one launch): the up matrix w2 (same type and shape) streams beside the
+    // gate rows, each in its own ordered chain; the epilogue forms gelu(gate) * up in registers
+    kq_pro_regs<XJ> pr;
+    kq_pro_load<XJ>(a, col, wave, KQ_THREADS / 64, lane, pr);
+    kq_raw<WT> r[KQ_PF], r2[DUAL ? KQ_PF : 1];
 #if GHIP_KQ_EARLY
     {
         const int64_t row0 = g0 * 8 + rr < a.rows ? g0 * 8 + rr : a.rows - 1;
 #pragma unroll
-        for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(a.w + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
+        for (int p = 0; p < KQ_PF; ++p) {
+            r[p] = kq_load<WT>(a.w + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
+            if (DUAL) r2[p] = kq_load<WT>(a.w2 + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
+        }
     }
     bool early = true;
 #else
     constexpr bool early = false;
 #endif
-    stage_q8k(a, xs, col, tid, KQ_THREADS);
+    kq_pro_build<XJ>(a, xs, kq_red(xs, a.nsb), col, tid, KQ_THREADS, pr);
     __syncthreads();
     for (int64_t g = g0; g < n_groups; g += (int64_t)gridDim.x * (KQ_THREADS / 64)) {
         const int64_t row_raw = g * 8 + rr;
         const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;  // all lanes stay active for the folds
         const uint8_t *wrow = a.w + row * a.row_bytes;
-        float acc = 0.0f, accm = 0.0f;
+        const uint8_t *wrow2 = DUAL ? a.w2 + row * a.row_bytes : nullptr;
+        float acc = 0.0f, accm = 0.0f, acc2 = 0.0f, accm2 = 0.0f;
         for (int s0 = 0; s0 < a.nsb; s0 += KQ_PF) {
             if (!early) {
 #pragma unroll
-                for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
+                for (int p = 0; p < KQ_PF; ++p) {
+                    r[p] = kq_load<WT>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
+                    if (DUAL) r2[p] = kq_load<WT>(wrow2, s0 + p < a.nsb ? s0 + p : s0, l);
+                }
             }
 #if GHIP_KQ_EARLY
             early = false;
@@ -196,9 +448,16 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
                 const kq_term t = kq_terms<WT>(r[p], xs, s0 + p, l);
                 acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
                 if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
+                if (DUAL) {
+                    const kq_term u = kq_terms<WT>(r2[p], xs, s0 + p, l);
+                    acc2 = __builtin_fmaf(u.d, (float)u.sumi, acc2);
+                    if (WT == T_Q4_K && l < 4) accm2 = __builtin_fmaf(u.dmin, (float)u.prod, accm2);
+                }
             }
         }
-        kq_store<WT>(a, col, row_raw, l, acc, accm);
+        if (DUAL) kq_store_gu<WT>(a, col, row_raw, l, acc, accm, acc2, accm2);
+        else kq_store<WT>(a, col, row_raw, l, acc, accm);
+        if (a.q8_mode != KQO_NONE) kq_handoff(a, col, g, lane, xs);
     }
 }
 
@@ -206,7 +465,7 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
 // KS waves each take nsb/KS super-blocks.  Waves 1..KS-1 stash their exact terms (sumi, d[, prod,
 // dmin]) in LDS; wave 0 runs its own segment, then continues ITS chain through the stash in
 // super-block order — the identical fmaf sequence (the Q4_0 path's ordered carry).
-template <int WT, int KS>
+template <int WT, int KS, int XJ>
 __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
@@ -219,6 +478,8 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
     const uint8_t *wrow = a.w + row * a.row_bytes;
     // first round of weight loads before the Q8_K staging (as in k_matvec_kq)
+    kq_pro_regs<XJ> pr;
+    kq_pro_load<XJ>(a, col, wave, KS, lane, pr);
     kq_raw<WT> r[KQ_PF];
 #if GHIP_KQ_EARLY
 #pragma unroll
@@ -227,7 +488,7 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
 #else
     constexpr bool early = false;
 #endif
-    stage_q8k(a, xs, col, tid, 64 * KS);
+    kq_pro_build<XJ>(a, xs, kq_red(xs, nsb), col, tid, 64 * KS, pr);  // red overlaps the stash (used before it)
     __syncthreads();
     float acc = 0.0f, accm = 0.0f;
     for (int s0 = wave * seg; s0 < (wave + 1) * seg; s0 += KQ_PF) {
@@ -263,6 +524,7 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
         if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(st_m[s * 8 + rr], (float)st_p[s * 64 + lane], accm);
     }
     kq_store<WT>(a, col, row_raw, l, acc, accm);
+    if (a.q8_mode != KQO_NONE) kq_handoff(a, col, blockIdx.x, lane, xs);  // waves 1.. are gone: LDS is free
 }
 
 }  // namespace
@@ -274,45 +536,6 @@ namespace {
 // bsums = sums of 16; d = 1/iscale (all-zero block: d = 0, q = 0).  One wave per super-block, 4
 // values per lane (all 64 lanes take part).  Divisions in double then rounded: equal to fp32
 // division for fp32 operands.
-__device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *blk) {
-    float amax = 0.0f, mx = 0.0f;
-    int idx = 0x7fffffff;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const float ax = fabsf(xv[j]);
-        if (ax > amax) {
-            amax = ax;
-            mx = xv[j];
-            idx = lane * 4 + j;
-        }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const float oa = __shfl_xor(amax, off), om = __shfl_xor(mx, off);
-        const int oi = __shfl_xor(idx, off);
-        if (oa > amax || (oa == amax && oi < idx)) {
-            amax = oa;
-            mx = om;
-            idx = oi;
-        }
-    }
-    int q[4] = {0, 0, 0, 0};
-    float d = 0.0f;
-    if (amax != 0.0f) {
-        const float iscale = (float)(-127.0 / (double)mx);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = min(127, (int)__builtin_rintf(iscale * xv[j]));
-        d = (float)(1.0 / (double)iscale);
-    }
-    int bs = q[0] + q[1] + q[2] + q[3];
-    bs += __shfl_xor(bs, 1);
-    bs += __shfl_xor(bs, 2);
-    *(uint32_t *)(blk + 4 + lane * 4) =
-        (uint32_t)(q[0] & 255) | ((uint32_t)(q[1] & 255) << 8) | ((uint32_t)(q[2] & 255) << 16) | ((uint32_t)q[3] << 24);
-    if ((lane & 3) == 0) *(int16_t *)(blk + 260 + (lane >> 2) * 2) = (int16_t)bs;
-    if (lane == 0) *(float *)blk = d;
-}
-
 __global__ void __launch_bounds__(64) k_quant_q8_K(const float *x, int64_t ldx, uint8_t *out, int64_t ld_out) {
     const int sb = blockIdx.x, c = blockIdx.y, lane = threadIdx.x;
     const float4 v = *(const float4 *)(x + (int64_t)c * ldx + (int64_t)sb * 256 + lane * 4);
@@ -463,19 +686,73 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         set_error("matvec_kq: unsupported type or shape");
         return -1;
     }
+    if (a.pro != KQP_COPY &&
+        (!a.xf || ((uintptr_t)a.xf & 15) || a.xf_col_stride % 4 || (a.pro == KQP_NORM && (!a.norm_w || ((uintptr_t)a.norm_w & 15))) ||
+         (a.pro != KQP_F32 && a.pro != KQP_NORM))) {
+        set_error("matvec_kq: fused Q8_K prologue needs 16-byte aligned f32 rows (and norm weights)");
+        return -1;
+    }
+    if (a.pro == KQP_COPY && !a.x) {
+        set_error("matvec_kq: no Q8_K activation");
+        return -1;
+    }
+    if (a.w2 && (a.gate_in || a.resid || !a.gelu_tab)) {
+        set_error("matvec_kq: fused gate/up takes the gelu table and no other epilogue");
+        return -1;
+    }
+    if (a.q8_mode != KQO_NONE) {
+        const int64_t need = (int64_t)a.ncols * (a.rows / 256 + (a.q8_mode == KQO_NORM ? 1 : 0));
+        if ((a.q8_mode != KQO_QUANT && a.q8_mode != KQO_NORM) || a.rows % 256 || !a.q8_out || !a.q8_cnt ||
+            (a.q8_mode == KQO_NORM && a.rows > 2048) ||
+            need > a.q8_cnt_cap || (a.q8_mode == KQO_NORM && (!a.q8_norm || ((uintptr_t)a.q8_norm & 15))) ||
+            a.y_col_stride % 4 || ((uintptr_t)a.y & 15)) {
+            set_error("matvec_kq: Q8_K hand-off needs rows % 256 == 0, aligned output, counters and the norm");
+            return -1;
+        }
+    }
     const int64_t groups = (a.rows + 7) / 8;
+    const size_t img0 = (size_t)a.nsb * 292;
+    const size_t img = std::max(img0, a.q8_mode == KQO_NORM ? (size_t)a.rows * 2 : (size_t)0);  // + the hand-off's tree
+    const size_t red = a.pro == KQP_NORM ? ((img0 + 15) & ~(size_t)15) + (size_t)a.nsb * 64 * sizeof(double) : 0;
     // few row groups and a long K: split K over 8 waves (the ordered carry keeps the fmaf chain)
-    const size_t lds_ks = (size_t)a.nsb * (292 + 64 * 4 * 2 + 8 * 4 * 2);
-    if (groups < 2048 && a.nsb % 8 == 0 && a.nsb >= 16 && lds_ks <= 64 * 1024) {
-        if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8>), dim3((unsigned)groups, a.ncols), dim3(512), lds_ks, s, a);
-        else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8>), dim3((unsigned)groups, a.ncols), dim3(512), lds_ks, s, a);
+    const size_t lds_ks = std::max(std::max((size_t)a.nsb * (292 + 64 * 4 * 2 + 8 * 4 * 2), red), img);
+    if (!a.w2 && groups < 2048 && a.nsb % 8 == 0 && a.nsb >= 16 && a.nsb <= 64 && lds_ks <= 64 * 1024) {
+        const dim3 grid((unsigned)groups, a.ncols);
+        if (a.nsb <= 16) {
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 2>), grid, dim3(512), lds_ks, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 2>), grid, dim3(512), lds_ks, s, a);
+        } else {
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 8>), grid, dim3(512), lds_ks, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 8>), grid, dim3(512), lds_ks, s, a);
+        }
         GHIP_CHECK(hipGetLastError());
         return 0;
     }
+    if (a.pro != KQP_COPY && a.nsb > 32) {
+        set_error("matvec_kq: fused Q8_K prologue takes at most 32 super-blocks per row on this shape");
+        return -1;
+    }
     const unsigned grid_x = (unsigned)std::min<int64_t>((groups + 3) / 4, 4096);
-    const size_t lds = (size_t)a.nsb * 292;
-    if (wtype == T_Q4_K) hipLaunchKernelGGL(k_matvec_kq<T_Q4_K>, dim3(grid_x, a.ncols), dim3(KQ_THREADS), lds, s, a);
-    else hipLaunchKernelGGL(k_matvec_kq<T_Q6_K>, dim3(grid_x, a.ncols), dim3(KQ_THREADS), lds, s, a);
+    const size_t lds = std::max(img, red);
+    if (lds > 64 * 1024) {
+        set_error("matvec_kq: row too long for the LDS image");
+        return -1;
+    }
+    const dim3 grid(grid_x, a.ncols);
+#define GHIP_KQ_LAUNCH(DUAL, XJ)                                                                              \
+    do {                                                                                                      \
+        if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ>), grid, dim3(KQ_THREADS), lds, s, a); \
+        else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ>), grid, dim3(KQ_THREADS), lds, s, a);        \
+    } while (0)
+    const bool wide = a.pro != KQP_COPY && a.nsb > 8;  // more than 2 super-blocks per wave
+    if (a.w2) {
+        if (wide) GHIP_KQ_LAUNCH(true, 8);
+        else GHIP_KQ_LAUNCH(true, 2);
+    } else {
+        if (wide) GHIP_KQ_LAUNCH(false, 8);
+        else GHIP_KQ_LAUNCH(false, 2);
+    }
+#undef GHIP_KQ_LAUNCH
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

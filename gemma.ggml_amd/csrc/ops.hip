@@ -824,7 +824,8 @@ int launch_attn_rows(const attnp_args &a, hipStream_t s) {
 
 int launch_attn_decode(const attn_args &a, hipStream_t s) {
     if (a.mode == ATTN_PER_HEAD) {
-        if (a.hd % 32 != 0 || a.hd > 256 || a.ctx % 32 != 0 || a.H % a.Hkv != 0 || !a.rope_cur) {
+        if (a.hd % 32 != 0 || a.hd > 256 || a.ctx % 32 != 0 || a.H % a.Hkv != 0 || !a.rope_cur ||
+            (a.out_q8k && a.hd != 256)) {
             set_error("attn_decode: unsupported shape for the per-head form");
             return -1;
         }
@@ -841,7 +842,7 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
     }
     const attn_geom g = attn_geometry(a.H, a.Hkv, a.hd, a.ctx);
     if (a.hd % 32 != 0 || a.hd > 512 || a.ctx % 32 != 0 || g.nwg == 0 || a.nwg != g.nwg || !a.sbuf || !a.sync ||
-        (a.out_act && attn_split_of(a.H / a.Hkv, a.hd).ds != 32)) {
+        (a.out_act && attn_split_of(a.H / a.Hkv, a.hd).ds != 32) || a.out_q8k) {
         set_error("attn_decode: unsupported shape or missing scratch");
         return -1;
     }

@@ -1,0 +1,118 @@
+// q8k.h — quantize_row_q8_K of one 256-value super-block by one wave (ggml INIT for K-quant src0,
+// restated in oracle/kquants_cpu.cpp): the first element of largest |x| gives max; iscale =
+// -127/max; q = min(127, rne(iscale*x)); bsums = sums of 16; d = 1/iscale (all-zero block: d = 0,
+// q = 0).  Lane l holds values 4l..4l+3; all 64 lanes take part.  Divisions in double then rounded:
+// equal to fp32 division for fp32 operands.  Shared by the K-quant matvec prologues/epilogues and
+// the attention kernel's per-head output image.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ghip {
+
+__device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *blk) {
+    float amax = 0.0f, mx = 0.0f;
+    int idx = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float ax = fabsf(xv[j]);
+        if (ax > amax) {
+            amax = ax;
+            mx = xv[j];
+            idx = lane * 4 + j;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float oa = __shfl_xor(amax, off), om = __shfl_xor(mx, off);
+        const int oi = __shfl_xor(idx, off);
+        if (oa > amax || (oa == amax && oi < idx)) {
+            amax = oa;
+            mx = om;
+            idx = oi;
+        }
+    }
+    int q[4] = {0, 0, 0, 0};
+    float d = 0.0f;
+    if (amax != 0.0f) {
+        const float iscale = (float)(-127.0 / (double)mx);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = min(127, (int)__builtin_rintf(iscale * xv[j]));
+        d = (float)(1.0 / (double)iscale);
+    }
+    int bs = q[0] + q[1] + q[2] + q[3];
+    bs += __shfl_xor(bs, 1);
+    bs += __shfl_xor(bs, 2);
+    *(uint32_t *)(blk + 4 + lane * 4) =
+        (uint32_t)(q[0] & 255) | ((uint32_t)(q[1] & 255) << 8) | ((uint32_t)(q[2] & 255) << 16) | ((uint32_t)q[3] << 24);
+    if ((lane & 3) == 0) *(int16_t *)(blk + 260 + (lane >> 2) * 2) = (int16_t)bs;
+    if (lane == 0) *(float *)blk = d;
+}
+
+// q8K_store of N super-blocks at once by one wave (blk + k*292 for block k): the N reductions run
+// interleaved level by level, so the cross-lane latency is paid once per level, not N times.
+// Bytes identical to N calls of q8K_store.
+template <int N>
+__device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, uint8_t *blk) {
+    float amax[N], mx[N];
+    int idx[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        amax[k] = 0.0f; mx[k] = 0.0f; idx[k] = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float ax = fabsf(xv[k][j]);
+            if (ax > amax[k]) {
+                amax[k] = ax;
+                mx[k] = xv[k][j];
+                idx[k] = lane * 4 + j;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        float oa[N], om[N];
+        int oi[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            oa[k] = __shfl_xor(amax[k], off);
+            om[k] = __shfl_xor(mx[k], off);
+            oi[k] = __shfl_xor(idx[k], off);
+        }
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            if (oa[k] > amax[k] || (oa[k] == amax[k] && oi[k] < idx[k])) {
+                amax[k] = oa[k];
+                mx[k] = om[k];
+                idx[k] = oi[k];
+            }
+        }
+    }
+    int bs[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        int q[4] = {0, 0, 0, 0};
+        float d = 0.0f;
+        if (amax[k] != 0.0f) {
+            const float iscale = (float)(-127.0 / (double)mx[k]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[j] = min(127, (int)__builtin_rintf(iscale * xv[k][j]));
+            d = (float)(1.0 / (double)iscale);
+        }
+        bs[k] = q[0] + q[1] + q[2] + q[3];
+        uint8_t *b = blk + k * 292;
+        *(uint32_t *)(b + 4 + lane * 4) =
+            (uint32_t)(q[0] & 255) | ((uint32_t)(q[1] & 255) << 8) | ((uint32_t)(q[2] & 255) << 16) | ((uint32_t)q[3] << 24);
+        if (lane == 0) *(float *)b = d;
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) bs[k] += __shfl_xor(bs[k], 1);
+#pragma unroll
+    for (int k = 0; k < N; ++k) bs[k] += __shfl_xor(bs[k], 2);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if ((lane & 3) == 0) *(int16_t *)(blk + k * 292 + 260 + (lane >> 2) * 2) = (int16_t)bs[k];
+}
+
+}  // namespace ghip

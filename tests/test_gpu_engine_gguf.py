@@ -123,7 +123,13 @@ def test_kquant_engine_synthetic_matches_oracle():
 
 
 @gpu
-def test_kquant_engine_gemma2b_layer_shapes():
+@pytest.mark.parametrize("fuse,dual", [(3, 1), (3, 0), (2, 1), (1, 1), (0, 0)])
+def test_kquant_engine_gemma2b_layer_shapes(monkeypatch, fuse, dual):
+    # fuse: the Q8_K INIT plan (enqueue_step_kq) — 3 norms in prologues + quantizations handed off,
+    # 2 the producer tails (hand-off), 1 the consumer prologues,
+    # 0 separate norm / quantize launches; dual: gate and up in one launch
+    monkeypatch.setenv("GHIP_KQ_FUSE", str(fuse))
+    monkeypatch.setenv("GHIP_KQ_DUAL", str(dual))
     shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
     m = O.Model(O.make_config(shape, n_ctx=256, kmix=1))
     e = G.Engine(shape, n_ctx=256, wtype=G.GGML_TYPE_Q4_K)
