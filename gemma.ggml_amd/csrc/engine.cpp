@@ -560,11 +560,12 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
     //   0 all LAUNCH; 1 all PROLOGUE; 2 all HANDOFF (measured: the norm tails cost more than a
     //   launch); 3 (default) norms PROLOGUE, quantizations HANDOFF.
     enum { LAUNCH, PROLOGUE, HANDOFF };
-    static const int plan[4][4] = {{LAUNCH, LAUNCH, LAUNCH, LAUNCH},
+    static const int plan[5][4] = {{LAUNCH, LAUNCH, LAUNCH, LAUNCH},
                                    {PROLOGUE, PROLOGUE, PROLOGUE, PROLOGUE},
                                    {HANDOFF, HANDOFF, HANDOFF, HANDOFF},
-                                   {PROLOGUE, HANDOFF, PROLOGUE, HANDOFF}};
-    const int mode = e->kq_fuse >= 0 && e->kq_fuse <= 3 ? e->kq_fuse : 3;
+                                   {PROLOGUE, HANDOFF, PROLOGUE, HANDOFF},
+                                   {PROLOGUE, HANDOFF, LAUNCH, HANDOFF}};
+    const int mode = e->kq_fuse >= 0 && e->kq_fuse <= 4 ? e->kq_fuse : 3;
     int srcA = plan[mode][0], srcB = plan[mode][1], srcC = plan[mode][2], srcD = plan[mode][3];
     if (E > 2048) {  // the norm hand-off holds <= 2048 values in one wave
         if (srcA == HANDOFF) srcA = PROLOGUE;

@@ -10,6 +10,7 @@
 // hsum_float_8(acc) + ((m0+m2)+(m1+m3)), folded with DPP like the Q4_0 path.
 // Bound: HBM (weights read once); 8 rows x 8 lanes per wave, the Q8_K column staged in LDS.
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_util.h"
 #include "kernels.h"
@@ -125,7 +126,7 @@ __device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *
 // KQ_PF super-blocks' weight loads are issued before any of their arithmetic (one memory round trip
 // per group instead of one per super-block)
 #ifndef GHIP_KQ_PF
-#define GHIP_KQ_PF 4
+#define GHIP_KQ_PF 2  // Q4_K_M decode, same box: 1 / 2 / 3 / 4 / 8 -> 1.170 / 1.132 / 1.140 / 1.155 / 1.315 ms/token
 #endif
 constexpr int KQ_PF = GHIP_KQ_PF;
 #ifndef GHIP_KQ_EARLY
@@ -465,7 +466,7 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
 // KS waves each take nsb/KS super-blocks.  Waves 1..KS-1 stash their exact terms (sumi, d[, prod,
 // dmin]) in LDS; wave 0 runs its own segment, then continues ITS chain through the stash in
 // super-block order — the identical fmaf sequence (the Q4_0 path's ordered carry).
-template <int WT, int KS, int XJ>
+template <int WT, int KS, int XJ, int PF>
 __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
@@ -480,10 +481,10 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     // first round of weight loads before the Q8_K staging (as in k_matvec_kq)
     kq_pro_regs<XJ> pr;
     kq_pro_load<XJ>(a, col, wave, KS, lane, pr);
-    kq_raw<WT> r[KQ_PF];
+    kq_raw<WT> r[PF];
 #if GHIP_KQ_EARLY
 #pragma unroll
-    for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, p < seg ? wave * seg + p : wave * seg, l);
+    for (int p = 0; p < PF; ++p) r[p] = kq_load<WT>(wrow, p < seg ? wave * seg + p : wave * seg, l);
     bool early = true;
 #else
     constexpr bool early = false;
@@ -491,16 +492,16 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     kq_pro_build<XJ>(a, xs, kq_red(xs, nsb), col, tid, 64 * KS, pr);  // red overlaps the stash (used before it)
     __syncthreads();
     float acc = 0.0f, accm = 0.0f;
-    for (int s0 = wave * seg; s0 < (wave + 1) * seg; s0 += KQ_PF) {
+    for (int s0 = wave * seg; s0 < (wave + 1) * seg; s0 += PF) {
     if (!early) {
 #pragma unroll
-        for (int p = 0; p < KQ_PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < (wave + 1) * seg ? s0 + p : s0, l);
+        for (int p = 0; p < PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < (wave + 1) * seg ? s0 + p : s0, l);
     }
 #if GHIP_KQ_EARLY
     early = false;
 #endif
 #pragma unroll
-    for (int p = 0; p < KQ_PF; ++p) {
+    for (int p = 0; p < PF; ++p) {
         const int s = s0 + p;
         if (s >= (wave + 1) * seg) break;
         const kq_term t = kq_terms<WT>(r[p], xs, s, l);
@@ -716,14 +717,26 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     const size_t red = a.pro == KQP_NORM ? ((img0 + 15) & ~(size_t)15) + (size_t)a.nsb * 64 * sizeof(double) : 0;
     // few row groups and a long K: split K over 8 waves (the ordered carry keeps the fmaf chain)
     const size_t lds_ks = std::max(std::max((size_t)a.nsb * (292 + 64 * 4 * 2 + 8 * 4 * 2), red), img);
-    if (!a.w2 && groups < 2048 && a.nsb % 8 == 0 && a.nsb >= 16 && a.nsb <= 64 && lds_ks <= 64 * 1024) {
+    // (min super-blocks per row for the split: GHIP_KQ_KSMIN, default 8 — the small q|k / v / o
+    // shapes then fill 256+ workgroups instead of rows/32)
+    static const int ks_min = getenv("GHIP_KQ_KSMIN") ? atoi(getenv("GHIP_KQ_KSMIN")) : 8;
+    if (!a.w2 && groups < 2048 && a.nsb % 8 == 0 && a.nsb >= ks_min && a.nsb <= 64 && lds_ks <= 64 * 1024) {
         const dim3 grid((unsigned)groups, a.ncols);
+        // a wave's whole segment (nsb/8 <= 8 super-blocks) in one round of loads when it is long
+        // (Q4_K_M decode, same box: 2 / 4 / 8 -> 1.158 / 1.174 / 1.214 ms/token)
+        static const int ks_pf = getenv("GHIP_KQ_KSPF") ? atoi(getenv("GHIP_KQ_KSPF")) : 2;
         if (a.nsb <= 16) {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 2>), grid, dim3(512), lds_ks, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 2>), grid, dim3(512), lds_ks, s, a);
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 2, 2>), grid, dim3(512), lds_ks, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 2, 2>), grid, dim3(512), lds_ks, s, a);
+        } else if (ks_pf == 8) {
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 8, 8>), grid, dim3(512), lds_ks, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 8, 8>), grid, dim3(512), lds_ks, s, a);
+        } else if (ks_pf == 2) {
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 8, 2>), grid, dim3(512), lds_ks, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 8, 2>), grid, dim3(512), lds_ks, s, a);
         } else {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 8>), grid, dim3(512), lds_ks, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 8>), grid, dim3(512), lds_ks, s, a);
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 8, KQ_PF>), grid, dim3(512), lds_ks, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 8, KQ_PF>), grid, dim3(512), lds_ks, s, a);
         }
         GHIP_CHECK(hipGetLastError());
         return 0;

@@ -123,7 +123,7 @@ def test_kquant_engine_synthetic_matches_oracle():
 
 
 @gpu
-@pytest.mark.parametrize("fuse,dual", [(3, 1), (3, 0), (2, 1), (1, 1), (0, 0)])
+@pytest.mark.parametrize("fuse,dual", [(3, 1), (3, 0), (4, 1), (2, 1), (1, 1), (0, 0)])
 def test_kquant_engine_gemma2b_layer_shapes(monkeypatch, fuse, dual):
     # fuse: the Q8_K INIT plan (enqueue_step_kq) — 3 norms in prologues + quantizations handed off,
     # 2 the producer tails (hand-off), 1 the consumer prologues,
