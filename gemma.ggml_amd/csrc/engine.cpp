@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1616,12 +1617,15 @@ static int prefill_alloc(gemma_engine *e, int T) {
     GHIP_CHECK(hipMalloc(&p.LG, (size_t)T * c.n_vocab * 4));  // all rows, as the reference computes them
     GHIP_CHECK(hipMalloc(&p.DA, (size_t)T * p.ldd * 4));
     GHIP_CHECK(hipMalloc(&p.Q16, (size_t)T * e->qw * 2));
-    GHIP_CHECK(hipMalloc(&p.XQ, (size_t)T * p.ldq));
+    // K-quant layers: XQ holds T Q8_K columns (292 B per 256 values) instead of the int8 image
+    GHIP_CHECK(hipMalloc(&p.XQ, (size_t)T * (e->kq ? p.ldq / 256 * 292 : p.ldq)));
     GHIP_CHECK(hipMalloc(&p.XH, (size_t)T * p.ldq * 2));
     GHIP_CHECK(hipMalloc(&p.keys, 256 * 8));
     p.T = T;
     return 0;
 }
+
+static int enqueue_prefill_kq(gemma_engine *e, int T);
 
 static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nullptr) {
     const gemma_hip_config &c = e->cfg;
@@ -1649,9 +1653,16 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
     int n_kv = 32 * (T / 32 + 1);  // src/gemma_model.cpp:429 with n_total = T
     if (n_kv > c.n_ctx) n_kv = c.n_ctx;
     const bool q6 = e->out_type == T_Q6_K;
-    if (q6 && launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, nullptr, T, (int)E, sqrtf((float)E), p.X, s))
+    if (e->kq) {
+        if (!exact) {
+            set_error("gemma_engine_prefill_fast: K-quant layer engines have the exact batched prefill only");
+            return -1;
+        }
+        if (enqueue_prefill_kq(e, T)) return -1;
+    } else if (q6 && launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, nullptr, T, (int)E, sqrtf((float)E), p.X, s)) {
         return -1;
-    for (int il = 0; il < c.n_layer; ++il) {
+    }
+    for (int il = 0; il < (e->kq ? 0 : c.n_layer); ++il) {
         layer_dev &L = e->layers[il];
         if (quant(il == 0 && !q6 ? QR_EMBED_NORM : QR_NORM, p.X, nullptr, E, L.attn_norm)) return -1;
         if (gemm(L.qkv, EPI_STORE, nullptr, p.QKV, e->qkv_rows)) return -1;
@@ -1699,6 +1710,68 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
     return launch_advance((const unsigned long long *)p.keys, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
 }
 
+// Batched prefill for K-quant layers (the reference's shipped Q4_K_M model, src/app.cpp:36): the
+// same T-column MUL_MATs the reference runs through mul_mat (src/hpc.cpp:216-273 with col_num = T),
+// each (row, column) the decode dot (vec_dot_q{4,6}_K_q8_K in ggml's AVX2 lane order) against the
+// column's Q8_K INIT — every K-quant launch covers all T columns (grid.y) — and the exact per-row
+// attention of the Q4_0 prefill (k_rope_kv_prefill + k_attn_rows).  Bit-identical to the token
+// loop and to the CPU path: no operation depends on the batching.
+static int enqueue_prefill_kq(gemma_engine *e, int T) {
+    const gemma_hip_config &c = e->cfg;
+    hipStream_t s = e->stream;
+    auto &p = e->pf;
+    const int64_t E = c.n_embd, F = c.n_ff;
+    const int64_t ldk = p.ldq / 256 * 292;  // Q8_K column stride in XQ
+    uint8_t *img = (uint8_t *)p.XQ;
+    auto mv = [&](const kq_mat &W, float *y, int64_t ldy, const float *resid, const float *gate_in, const kq_mat *up) {
+        kq_args k;
+        k.w = W.w; k.row_bytes = W.rb; k.rows = W.rows; k.nsb = (int)(W.K / 256);
+        k.x = img; k.x_col_stride = ldk; k.y = y; k.y_col_stride = ldy; k.ncols = T;
+        k.resid = resid; k.gate_in = gate_in; k.gelu_tab = e->gelu_tab; k.gelu_clamp = c.gelu_clamp;
+        if (up) k.w2 = up->w;
+        return launch_matvec_kq(W.type, k, s);
+    };
+    int n_kv = 32 * (T / 32 + 1);  // src/gemma_model.cpp:429 with n_total = T
+    if (n_kv > c.n_ctx) n_kv = c.n_ctx;
+    if (launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, nullptr, T, (int)E, sqrtf((float)E), p.X, s)) return -1;
+    for (int il = 0; il < c.n_layer; ++il) {
+        const layer_dev &L = e->layers[il];
+        const kq_layer &K = e->kql[il];
+        if (launch_norm_q8K(p.X, E, L.attn_norm, (int)E, c.eps, T, img, ldk, s)) return -1;
+        const int64_t ldqkv = e->qkv_rows;
+        if (K.qk_fused) {
+            kq_mat qk = K.q;
+            qk.rows = K.q.rows + K.k.rows;
+            if (mv(qk, p.QKV, ldqkv, nullptr, nullptr, nullptr)) return -1;
+        } else if (mv(K.q, p.QKV, ldqkv, nullptr, nullptr, nullptr) ||
+                   mv(K.k, p.QKV + e->qw, ldqkv, nullptr, nullptr, nullptr)) {
+            return -1;
+        }
+        if (mv(K.v, p.QKV + e->qw + e->kvw, ldqkv, nullptr, nullptr, nullptr)) return -1;
+        ropekv_args r;
+        r.qkv = p.QKV; r.ldqkv = e->qkv_rows; r.rope_cos = e->rope_cos; r.rope_sin = e->rope_sin; r.q16 = p.Q16;
+        r.kc = kc_of(e, il); r.vc = vc_of(e, il);
+        r.H = c.n_head; r.Hkv = c.n_head_kv; r.hd = c.head_dim; r.ctx = c.n_ctx; r.p0 = 0;
+        r.q_scale = 1.0f / sqrtf((float)c.head_dim);
+        if (launch_rope_kv_prefill(r, T, s)) return -1;
+        attnp_args at;
+        at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
+        at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
+        if (launch_attn_rows(at, s)) return -1;
+        if (launch_quant_q8_K(p.ATT, e->qw, e->qw, T, img, ldk, s)) return -1;
+        if (mv(K.o, p.SA, E, p.X, nullptr, nullptr)) return -1;  // + inpL
+        if (launch_norm_q8K(p.SA, E, L.ffn_norm, (int)E, c.eps, T, img, ldk, s)) return -1;
+        if (K.gate.type == K.up.type && K.gate.rows == K.up.rows && K.gate.K == K.up.K && e->kq_dual) {
+            if (mv(K.gate, p.U, F, nullptr, nullptr, &K.up)) return -1;  // gelu(gate)*up
+        } else if (mv(K.gate, p.G, F, nullptr, nullptr, nullptr) || mv(K.up, p.U, F, nullptr, p.G, nullptr)) {
+            return -1;
+        }
+        if (launch_quant_q8_K(p.U, F, F, T, img, ldk, s)) return -1;
+        if (mv(K.down, p.X, E, p.SA, nullptr, nullptr)) return -1;  // + sa
+    }
+    return 0;
+}
+
 // Batched prefill of the prompt given to gemma_engine_begin: all prompt
 // positions in one pass, KV cache filled, logits for every row as the reference computes them
 // (src/gemma_model.cpp:740); returns the greedy token and leaves the engine at position T, ready
@@ -1715,10 +1788,6 @@ static int prefill_run(gemma_engine *e, bool exact, float *logits_last, float *l
     }
     if (e->tp_n > 1) {
         set_error("gemma_engine_prefill: the MFMA prefill is single-GPU (row-split engines prefill token by token)");
-        return -1;
-    }
-    if (e->kq) {
-        set_error("gemma_engine_prefill: K-quant layer engines prefill token by token (gemma_engine_step)");
         return -1;
     }
     if (prefill_alloc(e, T)) return -1;
@@ -1968,6 +2037,9 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
         set_error("gemma_engine_ext_decode: token or position out of range");
         return -1;
     }
+    static const bool prof = getenv("GHIP_GGML_FAST_PROF") != nullptr;
+    auto us = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = prof ? us() : 0.0;
     (void)hipSetDevice(e->device);
     if (ext_set_position(e, token, pos)) return -1;
     if (!e->graph_exec) {  // first step eager (sets the kernels' LDS attributes), then capture
@@ -1976,23 +2048,38 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
     } else {
         GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
     }
+    if (prof) GHIP_CHECK(hipStreamSynchronize(e->stream));
+    const double t1 = prof ? us() : 0.0;
     // logits through a pinned staging row (a pageable device-to-host copy stages through the driver)
     const size_t lb = (size_t)c.n_vocab * 4;
     if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, lb, hipHostMallocDefault));
     GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
     GHIP_CHECK(hipStreamSynchronize(e->stream));
+    const double t2 = prof ? us() : 0.0;
     memcpy(logits, e->ext_stage, lb);
+    if (prof) fprintf(stderr, "[gemma_hip] ext_decode: launch+run %.1f us, copy %.1f us, host copy %.1f us\n", t1 - t0, t2 - t1, us() - t2);
     e->host_pos = pos + 1;
     return 0;
 }
 
 int gemma_engine_ext_prefill(gemma_engine *e, const int32_t *tokens, int T, float *logits_all) {
-    if (gemma_engine_begin(e, tokens, T)) return -1;
-    if (e->kq || e->cfg.wtype == T_Q4_K) {  // K-quant layers: token by token
-        for (int i = 0; i < T; ++i)
-            if (gemma_engine_ext_decode(e, tokens[i], i, logits_all + (size_t)i * e->cfg.n_vocab)) return -1;
-        return 0;
+    if (!e->graph_exec) {
+        // the decode step's first launches (code-object loading, LDS attributes) and its graph
+        // capture happen here, in the prompt's call, instead of in the first generated token: one
+        // eager step at position 0, whose cache row the prefill below rewrites (begin clears it)
+        (void)hipSetDevice(e->device);
+        if (ext_set_position(e, tokens[0], 0) || enqueue_step(e) || ensure_graph(e)) return -1;
+        GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));  // the graph's first launch uploads it
+        if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, (size_t)e->cfg.n_vocab * 4, hipHostMallocDefault));
+        GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, (size_t)e->cfg.n_vocab * 4, hipMemcpyDeviceToHost, e->stream));
+        GHIP_CHECK(hipStreamSynchronize(e->stream));
     }
+    if (gemma_engine_begin(e, tokens, T)) return -1;
     std::vector<float> last(e->cfg.n_vocab);
-    return gemma_engine_prefill(e, last.data(), logits_all) < 0 ? -1 : 0;
+    if (gemma_engine_prefill(e, last.data(), logits_all) < 0) return -1;
+    // measured: the first pinned-row copy after the prompt's large pageable copy takes ~10 ms; pay
+    // it here rather than in the first generated token
+    GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, (size_t)e->cfg.n_vocab * 4, hipMemcpyDeviceToHost, e->stream));
+    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    return 0;
 }

@@ -115,9 +115,49 @@ def test_kquant_engine_synthetic_matches_oracle():
         ref = m.tensor(tid)
         assert np.array_equal(e.tensor(tid, ref.size), ref), tid
     _compare(e, m, KSHAPE, 7, 16)
-    with pytest.raises(RuntimeError):  # batched prefill is not provided for K-quant layers
+    with pytest.raises(RuntimeError):  # the approximate MFMA prefill is Q4_0 / Q8_0 only
         e.begin(O.make_prompt(5, KSHAPE["n_vocab"]))
-        e.prefill(5)
+        e.prefill(5, exact=False)
+    e.close()
+    m.close()
+
+
+def _prefill_compare(e, m, shape, n_prompt, n_decode):
+    prompt = O.make_prompt(n_prompt, shape["n_vocab"])
+    m.reset()
+    tok_ref, _, all_ref = m.inference(prompt, 0, want_all=True)
+    e.begin(prompt)
+    tok, last, allv = e.prefill(len(prompt), want_all=True)
+    assert tok == tok_ref
+    bad = np.argwhere(allv.view(np.uint32) != all_ref.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} prefill logits differ, first {bad[:5]}"
+    # decode continues from the KV cache the batched prefill wrote
+    seq = list(prompt) + [tok]
+    lg = e.step(n_decode, want_logits=True)
+    for i in range(n_decode):
+        t, ref, _ = m.inference(seq, 1)
+        assert np.array_equal(lg[i].view(np.uint32), ref.view(np.uint32)), i
+        seq.append(t)
+
+
+@gpu
+@pytest.mark.parametrize("n_prompt", [1, 7, 33, 64])
+def test_kquant_engine_batched_prefill_matches_oracle(n_prompt):
+    # every prompt row's logits of the batched K-quant prefill (all T columns per launch) equal the
+    # CPU path's, and decode continues bit-exactly from its KV cache
+    m = O.Model(O.make_config(KSHAPE, n_ctx=128, kmix=1))
+    e = G.Engine(KSHAPE, n_ctx=128, wtype=G.GGML_TYPE_Q4_K)
+    _prefill_compare(e, m, KSHAPE, n_prompt, 3)
+    e.close()
+    m.close()
+
+
+@gpu
+def test_kquant_engine_batched_prefill_gemma2b_layer_shapes():
+    shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
+    m = O.Model(O.make_config(shape, n_ctx=256, kmix=1))
+    e = G.Engine(shape, n_ctx=256, wtype=G.GGML_TYPE_Q4_K)
+    _prefill_compare(e, m, shape, 40, 2)
     e.close()
     m.close()
 
