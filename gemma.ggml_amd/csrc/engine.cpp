@@ -156,6 +156,7 @@ struct kq_mat {
     uint8_t *w = nullptr;
     int type = 0;
     int64_t rows = 0, K = 0, rb = 0;
+    bool tiled = false;  // lane-contiguous layout (launch_kq_retile), else ggml rows
 };
 struct kq_layer {
     kq_mat q, k, v, o, gate, up, down;
@@ -198,6 +199,7 @@ struct gemma_engine {
     int kq_cnt_cap = 0;
     float *kq_g = nullptr;        // ffn gate output (n_ff), consumed by the up matvec's gelu*mul epilogue
     uint8_t *embd_q6k = nullptr;
+    bool embd_tiled = false;  // embd_q6k in the lane-contiguous layout (launch_kq_retile)
     int64_t embd_row_bytes = 0;
     uint8_t *xq8k = nullptr;  // Q8_K rows of rms_norm(x)*out_norm (decode: 1 row; prefill: T rows)
     int64_t xq8k_rows = 0;
@@ -333,6 +335,23 @@ static inline uint16_t *vc_of(const gemma_engine *e, int il) {
 static inline int wfmt_scale(int wt) { return wt == T_Q4_0 ? 16 : 8; }  // scale bytes per row and tile
 
 // join the warm-up side stream back into the engine stream (one join per step / capture)
+// ggml K-quant rows -> the lane-contiguous layout, in place (through a scratch copy); GHIP_KQ_TILE=0
+// keeps ggml rows.  Q6_K needs K % 2048 == 0 (else the rows stay as they are).
+static int kq_retile_inplace(uint8_t *w, int type, int64_t rows, int64_t K, hipStream_t s, bool *tiled) {
+    static const bool on = !getenv("GHIP_KQ_TILE") || atoi(getenv("GHIP_KQ_TILE"));
+    *tiled = false;
+    if (!on || (type == T_Q6_K && K % 2048)) return 0;
+    const size_t bytes = (size_t)(K / 256 * (type == T_Q4_K ? 144 : 210) * rows);
+    uint8_t *tmp = nullptr;
+    GHIP_CHECK(hipMalloc(&tmp, bytes));
+    if (launch_kq_retile(type, w, tmp, rows, K, true, s)) return -1;
+    GHIP_CHECK(hipMemcpyAsync(w, tmp, bytes, hipMemcpyDeviceToDevice, s));
+    GHIP_CHECK(hipStreamSynchronize(s));
+    GHIP_CHECK(hipFree(tmp));
+    *tiled = true;
+    return 0;
+}
+
 static int warm_join(gemma_engine *e) {
     if (!e->warm || !e->side) return 0;
     GHIP_CHECK(hipEventRecord(e->ev_join, e->side));
@@ -353,7 +372,7 @@ static int enqueue_step(gemma_engine *e) {
         return enqueue_step_kq(e, rr);
     }
     if (e->out_type == T_Q6_K &&
-        launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s))
+        launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s, e->embd_tiled))
         return -1;
     const bool front_ok = e->front_cnt && e->fuse_front && e->tp_n == 1 && e->n_virtual == 1 && !e->warm &&
                           e->att_mode == ATTN_PER_HEAD && e->att_act && e->plan[MC_QKV].ks == KS_RR &&
@@ -508,7 +527,7 @@ static int enqueue_step(gemma_engine *e) {
     if (e->out_type == T_Q6_K) {  // rms_norm*out_norm -> Q8_K -> Q6_K tied output -> argmax
         if (launch_norm_q8K(e->x, E, e->out_norm, E, c.eps, 1, e->xq8k, (E / 256) * 292, s)) return -1;
         kq_args k;
-        k.w = e->embd_q6k; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = E / 256;
+        k.w = e->embd_q6k; k.tiled = e->embd_tiled; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = E / 256;
         k.x = e->xq8k; k.x_col_stride = (E / 256) * 292; k.y = e->logits; k.y_col_stride = c.n_vocab; k.ncols = 1;
         if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
         if (launch_row_argmax(e->logits, c.n_vocab, e->key, 256, s)) return -1;
@@ -589,6 +608,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         kq_args k;
         k.w = W.w; k.row_bytes = W.rb; k.rows = W.rows; k.nsb = (int)(W.K / 256);
         k.x = in.x; k.x_col_stride = (W.K / 256) * 292; k.y = y; k.y_col_stride = W.rows; k.ncols = 1;
+        k.tiled = W.tiled;
         k.resid = resid; k.gate_in = gate_in; k.gelu_tab = e->gelu_tab; k.gelu_clamp = c.gelu_clamp;
         k.eps = c.eps;
         if (in.src == PROLOGUE) {
@@ -606,7 +626,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         if (in.norm_w) return launch_norm_q8K(in.xf, K, in.norm_w, K, c.eps, 1, in.x, (K / 256) * 292, s);
         return launch_quant_q8_K(in.xf, K, K, 1, in.x, (K / 256) * 292, s);
     };
-    if (launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s)) return -1;
+    if (launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s, e->embd_tiled)) return -1;
     for (int il = 0; il < c.n_layer; ++il) {
         const layer_dev &L = e->layers[il];
         const kq_layer &K = e->kql[il];
@@ -670,7 +690,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
     // thousands of workgroups would each redo the norm in a prologue)
     if (srcA != HANDOFF && launch_norm_q8K(e->x, E, e->out_norm, E, c.eps, 1, e->xq8k, (E / 256) * 292, s)) return -1;
     kq_args k;
-    k.w = e->embd_q6k; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = E / 256;
+    k.w = e->embd_q6k; k.tiled = e->embd_tiled; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = E / 256;
     k.x = e->xq8k; k.x_col_stride = (E / 256) * 292; k.y = e->logits; k.y_col_stride = c.n_vocab; k.ncols = 1;
     if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
     if (launch_row_argmax(e->logits, c.n_vocab, e->key, 256, s)) return -1;
@@ -777,6 +797,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     } else {
         launch_synth_norm(e->out_norm, c.n_embd, tensor_key(seed, TID_OUT_NORM), synth_scale(0.05), s);
     }
+    if (e->out_type == T_Q6_K && kq_retile_inplace(e->embd_q6k, T_Q6_K, c.n_vocab, c.n_embd, s, &e->embd_tiled)) up_fail = true;
     e->n_virtual = (tp_n > 1 && !nccl_id) ? tp_n : 1;
     e->layers.resize((size_t)c.n_layer * e->n_virtual);
     const double se = 1.0 / sqrt((double)c.n_embd), sq = 1.0 / sqrt((double)e->qw), sf = 1.0 / sqrt((double)c.n_ff);
@@ -830,6 +851,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
                     launch_synth_kquant(type, m.w, rows, k, tensor_key(seed, tid_layer(il, tid)),
                                         (float)(stdv / (type == T_Q4_K ? 0.8 : 0.68)), s);
                 }
+                if (!up_fail && kq_retile_inplace(m.w, type, rows, k, s, &m.tiled)) up_fail = true;
             };
             make(K.q, H ? H->tq : T_Q4_K, e->qw, c.n_embd, L_Q, se, H ? H->q : nullptr);
             make(K.k, H ? H->tk : T_Q4_K, e->kvw, c.n_embd, L_K, se, H ? H->k : nullptr);
@@ -1285,12 +1307,23 @@ extern "C" int64_t gemma_engine_tensor(gemma_engine *e, int tid, void *dst, int6
         GHIP_CHECK(hipFree(tmp));
         return bytes;
     };
-    if (tid == TID_EMBD && e->out_type == T_Q6_K) {
-        const int64_t bytes = e->embd_row_bytes * c.n_vocab;
+    // K-quant rows back in ggml layout
+    auto copy_kq = [&](const uint8_t *w, int type, int64_t rows, int64_t K, bool tiled) -> int64_t {
+        const int64_t bytes = K / 256 * (type == T_Q4_K ? 144 : 210) * rows;
         if (cap < bytes) return -1;
-        GHIP_CHECK(hipMemcpy(dst, e->embd_q6k, (size_t)bytes, hipMemcpyDeviceToHost));
+        if (!tiled) {
+            GHIP_CHECK(hipMemcpy(dst, w, (size_t)bytes, hipMemcpyDeviceToHost));
+            return bytes;
+        }
+        uint8_t *tmp = nullptr;
+        GHIP_CHECK(hipMalloc(&tmp, (size_t)bytes));
+        if (launch_kq_retile(type, w, tmp, rows, K, false, e->stream)) return -1;
+        GHIP_CHECK(hipStreamSynchronize(e->stream));
+        GHIP_CHECK(hipMemcpy(dst, tmp, (size_t)bytes, hipMemcpyDeviceToHost));
+        GHIP_CHECK(hipFree(tmp));
         return bytes;
-    }
+    };
+    if (tid == TID_EMBD && e->out_type == T_Q6_K) return copy_kq(e->embd_q6k, T_Q6_K, c.n_vocab, c.n_embd, e->embd_tiled);
     if (tid == TID_EMBD) return copy_mat(e->embd);
     if (tid == TID_OUT_NORM) return copy_f32(e->out_norm, c.n_embd);
     const int il = (tid - 16) / 16, k = (tid - 16) % 16;
@@ -1300,9 +1333,8 @@ extern "C" int64_t gemma_engine_tensor(gemma_engine *e, int tid, void *dst, int6
         const kq_layer &K = e->kql[il];
         const kq_mat *m = k == L_Q ? &K.q : k == L_K ? &K.k : k == L_V ? &K.v : k == L_O ? &K.o : k == L_GATE ? &K.gate
                         : k == L_UP ? &K.up : k == L_DOWN ? &K.down : nullptr;
-        if (!m || cap < m->rb * m->rows) return -1;
-        GHIP_CHECK(hipMemcpy(dst, m->w, (size_t)(m->rb * m->rows), hipMemcpyDeviceToHost));
-        return m->rb * m->rows;
+        if (!m) return -1;
+        return copy_kq(m->w, m->type, m->rows, m->K, m->tiled);
     }
     switch (k) {
         case L_ATTN_NORM: return copy_f32(L.attn_norm, c.n_embd);
@@ -1659,7 +1691,7 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
             return -1;
         }
         if (enqueue_prefill_kq(e, T)) return -1;
-    } else if (q6 && launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, nullptr, T, (int)E, sqrtf((float)E), p.X, s)) {
+    } else if (q6 && launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, nullptr, T, (int)E, sqrtf((float)E), p.X, s, e->embd_tiled)) {
         return -1;
     }
     for (int il = 0; il < (e->kq ? 0 : c.n_layer); ++il) {
@@ -1694,7 +1726,7 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
         }
         if (launch_norm_q8K(p.X, E, e->out_norm, (int)E, c.eps, T, e->xq8k, ld, s)) return -1;
         kq_args k;
-        k.w = e->embd_q6k; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = (int)(E / 256);
+        k.w = e->embd_q6k; k.tiled = e->embd_tiled; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = (int)(E / 256);
         k.x = e->xq8k; k.x_col_stride = ld; k.y = p.LG; k.y_col_stride = c.n_vocab; k.ncols = T;
         if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
     } else {
@@ -1727,13 +1759,14 @@ static int enqueue_prefill_kq(gemma_engine *e, int T) {
         kq_args k;
         k.w = W.w; k.row_bytes = W.rb; k.rows = W.rows; k.nsb = (int)(W.K / 256);
         k.x = img; k.x_col_stride = ldk; k.y = y; k.y_col_stride = ldy; k.ncols = T;
+        k.tiled = W.tiled;
         k.resid = resid; k.gate_in = gate_in; k.gelu_tab = e->gelu_tab; k.gelu_clamp = c.gelu_clamp;
         if (up) k.w2 = up->w;
         return launch_matvec_kq(W.type, k, s);
     };
     int n_kv = 32 * (T / 32 + 1);  // src/gemma_model.cpp:429 with n_total = T
     if (n_kv > c.n_ctx) n_kv = c.n_ctx;
-    if (launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, nullptr, T, (int)E, sqrtf((float)E), p.X, s)) return -1;
+    if (launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, nullptr, T, (int)E, sqrtf((float)E), p.X, s, e->embd_tiled)) return -1;
     for (int il = 0; il < c.n_layer; ++il) {
         const layer_dev &L = e->layers[il];
         const kq_layer &K = e->kql[il];

@@ -121,7 +121,11 @@ struct kq_args {  // y[c][r] = vec_dot_{q4_K,q6_K}_q8_K(row r of w, column c of 
     int q8_cnt_cap = 0;
     const float *q8_norm = nullptr;
     int q8_abl = 0;  // timing ablation only (wrong bytes): 1 no tail work, 2 no counting, 4 plain stores
+    int tiled = 0;   // w (and w2) in the lane-contiguous layout of launch_kq_retile
 };
+// ggml K-quant rows <-> the lane-contiguous device layout the matvec reads with one vector load per
+// lane (Q4_K any K % 256 == 0, Q6_K K % 2048 == 0); src != dst
+int launch_kq_retile(int wtype, const uint8_t *src, uint8_t *dst, int64_t rows, int64_t K, bool to_tiled, hipStream_t s);
 enum kq_prologue_mode { KQP_COPY = 0, KQP_F32 = 1, KQP_NORM = 2 };
 enum kq_handoff_mode { KQO_NONE = 0, KQO_QUANT = 1, KQO_NORM = 2 };
 int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s);
@@ -133,7 +137,7 @@ int launch_norm_q8K(const float *x, int64_t ldx, const float *w, int E, float ep
                     int64_t ld_out, hipStream_t s);
 // T rows of get_rows(Q6_K token_embd, tokens)*scale; token of row t: tokens[*pos] if pos else tokens[t]
 int launch_embed_q6K(const uint8_t *embd, int64_t row_bytes, const int *tokens, const int *pos, int T, int E,
-                     float scale, float *out, hipStream_t s);
+                     float scale, float *out, hipStream_t s, bool tiled = false);
 // synthetic Q4_K / Q6_K rows: oracle orc_synth_kquant(seed) with d (and dmin) rescaled by f
 int launch_synth_kquant(int wtype, uint8_t *out, int64_t rows, int64_t K, uint64_t seed, float f, hipStream_t s);
 

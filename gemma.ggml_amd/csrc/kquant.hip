@@ -38,9 +38,38 @@ template <int WT> struct kq_raw;
 template <> struct kq_raw<T_Q4_K> { uint4 h; uint32_t q[4]; };
 template <> struct kq_raw<T_Q6_K> { uint32_t qla[2], qlb[2], qh[2], sc[4]; uint32_t d; };
 
-template <int WT>
+// Lane-contiguous device layout of K-quant rows (launch_kq_retile; the engine's weights, `TL`):
+// row-major rows, row_bytes unchanged, only the bytes inside a row move so that each AVX2 lane's
+// operands are one contiguous, aligned vector:
+//   Q4_K, per super-block (144 B): header [d, dmin, scales] (16 B) unchanged; quant dword j of lane
+//     l (ggml byte 16 + 32j + 4l) -> 16 + 16l + 4j: one 16-B load per lane instead of four.
+//   Q6_K, per group of 8 super-blocks (1680 B, 16-aligned): [8 x ql 128 B][8 x qh 64 B]
+//     [8 x scales 16 B][8 x d 2 B]; within super-block i: ql dword k of lane l (ggml byte 32k + 4l)
+//     -> 128i + 16l + 4k, qh dword j (ggml byte 128 + 32j + 4l) -> 1024 + 64i + 8l + 4j; scales
+//     -> 1536 + 16i, d -> 1664 + 2i: four loads per lane instead of ~21 two-byte-aligned ones.
+// Same bytes, same arithmetic: the dots are unchanged.
+template <int WT, bool TL = false>
 __device__ __forceinline__ kq_raw<WT> kq_load(const uint8_t *wrow, int s, int l) {
     kq_raw<WT> r;
+    if constexpr (TL && WT == T_Q4_K) {
+        const uint8_t *blk = wrow + (int64_t)s * 144;
+        r.h = *(const uint4 *)blk;
+        const uint4 q = *(const uint4 *)(blk + 16 + 16 * l);
+        r.q[0] = q.x; r.q[1] = q.y; r.q[2] = q.z; r.q[3] = q.w;
+        return r;
+    }
+    if constexpr (TL && WT == T_Q6_K) {
+        const uint8_t *g = wrow + (int64_t)(s >> 3) * 1680;
+        const int i = s & 7;
+        const uint4 ql = *(const uint4 *)(g + 128 * i + 16 * l);
+        const uint2 qh = *(const uint2 *)(g + 1024 + 64 * i + 8 * l);
+        const uint4 sc = *(const uint4 *)(g + 1536 + 16 * i);
+        r.qla[0] = ql.x; r.qlb[0] = ql.y; r.qla[1] = ql.z; r.qlb[1] = ql.w;
+        r.qh[0] = qh.x; r.qh[1] = qh.y;
+        r.sc[0] = sc.x; r.sc[1] = sc.y; r.sc[2] = sc.z; r.sc[3] = sc.w;
+        r.d = *(const uint16_t *)(g + 1664 + 2 * i);
+        return r;
+    }
     if constexpr (WT == T_Q4_K) {
         const uint8_t *blk = wrow + (int64_t)s * 144;
         r.h = *(const uint4 *)blk;  // d, dmin, scales[12]
@@ -397,7 +426,7 @@ __device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t r
     }
 }
 
-template <int WT, bool DUAL, int XJ>
+template <int WT, bool DUAL, int XJ, bool TL>
 __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];  // the column's Q8_K blocks
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
@@ -416,8 +445,8 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
         const int64_t row0 = g0 * 8 + rr < a.rows ? g0 * 8 + rr : a.rows - 1;
 #pragma unroll
         for (int p = 0; p < KQ_PF; ++p) {
-            r[p] = kq_load<WT>(a.w + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
-            if (DUAL) r2[p] = kq_load<WT>(a.w2 + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
+            r[p] = kq_load<WT, TL>(a.w + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
+            if (DUAL) r2[p] = kq_load<WT, TL>(a.w2 + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
         }
     }
     bool early = true;
@@ -436,8 +465,8 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
             if (!early) {
 #pragma unroll
                 for (int p = 0; p < KQ_PF; ++p) {
-                    r[p] = kq_load<WT>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
-                    if (DUAL) r2[p] = kq_load<WT>(wrow2, s0 + p < a.nsb ? s0 + p : s0, l);
+                    r[p] = kq_load<WT, TL>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
+                    if (DUAL) r2[p] = kq_load<WT, TL>(wrow2, s0 + p < a.nsb ? s0 + p : s0, l);
                 }
             }
 #if GHIP_KQ_EARLY
@@ -462,11 +491,70 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
     }
 }
 
+// T-column form (the batched prefill): NC columns per workgroup share every weight load, so the
+// weights leave L2 / HBM once per NC prompt rows instead of once per row; each (row, column) is
+// still the decode dot in ggml's lane order (one fmaf chain per lane and column), so the result is
+// bit-identical.  Q8_K columns precomputed (KQP_COPY), no hand-off.
+template <int WT, bool DUAL, int NC, bool TL>
+__global__ void __launch_bounds__(KQ_THREADS) k_matmul_kq(kq_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xs[];  // NC columns' Q8_K images
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
+    const int c0 = blockIdx.y * NC;
+    const int nc = min(NC, a.ncols - c0);
+    const int64_t img = (int64_t)a.nsb * 292;
+    for (int c = 0; c < nc; ++c) {
+        const uint32_t *src = (const uint32_t *)(a.x + (int64_t)(c0 + c) * a.x_col_stride);
+        uint32_t *dst = (uint32_t *)(xs + c * img);
+        for (int i = tid; i < a.nsb * 73; i += KQ_THREADS) dst[i] = src[i];
+    }
+    __syncthreads();
+    const int64_t n_groups = (a.rows + 7) / 8;
+    for (int64_t g = (int64_t)blockIdx.x * (KQ_THREADS / 64) + wave; g < n_groups;
+         g += (int64_t)gridDim.x * (KQ_THREADS / 64)) {
+        const int64_t row_raw = g * 8 + rr;
+        const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
+        const uint8_t *wrow = a.w + row * a.row_bytes;
+        const uint8_t *wrow2 = DUAL ? a.w2 + row * a.row_bytes : nullptr;
+        float acc[NC], accm[NC], acc2[NC], accm2[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] = accm[c] = acc2[c] = accm2[c] = 0.0f;
+        for (int s0 = 0; s0 < a.nsb; s0 += KQ_PF) {
+            kq_raw<WT> r[KQ_PF], r2[DUAL ? KQ_PF : 1];
+#pragma unroll
+            for (int p = 0; p < KQ_PF; ++p) {
+                r[p] = kq_load<WT, TL>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
+                if (DUAL) r2[p] = kq_load<WT, TL>(wrow2, s0 + p < a.nsb ? s0 + p : s0, l);
+            }
+#pragma unroll
+            for (int p = 0; p < KQ_PF; ++p) {
+                if (s0 + p >= a.nsb) break;
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const kq_term t = kq_terms<WT>(r[p], xs + c * img, s0 + p, l);
+                    acc[c] = __builtin_fmaf(t.d, (float)t.sumi, acc[c]);
+                    if (WT == T_Q4_K && l < 4) accm[c] = __builtin_fmaf(t.dmin, (float)t.prod, accm[c]);
+                    if (DUAL) {
+                        const kq_term u = kq_terms<WT>(r2[p], xs + c * img, s0 + p, l);
+                        acc2[c] = __builtin_fmaf(u.d, (float)u.sumi, acc2[c]);
+                        if (WT == T_Q4_K && l < 4) accm2[c] = __builtin_fmaf(u.dmin, (float)u.prod, accm2[c]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c >= nc) break;  // wave-uniform
+            if (DUAL) kq_store_gu<WT>(a, c0 + c, row_raw, l, acc[c], accm[c], acc2[c], accm2[c]);
+            else kq_store<WT>(a, c0 + c, row_raw, l, acc[c], accm[c]);
+        }
+    }
+}
+
 // K split for tall-K / few-row shapes (e.g. ffn_down, 2048 x 16384): one row group per workgroup,
 // KS waves each take nsb/KS super-blocks.  Waves 1..KS-1 stash their exact terms (sumi, d[, prod,
 // dmin]) in LDS; wave 0 runs its own segment, then continues ITS chain through the stash in
 // super-block order — the identical fmaf sequence (the Q4_0 path's ordered carry).
-template <int WT, int KS, int XJ, int PF>
+template <int WT, int KS, int XJ, int PF, bool TL>
 __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
@@ -484,7 +572,7 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     kq_raw<WT> r[PF];
 #if GHIP_KQ_EARLY
 #pragma unroll
-    for (int p = 0; p < PF; ++p) r[p] = kq_load<WT>(wrow, p < seg ? wave * seg + p : wave * seg, l);
+    for (int p = 0; p < PF; ++p) r[p] = kq_load<WT, TL>(wrow, p < seg ? wave * seg + p : wave * seg, l);
     bool early = true;
 #else
     constexpr bool early = false;
@@ -495,7 +583,7 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     for (int s0 = wave * seg; s0 < (wave + 1) * seg; s0 += PF) {
     if (!early) {
 #pragma unroll
-        for (int p = 0; p < PF; ++p) r[p] = kq_load<WT>(wrow, s0 + p < (wave + 1) * seg ? s0 + p : s0, l);
+        for (int p = 0; p < PF; ++p) r[p] = kq_load<WT, TL>(wrow, s0 + p < (wave + 1) * seg ? s0 + p : s0, l);
     }
 #if GHIP_KQ_EARLY
     early = false;
@@ -577,6 +665,25 @@ __global__ void __launch_bounds__(1024) k_norm_q8K(const float *x, int64_t ldx, 
 
 // ---- Q6_K token_embd / tied output (llama.cpp's choice for Q4_0 / Q8_0 Gemma files) -------------
 // dequantize_row_q6_K of element e of a row (y = d*sc*(q6 - 32), left to right)
+// the same element in the lane-contiguous layout (kq_load's TL form)
+__device__ __forceinline__ float q6K_elem_t(const uint8_t *row, int64_t i) {
+    const int64_t sb = i >> 8;
+    const uint8_t *g = row + (sb >> 3) * 1680;
+    const int si = (int)(sb & 7), e = (int)(i & 255), n = e >> 7, gq = (e >> 5) & 3, l = e & 31;
+    auto qlb = [&](int o) {  // ggml ql byte o (0..127) of this super-block
+        const int k = o >> 5, r = o & 31;
+        return g[128 * si + 16 * (r >> 2) + 4 * k + (r & 3)];
+    };
+    auto qhb = [&](int o) {  // ggml qh byte o (0..63)
+        const int j = o >> 5, r = o & 31;
+        return g[1024 + 64 * si + 8 * (r >> 2) + 4 * j + (r & 3)];
+    };
+    const int lo = (gq & 1) ? qlb(n * 64 + l + 32) : qlb(n * 64 + l);
+    const int q = (((gq & 2) ? lo >> 4 : lo & 15) | (((qhb(n * 32 + l) >> (2 * gq)) & 3) << 4)) - 32;
+    const int8_t scv = (int8_t)g[1536 + 16 * si + n * 8 + l / 16 + 2 * gq];
+    return pin(h2f(*(const uint16_t *)(g + 1664 + 2 * si)) * (float)scv) * (float)q;
+}
+
 __device__ __forceinline__ float q6K_elem(const uint8_t *row, int64_t i) {
     const uint8_t *blk = row + (i >> 8) * 210;
     const int e = (int)(i & 255), n = e >> 7, g = (e >> 5) & 3, l = e & 31;
@@ -589,12 +696,48 @@ __device__ __forceinline__ float q6K_elem(const uint8_t *row, int64_t i) {
 
 // get_rows(token_embd, tokens) * sqrt(E) (src/gemma_model.cpp:677-679): row t reads token
 // tokens[*pos] (decode: the engine's device-side position) or tokens[t] (prefill)
+template <bool TL>
 __global__ void k_embed_q6K(const uint8_t *embd, int64_t row_bytes, const int *tokens, const int *pos, int E,
                             float scale, float *out) {
     const int t = blockIdx.x;
     const int tok = pos ? tokens[*pos] : tokens[t];
     const uint8_t *row = embd + (int64_t)tok * row_bytes;
-    for (int i = threadIdx.x; i < E; i += blockDim.x) out[(int64_t)t * E + i] = q6K_elem(row, i) * scale;
+    for (int i = threadIdx.x; i < E; i += blockDim.x) out[(int64_t)t * E + i] = (TL ? q6K_elem_t(row, i) : q6K_elem(row, i)) * scale;
+}
+
+// ggml rows <-> the lane-contiguous layout of kq_load<WT, true> (one thread per (row, super-block);
+// TO: ggml -> lane-contiguous, else back).  src and dst are distinct buffers.
+template <int WT, bool TO>
+__global__ void k_kq_retile(const uint8_t *src, uint8_t *dst, int64_t rows, int nsb) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= rows * nsb) return;
+    const int64_t row = gid / nsb;
+    const int sb = (int)(gid % nsb);
+    auto mv = [&](int64_t raw, int64_t til) {
+        if (TO) dst[til] = src[raw];
+        else dst[raw] = src[til];
+    };
+    if (WT == T_Q4_K) {
+        const int64_t b = row * (int64_t)nsb * 144 + (int64_t)sb * 144;
+        for (int o = 0; o < 16; ++o) mv(b + o, b + o);
+        for (int o = 0; o < 128; ++o) {  // ggml byte 16 + 32j + 4l + c -> 16 + 16l + 4j + c
+            const int j = o >> 5, l = (o & 31) >> 2, c = o & 3;
+            mv(b + 16 + o, b + 16 + 16 * l + 4 * j + c);
+        }
+    } else {
+        const int64_t rb = (int64_t)nsb * 210, raw = row * rb + (int64_t)sb * 210, g = row * rb + (int64_t)(sb >> 3) * 1680;
+        const int i = sb & 7;
+        for (int o = 0; o < 128; ++o) {  // ql: ggml byte 32k + 4l + c -> 128i + 16l + 4k + c
+            const int k = o >> 5, l = (o & 31) >> 2, c = o & 3;
+            mv(raw + o, g + 128 * i + 16 * l + 4 * k + c);
+        }
+        for (int o = 0; o < 64; ++o) {  // qh: ggml byte 128 + 32j + 4l + c -> 1024 + 64i + 8l + 4j + c
+            const int j = o >> 5, l = (o & 31) >> 2, c = o & 3;
+            mv(raw + 128 + o, g + 1024 + 64 * i + 8 * l + 4 * j + c);
+        }
+        for (int o = 0; o < 16; ++o) mv(raw + 192 + o, g + 1536 + 16 * i + o);
+        for (int o = 0; o < 2; ++o) mv(raw + 208 + o, g + 1664 + 2 * i + o);
+    }
 }
 
 // device twin of oracle orc_synth_kquant (splitmix64 stream: draw n of the matrix is mix(st0 +
@@ -657,12 +800,17 @@ int launch_norm_q8K(const float *x, int64_t ldx, const float *w, int E, float ep
 }
 
 int launch_embed_q6K(const uint8_t *embd, int64_t row_bytes, const int *tokens, const int *pos, int T, int E,
-                     float scale, float *out, hipStream_t s) {
+                     float scale, float *out, hipStream_t s, bool tiled) {
     if (E % 256 || T <= 0) {
         set_error("embed_q6K: needs n_embd % 256 == 0");
         return -1;
     }
-    hipLaunchKernelGGL(k_embed_q6K, dim3((unsigned)T), dim3(256), 0, s, embd, row_bytes, tokens, pos, E, scale, out);
+    if (tiled && E % 2048) {
+        set_error("embed_q6K: the lane-contiguous layout needs n_embd % 2048 == 0");
+        return -1;
+    }
+    if (tiled) hipLaunchKernelGGL(k_embed_q6K<true>, dim3((unsigned)T), dim3(256), 0, s, embd, row_bytes, tokens, pos, E, scale, out);
+    else hipLaunchKernelGGL(k_embed_q6K<false>, dim3((unsigned)T), dim3(256), 0, s, embd, row_bytes, tokens, pos, E, scale, out);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -681,6 +829,21 @@ int launch_synth_kquant(int wtype, uint8_t *out, int64_t rows, int64_t K, uint64
     return 0;
 }
 
+int launch_kq_retile(int wtype, const uint8_t *src, uint8_t *dst, int64_t rows, int64_t K, bool to_tiled, hipStream_t s) {
+    if ((wtype != T_Q4_K && wtype != T_Q6_K) || K % 256 || (wtype == T_Q6_K && K % 2048) || rows <= 0 || src == dst) {
+        set_error("kq_retile: Q4_K (K % 256 == 0) or Q6_K (K % 2048 == 0), distinct buffers");
+        return -1;
+    }
+    const int nsb = (int)(K / 256);
+    const unsigned grid = (unsigned)((rows * nsb + 255) / 256);
+    if (wtype == T_Q4_K && to_tiled) hipLaunchKernelGGL((k_kq_retile<T_Q4_K, true>), dim3(grid), dim3(256), 0, s, src, dst, rows, nsb);
+    else if (wtype == T_Q4_K) hipLaunchKernelGGL((k_kq_retile<T_Q4_K, false>), dim3(grid), dim3(256), 0, s, src, dst, rows, nsb);
+    else if (to_tiled) hipLaunchKernelGGL((k_kq_retile<T_Q6_K, true>), dim3(grid), dim3(256), 0, s, src, dst, rows, nsb);
+    else hipLaunchKernelGGL((k_kq_retile<T_Q6_K, false>), dim3(grid), dim3(256), 0, s, src, dst, rows, nsb);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     if ((wtype != T_Q4_K && wtype != T_Q6_K) || a.nsb <= 0 || a.rows <= 0 || a.ncols <= 0 || a.x_col_stride % 4 ||
         a.nsb * 292 > 64 * 1024) {
@@ -691,6 +854,10 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         (!a.xf || ((uintptr_t)a.xf & 15) || a.xf_col_stride % 4 || (a.pro == KQP_NORM && (!a.norm_w || ((uintptr_t)a.norm_w & 15))) ||
          (a.pro != KQP_F32 && a.pro != KQP_NORM))) {
         set_error("matvec_kq: fused Q8_K prologue needs 16-byte aligned f32 rows (and norm weights)");
+        return -1;
+    }
+    if (a.tiled && (wtype == T_Q6_K ? a.nsb % 8 : 0)) {
+        set_error("matvec_kq: the lane-contiguous Q6_K layout needs K % 2048 == 0");
         return -1;
     }
     if (a.pro == KQP_COPY && !a.x) {
@@ -720,24 +887,45 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     // (min super-blocks per row for the split: GHIP_KQ_KSMIN, default 8 — the small q|k / v / o
     // shapes then fill 256+ workgroups instead of rows/32)
     static const int ks_min = getenv("GHIP_KQ_KSMIN") ? atoi(getenv("GHIP_KQ_KSMIN")) : 8;
+    // many columns (the batched prefill): NC = 4 columns per workgroup share the weight loads
+    static const int kq_nc = getenv("GHIP_KQ_NC") ? atoi(getenv("GHIP_KQ_NC")) : 4;
+    if (kq_nc == 4 && a.ncols >= 4 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && 4 * img0 <= 160 * 1024) {
+        const size_t lds4 = 4 * img0;
+        const unsigned gx = (unsigned)std::min<int64_t>((groups + 3) / 4, 4096);
+        const dim3 grid(gx, (unsigned)((a.ncols + 3) / 4));
+        auto go = [&](const void *fn) -> int {
+            if (lds4 > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4));
+            void *args[] = {(void *)&a};
+            GHIP_CHECK(hipLaunchKernel(fn, grid, dim3(KQ_THREADS), args, lds4, s));
+            return 0;
+        };
+        const bool d = a.w2 != nullptr;
+        if (wtype == T_Q4_K) {
+            if (a.tiled) return d ? go((const void *)k_matmul_kq<T_Q4_K, true, 4, true>) : go((const void *)k_matmul_kq<T_Q4_K, false, 4, true>);
+            return d ? go((const void *)k_matmul_kq<T_Q4_K, true, 4, false>) : go((const void *)k_matmul_kq<T_Q4_K, false, 4, false>);
+        }
+        if (a.tiled) return d ? go((const void *)k_matmul_kq<T_Q6_K, true, 4, true>) : go((const void *)k_matmul_kq<T_Q6_K, false, 4, true>);
+        return d ? go((const void *)k_matmul_kq<T_Q6_K, true, 4, false>) : go((const void *)k_matmul_kq<T_Q6_K, false, 4, false>);
+    }
     if (!a.w2 && groups < 2048 && a.nsb % 8 == 0 && a.nsb >= ks_min && a.nsb <= 64 && lds_ks <= 64 * 1024) {
         const dim3 grid((unsigned)groups, a.ncols);
-        // a wave's whole segment (nsb/8 <= 8 super-blocks) in one round of loads when it is long
-        // (Q4_K_M decode, same box: 2 / 4 / 8 -> 1.158 / 1.174 / 1.214 ms/token)
+        // prefetch depth of a wave's segment (Q4_K_M decode, same box: 2 / 4 / 8 -> 1.158 / 1.174 /
+        // 1.214 ms/token; 8 super-blocks of Q6_K raw rows exceed the 63 outstanding loads vmcnt counts)
         static const int ks_pf = getenv("GHIP_KQ_KSPF") ? atoi(getenv("GHIP_KQ_KSPF")) : 2;
-        if (a.nsb <= 16) {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 2, 2>), grid, dim3(512), lds_ks, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 2, 2>), grid, dim3(512), lds_ks, s, a);
-        } else if (ks_pf == 8) {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 8, 8>), grid, dim3(512), lds_ks, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 8, 8>), grid, dim3(512), lds_ks, s, a);
-        } else if (ks_pf == 2) {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 8, 2>), grid, dim3(512), lds_ks, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 8, 2>), grid, dim3(512), lds_ks, s, a);
-        } else {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, 8, KQ_PF>), grid, dim3(512), lds_ks, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, 8, KQ_PF>), grid, dim3(512), lds_ks, s, a);
-        }
+#define GHIP_KQ_KS(XJ, PF)                                                                                  \
+    do {                                                                                                    \
+        if (a.tiled) {                                                                                      \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, XJ, PF, true>), grid, dim3(512), lds_ks, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, XJ, PF, true>), grid, dim3(512), lds_ks, s, a);            \
+        } else {                                                                                            \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_ks<T_Q4_K, 8, XJ, PF, false>), grid, dim3(512), lds_ks, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, XJ, PF, false>), grid, dim3(512), lds_ks, s, a);            \
+        }                                                                                                   \
+    } while (0)
+        if (a.nsb <= 16) GHIP_KQ_KS(2, 2);
+        else if (ks_pf == 4) GHIP_KQ_KS(8, 4);
+        else GHIP_KQ_KS(8, 2);
+#undef GHIP_KQ_KS
         GHIP_CHECK(hipGetLastError());
         return 0;
     }
@@ -754,8 +942,13 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     const dim3 grid(grid_x, a.ncols);
 #define GHIP_KQ_LAUNCH(DUAL, XJ)                                                                              \
     do {                                                                                                      \
-        if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ>), grid, dim3(KQ_THREADS), lds, s, a); \
-        else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ>), grid, dim3(KQ_THREADS), lds, s, a);        \
+        if (a.tiled) {                                                                                        \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, true>), grid, dim3(KQ_THREADS), lds, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, true>), grid, dim3(KQ_THREADS), lds, s, a);            \
+        } else {                                                                                              \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, false>), grid, dim3(KQ_THREADS), lds, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, false>), grid, dim3(KQ_THREADS), lds, s, a);            \
+        }                                                                                                     \
     } while (0)
     const bool wide = a.pro != KQP_COPY && a.nsb > 8;  // more than 2 super-blocks per wave
     if (a.w2) {

@@ -12,7 +12,10 @@ gpu = pytest.mark.gpu
 @gpu
 @pytest.mark.parametrize("wtype", [O.Q4_K, O.Q6_K], ids=["q4_K", "q6_K"])
 @pytest.mark.parametrize("rows,K,ncols", [(8, 256, 1), (100, 2048, 3), (37, 16384, 1), (2048, 2048, 2),
-                                          (1000, 4096, 1)])
+                                          (1000, 4096, 1),
+                                          # >= 4 columns: the T-column kernel (4 columns share each
+                                          # weight load), ragged column tails, > 64 KiB of LDS
+                                          (72, 2048, 4), (300, 4096, 7), (64, 16384, 9)])
 def test_kquant_mul_mat_bit_exact(wtype, rows, K, ncols):
     import gemma_hip as G
     G.lib().hpc_set_error_mode(0)
