@@ -162,10 +162,34 @@ constexpr int KQ_PF = GHIP_KQ_PF;
 #define GHIP_KQ_EARLY 1  // 1: first weight round issued before the Q8_K staging
 #endif
 
+// the column's Q8_K image into LDS: 16-B loads, all of a thread's loads issued before the first
+// store (a plain copy loop waits one memory round trip per iteration, behind the weight loads
+// issued earlier — it cost the Q6_K down ~µs)
 __device__ __forceinline__ void stage_q8k(const kq_args &a, uint8_t *xs, int col, int tid, int nth) {
-    const uint32_t *src = (const uint32_t *)(a.x + (int64_t)col * a.x_col_stride);
-    uint32_t *dst = (uint32_t *)xs;
-    for (int i = tid; i < a.nsb * 73; i += nth) dst[i] = src[i];
+    const uint8_t *src = a.x + (int64_t)col * a.x_col_stride;
+    const int bytes = a.nsb * 292;
+    if ((bytes & 15) == 0 && ((uintptr_t)src & 15) == 0) {
+        const int n16 = bytes >> 4;
+        const uint4 *s4 = (const uint4 *)src;
+        uint4 *d4 = (uint4 *)xs;
+        for (int i0 = 0; i0 < n16; i0 += 4 * nth) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + tid + k * nth;
+                v[k] = s4[i < n16 ? i : 0];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + tid + k * nth;
+                if (i < n16) d4[i] = v[k];
+            }
+        }
+        return;
+    }
+    const uint32_t *s1 = (const uint32_t *)src;
+    uint32_t *d1 = (uint32_t *)xs;
+    for (int i = tid; i < a.nsb * 73; i += nth) d1[i] = s1[i];
 }
 
 // The column's Q8_K image in LDS = ggml's INIT for K-quant src0, fused into the matvec (no separate
