@@ -178,7 +178,8 @@ struct attn_pre {
     int pos_v;
 };
 template <int NTH, int KPF, int VPF>
-__device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, attn_pre<KPF, VPF> &p) {
+__device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, attn_pre<KPF, VPF> &p, int d_lo = 0,
+                                              int d_hi = 1 << 30) {
     const int hd = a.hd, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
     const int G = a.H / a.Hkv, kvh = h / G, kvw = a.Hkv * hd;
     p.pos_v = ((const int *)a.rope_cur)[hd];  // published with the row (k_advance / begin)
@@ -188,7 +189,7 @@ __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, a
 #pragma unroll
         for (int s = 0; s < KPF; ++s) p.k[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
     }
-    const int d0 = quad < hd ? quad : 0;
+    const int d0 = d_lo + quad < (hd < d_hi ? hd : d_hi) ? d_lo + quad : d_lo;
     const uint16_t *vrow0 = a.vc + ((int64_t)kvh * hd + d0) * a.ctx;
 #pragma unroll
     for (int s = 0; s < VPF; ++s) p.v[s] = *(const uint4 *)(vrow0 + (s * 32 < a.ctx ? s * 32 : 0) + t4 * 8);
@@ -197,9 +198,15 @@ __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, a
 // One token's attention for query head h by one NTH-thread workgroup (SURVEY A.4/A.6 order).
 // PRE: the K/V prefetch `pre` was issued by the caller (the fused kernel issues it before waiting
 // for q|k|v); otherwise it is issued here, after the RoPE inputs (issue order = wait order).
+// sp: with a.dsplit = S > 1, S workgroups serve head h, each the whole KQ / softmax (K rows are
+// shared through the XCD's L2) and the KQV of output dims [sp*hd/S, (sp+1)*hd/S) — each output
+// is still one vec_dot_f16 in ggml's order, so the split changes no bits, only how much of V
+// each CU streams.
 template <int NTH, bool SC1, int KPF = AH_KPF, int VPF = AH_VPF, bool PRE = false>
-__device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, const attn_pre<KPF, VPF> *pre = nullptr) {
+__device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, const attn_pre<KPF, VPF> *pre = nullptr,
+                              const int sp = 0) {
     const int hd = a.hd, half = hd / 2, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
+    const int dsz = hd / (a.dsplit > 1 ? a.dsplit : 1), d_lo = sp * dsz, d_hi = d_lo + dsz;
     const int lane = tid & 63, wave = tid >> 6, nwave = NTH / 64;
     const int G = a.H / a.Hkv, kvh = h / G;
     AH_STAMP(0);
@@ -219,11 +226,11 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         ca = *(const float4 *)(cs + i4); sa = *(const float4 *)(sn + i4);
     }
     attn_pre<KPF, VPF> own;
-    if (!PRE) attn_prefetch<NTH, KPF, VPF>(a, h, own);
+    if (!PRE) attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi);
     const attn_pre<KPF, VPF> &P = PRE ? *pre : own;
     const int pos_v = P.pos_v;
     const uint4 *kpre = P.k, *vpre = P.v;
-    const int d0 = quad < hd ? quad : 0;
+    const int d0 = d_lo + quad < d_hi ? d_lo + quad : d_lo;
     const float vx0 = ld1<SC1>(vh + d0);
     const int pos = __builtin_amdgcn_readfirstlane(pos_v);
     const int n_total = pos + 1;
@@ -260,7 +267,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     AH_STAMP(1);
     // this token's cache entries (src/gemma_model.cpp:506-517), by the group's first head; readers
     // in this launch use k16 / the v values instead
-    if (h % G == 0) {
+    if (h % G == 0 && sp == 0) {
         for (int i = tid; i < hd; i += NTH) a.kc[(int64_t)pos * kvw + (int64_t)kvh * hd + i] = k16[i];
         for (int d = quad; d < hd; d += NTH / 4)
             if (t4 == 0) a.vc[((int64_t)kvh * hd + d) * a.ctx + pos] = f2h(d == d0 ? vx0 : ld1<SC1>(vh + d));
@@ -333,7 +340,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     __syncthreads();
     AH_STAMP(3);
     // ---- KQV: out[d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16); lane t4 runs accumulator j = t4
-    for (int d = quad; d < hd; d += NTH / 4) {
+    for (int d = d_lo + quad; d < d_hi; d += NTH / 4) {
         float acc[8];
 #pragma unroll
         for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
@@ -372,13 +379,14 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         // this head's hd/32 blocks of the Q8_0 activation image of `out` (attn-out's PRO_IMG input;
         // the same quantize_row_q8_0 the consumer would run, DESIGN.md §Activation image)
         __syncthreads();
-        if (tid < hd / 8) {
-            const float *o = (const float *)smem + (tid >> 2) * 32 + (tid & 3) * 8;
+        if (tid < dsz / 8) {  // this workgroup's dims: dsz / 32 whole blocks
+            const int b = d_lo / 32 + (tid >> 2);
+            const float *o = (const float *)smem + b * 32 + (tid & 3) * 8;
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = o[j];
-            if (SC1) image_put_quad_sc1(a.out_act, a.out_da, (int64_t)h * (hd / 32) + (tid >> 2), tid & 3, v);
-            else image_put_quad(a.out_act, nullptr, a.out_da, (int64_t)h * (hd / 32) + (tid >> 2), tid & 3, v);
+            if (SC1) image_put_quad_sc1(a.out_act, a.out_da, (int64_t)h * (hd / 32) + b, tid & 3, v);
+            else image_put_quad(a.out_act, nullptr, a.out_da, (int64_t)h * (hd / 32) + b, tid & 3, v);
         }
     }
     if (a.out_q8k) {

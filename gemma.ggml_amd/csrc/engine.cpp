@@ -232,6 +232,9 @@ struct gemma_engine {
     // 1 consumer prologues, 2 producer hand-offs, 3 norms in prologues + quantizations handed off);
     // kq_dual: gate+up in one launch
     int kq_fuse = 3, kq_dual = 1;
+    // per-head decode attention: workgroups per head (each the KQ/softmax, 1/att_dsplit of the KQV
+    // dims; GHIP_ATT_DSPLIT). Same box, decode tok/s: 1 / 2 / 4 -> 1,443 / 1,458 / 1,458
+    int att_dsplit = 2;
     int kq_abl = 0;  // GHIP_KQ_ABL: hand-off timing ablation (kq_args::q8_abl; wrong results)
     int fuse_front = 0;  // measured: 727 vs 672 us/token (the in-launch hand-offs cost as much as the
                          // launch boundaries they replace; DESIGN.md perf log) — kept as an option
@@ -456,6 +459,7 @@ static int enqueue_step(gemma_engine *e) {
             GHIP_CHECK(hipStreamWaitEvent(e->side, e->ev_fork[il], 0));
             if (launch_mall_warm(ptrs, bytes, 6, e->warm_grid, e->side)) return -1;
         }
+        if (t.mode == ATTN_PER_HEAD) t.dsplit = e->att_dsplit;
         if (launch_attn_decode(t, s)) return -1;
         const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
         if (e->dbg) GHIP_CHECK(hipMemcpyAsync(e->dbg + tap, e->qkv, (size_t)e->qkv_rows * 4, hipMemcpyDeviceToDevice, s));
@@ -653,6 +657,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         t.mode = e->att_mode;
         t.nwg = e->ag.nwg; t.sbuf = e->att_sbuf; t.sync = e->att_sync; t.err = e->att_sync + e->ag.sync_ints;
         if (srcB == HANDOFF) t.out_q8k = e->kq_xa;  // each head's 256 outputs are one super-block
+        else if (t.mode == ATTN_PER_HEAD) t.dsplit = e->att_dsplit;
         if (launch_attn_decode(t, s)) return -1;
         const img in_b{srcB, e->kq_xa, KQP_F32, e->attn, nullptr};
         if (launch_img(in_b, e->qw)) return -1;
@@ -949,6 +954,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     if (const char *v = getenv("GHIP_KQ_FUSE")) e->kq_fuse = atoi(v);
     if (const char *v = getenv("GHIP_KQ_DUAL")) e->kq_dual = atoi(v);
     if (const char *v = getenv("GHIP_KQ_ABL")) e->kq_abl = atoi(v);
+    if (const char *v = getenv("GHIP_ATT_DSPLIT")) e->att_dsplit = atoi(v);
     if (e->qw % 128 == 0) {  // whole 4-block groups
         GHIP_FATAL(hipMalloc(&e->att_act, (size_t)e->qw));
         GHIP_FATAL(hipMalloc(&e->att_da, (size_t)e->qw / 32 * 4));
@@ -1946,7 +1952,9 @@ extern "C" int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *
     GHIP_CHECK(hipMemcpy(d_rc + hd / 2, rs.data() + (size_t)pos * (hd / 2), (size_t)(hd / 2) * 4, hipMemcpyHostToDevice));
     GHIP_CHECK(hipMemcpy(d_rc + hd, &pos, 4, hipMemcpyHostToDevice));
     a.rope_cur = d_rc;
-    a.mode = mode;
+    // mode 0 per-head, 1 split form; 2 / 3: per-head with 2 / 4 workgroups per head (dim split)
+    a.mode = mode >= 2 ? ATTN_PER_HEAD : mode;
+    a.dsplit = mode == 2 ? 2 : mode == 3 ? 4 : 1;
     a.out = d_out; a.H = H; a.Hkv = Hkv; a.hd = hd; a.ctx = ctx; a.q_scale = 1.0f / sqrtf((float)hd);
     a.dbg_w = d_dw; a.dbg_p = d_dp; a.dbg_inv = d_di; a.dbg_t = d_dt;
     int r = 0;

@@ -223,6 +223,7 @@ struct attn_args {
     uint32_t *out_act = nullptr;  // per-head mode: also out's Q8_0 image (attn-out's PRO_IMG input)
     float *out_da = nullptr;
     uint8_t *out_q8k = nullptr;   // per-head mode, hd == 256: out's Q8_K image (one super-block per head)
+    int dsplit = 1;               // per-head mode: workgroups per head, each the KQV of hd/dsplit dims
     int H, Hkv, hd, ctx;
     float q_scale;
     float *dbg_w = nullptr;      // optional debug taps: [H][ctx] scores, [H][ctx] fp16 P, [H] inv

@@ -512,9 +512,9 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
 // the per-head form (k_attn_head) lives in attn_impl.h: the fused layer-front kernel runs it too
 __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int G = a.H / a.Hkv, h = blockIdx.x >> 3, kvh = h / G;
-    if ((int)(blockIdx.x & 7) != (kvh & 7)) return;  // the G heads of a kv head share an XCD (speed only)
-    attn_head_dev<AH_THREADS, false>(a, h, smem);
+    const int S = a.dsplit, G = a.H / a.Hkv, hs = blockIdx.x >> 3, h = hs / S, kvh = h / G;
+    if ((int)(blockIdx.x & 7) != (kvh & 7)) return;  // the G*S workgroups of a kv head share an XCD (speed only)
+    attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false>(a, h, smem, nullptr, hs % S);
 }
 
 // ---- exact causal attention for T prompt rows (the reference's prefill graph) -----------------
@@ -825,7 +825,8 @@ int launch_attn_rows(const attnp_args &a, hipStream_t s) {
 int launch_attn_decode(const attn_args &a, hipStream_t s) {
     if (a.mode == ATTN_PER_HEAD) {
         if (a.hd % 32 != 0 || a.hd > 256 || a.ctx % 32 != 0 || a.H % a.Hkv != 0 || !a.rope_cur ||
-            (a.out_q8k && a.hd != 256)) {
+            (a.out_q8k && (a.hd != 256 || a.dsplit != 1)) || a.dsplit < 1 || a.hd % (32 * a.dsplit) ||
+            4 * (a.hd / a.dsplit) > AH_THREADS) {
             set_error("attn_decode: unsupported shape for the per-head form");
             return -1;
         }
@@ -836,7 +837,7 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
         }
         if (lds > 64 * 1024)
             GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_head, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k_attn_head, dim3(8 * a.H), dim3(AH_THREADS), lds, s, a);
+        hipLaunchKernelGGL(k_attn_head, dim3(8 * a.H * a.dsplit), dim3(AH_THREADS), lds, s, a);
         GHIP_CHECK(hipGetLastError());
         return 0;
     }

@@ -23,7 +23,7 @@ def _attn_case(rng, pos, H, Hkv, hd, ctx, scale_q=1.0):
 
 
 @gpu
-@pytest.mark.parametrize("mode", [0, 1], ids=["per_head", "split"])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3], ids=["per_head", "split", "per_head_d2", "per_head_d4"])
 @pytest.mark.parametrize("H,Hkv", [(8, 1), (2, 1), (4, 2), (16, 16)])
 def test_attn_decode_bitexact(H, Hkv, mode):
     import gemma_hip as G
