@@ -282,12 +282,24 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             for (int s = 0; s * 32 < hd; ++s)
                 f16_step8(acc, *(const uint4 *)(k16 + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
         } else if (j0 == 0) {
+            // the row's remaining K steps (hd <= 256: at most 8 - KPF) issued together before the
+            // prefetched steps' arithmetic: one round trip, not one per step
+            const uint16_t *krow = a.kc + (int64_t)(j < a.ctx ? j : 0) * kvw + (int64_t)kvh * hd;
+            constexpr int KR = 8 - KPF > 0 ? 8 - KPF : 1;
+            uint4 krest[KR];
+#pragma unroll
+            for (int r = 0; r < KR; ++r) {
+                const int s = KPF + r;
+                krest[r] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0) + t4 * 8);
+            }
 #pragma unroll
             for (int s = 0; s < KPF; ++s)
                 if (s * 32 < hd) f16_step8(acc, kpre[s], *(const uint4 *)(q16 + s * 32 + t4 * 8));
-            const uint16_t *krow = a.kc + (int64_t)(j < a.ctx ? j : 0) * kvw + (int64_t)kvh * hd;
-            for (int s = KPF; s * 32 < hd; ++s)
-                f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
+#pragma unroll
+            for (int r = 0; r < KR; ++r) {
+                const int s = KPF + r;
+                if (KPF < 8 && s * 32 < hd) f16_step8(acc, krest[r], *(const uint4 *)(q16 + s * 32 + t4 * 8));
+            }
         } else {
             const int jc = j < pos ? j : 0;  // j > pos is masked below
             const uint16_t *krow = a.kc + (int64_t)jc * kvw + (int64_t)kvh * hd;
@@ -346,6 +358,38 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
         const uint16_t *vr = a.vc + ((int64_t)kvh * hd + d) * a.ctx;
         const float vx = d == d0 ? vx0 : ld1<SC1>(vh + d);
+        auto patch = [&](uint4 &xv, int e0) {  // this token's V: its cache write may not be visible
+            if (pos >= e0 && pos < e0 + 8) {
+                const uint32_t hv = f2h(vx), sh = 16 * ((pos - e0) & 1);
+                const uint32_t msk = ~(0xFFFFu << sh);
+                switch ((pos - e0) >> 1) {
+                    case 0: xv.x = (xv.x & msk) | (hv << sh); break;
+                    case 1: xv.y = (xv.y & msk) | (hv << sh); break;
+                    case 2: xv.z = (xv.z & msk) | (hv << sh); break;
+                    default: xv.w = (xv.w & msk) | (hv << sh); break;
+                }
+            }
+        };
+        if (n_kv <= 256) {
+            // every step's V load issued before the first step's arithmetic (one round trip);
+            // the prefetched steps of the first dimension come from the early loads
+            uint4 xs8[8];
+            const bool first = d == d0;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int e0 = s * 32 + t4 * 8;
+                if (s < VPF && first) xs8[s] = vpre[s < VPF ? s : 0];
+                else xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                if (s * 32 >= n_kv) break;
+                const int e0 = s * 32 + t4 * 8;
+                uint4 xv = xs8[s];
+                patch(xv, e0);
+                f16_step8(acc, xv, *(const uint4 *)(P16 + e0));
+            }
+        } else
         for (int st = 0, s = 0; st < n_kv; st += 32, ++s) {
             const int e0 = st + t4 * 8;
             uint4 xv;
