@@ -523,9 +523,10 @@ __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
 // past the row's own padded n_kv multiply exact zeros, so each row runs k_attn_head's arithmetic
 // (vec_dot_f16 lane order via v_fma_mix, fp16 exp, integer-exact sum, (float)(1/sum)) over
 // n_kv(i) = 32*((i+1)/32+1) positions.  One 1024-thread workgroup per (row, kv head) serves the
-// G query heads of that kv head, so every K/V row leaves L2 once per row for all of them:
-// quad q -> head q % G, KQ position q / G (+ 256/G per pass), KQV dim q / G (+ 256/G).  Rows are
-// issued longest first.  q16 / caches come from k_rope_kv_prefill (same RoPE/f16 arithmetic).
+// G <= 8 query heads of that kv head: quad q -> KQ position q (+ 256 per pass) and KQV dim q, each
+// for all G heads, so every K / V row is loaded once per row and 8 steps share one round trip
+// (the head-major mapping of round 1 paid a round trip per 256/G positions).  Rows are issued
+// longest first.  q16 / caches come from k_rope_kv_prefill (same RoPE/f16 arithmetic).
 constexpr int AR_THREADS = 1024;
 
 __global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
@@ -533,31 +534,38 @@ __global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
     const int tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2, lane = tid & 63, wave = tid >> 6;
     const int G = a.H / a.Hkv, hd = a.hd, kvw = a.Hkv * hd, nkp = a.n_kv;
     const int kvh = blockIdx.x % a.Hkv, i = a.T - 1 - (int)(blockIdx.x / a.Hkv);
-    const int g = quad % G, qo = quad / G, QP = (AR_THREADS / 4) / G, h = kvh * G + g;
     float *S = (float *)smem;                      // [G][nkp]
     uint16_t *P16 = (uint16_t *)(S + (size_t)G * nkp);  // [G][nkp]
+    uint16_t *Q16 = P16 + (size_t)G * nkp;              // [G][hd]: this row's q of the G heads
     int n_kv = 32 * ((i + 1) / 32 + 1);
     if (n_kv > nkp) n_kv = nkp;
-    uint4 qv[8];
-    const uint16_t *qrow = a.q16 + ((int64_t)i * a.H + h) * hd;
+    for (int k = tid; k < G * hd / 8; k += AR_THREADS) {
+        const int gg = k / (hd / 8), o = (k % (hd / 8)) * 8;
+        *(uint4 *)(Q16 + gg * hd + o) = *(const uint4 *)(a.q16 + ((int64_t)i * a.H + kvh * G + gg) * hd + o);
+    }
+    __syncthreads();
+    // KQ + mask (scale 1.0, mask 0 / -inf): quad -> one position per pass (256 per pass) for all G
+    // heads, so each K row is loaded once per pass (8 x 16 B per lane, one round trip) and every
+    // (head, position) dot is the same 32-accumulator vec_dot_f16 chain against that head's q
+    for (int j0 = 0; j0 < n_kv; j0 += AR_THREADS / 4) {
+        const int j = j0 + quad;
+        const int jl = j <= i ? j : i;  // masked positions load a valid row (result unused)
+        const uint16_t *krow = a.kc + (int64_t)jl * kvw + (int64_t)kvh * hd + t4 * 8;
+        uint4 kv[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) qv[s] = s * 32 < hd ? *(const uint4 *)(qrow + s * 32 + t4 * 8) : make_uint4(0, 0, 0, 0);
-    // KQ + mask (scale 1.0, mask 0 / -inf)
-    for (int j0 = 0; j0 < n_kv; j0 += QP) {
-        const int j = j0 + qo;
-        if (j >= n_kv) continue;
-        float kq = 0.0f;
-        if (j <= i) {
+        for (int s = 0; s < 8; ++s) kv[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
+#pragma unroll
+        for (int gg = 0; gg < 8; ++gg) {
+            if (gg >= G) break;
             float acc[8];
 #pragma unroll
             for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
-            const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
 #pragma unroll
             for (int s = 0; s < 8; ++s)
-                if (s * 32 < hd) f16_step8(acc, *(const uint4 *)(krow + s * 32), qv[s]);
-            kq = quad_reduce_f16(acc);
+                if (s * 32 < hd) f16_step8(acc, kv[s], *(const uint4 *)(Q16 + gg * hd + s * 32 + t4 * 8));
+            const float kq = quad_reduce_f16(acc);
+            if (t4 == 0 && j < n_kv) S[gg * nkp + j] = (j > i) ? -INFINITY : kq * 1.0f + 0.0f;
         }
-        if (t4 == 0) S[g * nkp + j] = (j > i) ? -INFINITY : kq * 1.0f + 0.0f;
     }
     __syncthreads();
     // soft_max_ext per head row: wave w takes heads w, w+16, ...
@@ -582,16 +590,36 @@ __global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
         }
     }
     __syncthreads();
-    // KQV: out[i][h][d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16[h])
-    for (int d = qo; d < hd; d += QP) {
-        float acc[8];
+    // KQV: out[i][h][d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16[h]): quad -> output dim d for
+    // all G heads, so each V row is loaded once (8 steps per round trip) and multiplied against each
+    // head's P16 row; each (head, dim) keeps vec_dot_f16's chain in step order
+    for (int d = quad; d < hd; d += AR_THREADS / 4) {
+        float acc[8][8];
 #pragma unroll
-        for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
+        for (int gg = 0; gg < 8; ++gg)
+#pragma unroll
+            for (int y = 0; y < 8; ++y) acc[gg][y] = 0.0f;
         const uint16_t *vr = a.vc + ((int64_t)kvh * hd + d) * a.ctx + t4 * 8;
-        const uint16_t *pr = P16 + g * nkp + t4 * 8;
-        for (int st = 0; st < n_kv; st += 32) f16_step8(acc, *(const uint4 *)(vr + st), *(const uint4 *)(pr + st));
-        const float o = quad_reduce_f16(acc);
-        if (t4 == 0) a.out[(int64_t)i * a.ldo + (int64_t)h * hd + d] = o;
+        for (int st0 = 0; st0 < n_kv; st0 += 256) {
+            uint4 vv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vv[u] = *(const uint4 *)(vr + (st0 + 32 * u < n_kv ? st0 + 32 * u : 0));
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (st0 + 32 * u >= n_kv) break;
+#pragma unroll
+                for (int gg = 0; gg < 8; ++gg) {
+                    if (gg >= G) break;
+                    f16_step8(acc[gg], vv[u], *(const uint4 *)(P16 + gg * nkp + st0 + 32 * u + t4 * 8));
+                }
+            }
+        }
+#pragma unroll
+        for (int gg = 0; gg < 8; ++gg) {
+            if (gg >= G) break;
+            const float o = quad_reduce_f16(acc[gg]);
+            if (t4 == 0) a.out[(int64_t)i * a.ldo + (int64_t)(kvh * G + gg) * hd + d] = o;
+        }
     }
 }
 
@@ -810,10 +838,10 @@ attn_geom attn_geometry(int H, int Hkv, int hd, int ctx) {
 
 int launch_attn_rows(const attnp_args &a, hipStream_t s) {
     const int G = a.Hkv > 0 ? a.H / a.Hkv : 0;
-    const size_t lds = (size_t)G * a.n_kv * 6;
-    if (G <= 0 || a.H % a.Hkv || (AR_THREADS / 4) % G || a.hd % 32 || a.hd > 256 || a.ctx % 32 || a.n_kv % 32 ||
+    const size_t lds = (size_t)G * a.n_kv * 6 + (size_t)G * a.hd * 2;
+    if (G <= 0 || G > 8 || a.H % a.Hkv || (AR_THREADS / 4) % G || a.hd % 32 || a.hd > 256 || a.ctx % 32 || a.n_kv % 32 ||
         a.n_kv > a.ctx || a.T <= 0 || a.T > a.n_kv || lds > 160 * 1024) {
-        set_error("attn_rows: unsupported shape (head_dim <= 256, 256 % G == 0, G*n_kv*6 B of LDS <= 160 KiB)");
+        set_error("attn_rows: unsupported shape (head_dim <= 256, G <= 8, 256 % G == 0, G*(n_kv*6 + hd*2) B of LDS <= 160 KiB)");
         return -1;
     }
     GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
