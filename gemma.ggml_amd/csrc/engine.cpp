@@ -231,7 +231,7 @@ struct gemma_engine {
     // K-quant layers: kq_fuse = the plan for where ggml's Q8_K INIT runs (enqueue_step_kq: 0 launches,
     // 1 consumer prologues, 2 producer hand-offs, 3 norms in prologues + quantizations handed off);
     // kq_dual: gate+up in one launch
-    int kq_fuse = 3, kq_dual = 1;
+    int kq_fuse = 3, kq_dual = 1, kq_pair = 1;  // kq_pair: q|k and v in one launch (GHIP_KQ_PAIR)
     // per-head decode attention: workgroups per head (each the KQ/softmax, 1/att_dsplit of the KQV
     // dims; GHIP_ATT_DSPLIT). Same box, decode tok/s: 1 / 2 / 4 -> 1,443 / 1,458 / 1,458
     int att_dsplit = 2;
@@ -607,8 +607,8 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         uint8_t *q8 = nullptr;
         const float *norm = nullptr;
     };
-    auto mv = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in, const img &in, const out &o,
-                  const kq_mat *up) {
+    auto args = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in, const img &in, const out &o,
+                    const kq_mat *up) {
         kq_args k;
         k.w = W.w; k.row_bytes = W.rb; k.rows = W.rows; k.nsb = (int)(W.K / 256);
         k.x = in.x; k.x_col_stride = (W.K / 256) * 292; k.y = y; k.y_col_stride = W.rows; k.ncols = 1;
@@ -623,8 +623,10 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
             k.q8_abl = e->kq_abl;
         }
         if (up) k.w2 = up->w;
-        return launch_matvec_kq(W.type, k, s);
+        return k;
     };
+    auto mv = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in, const img &in, const out &o,
+                  const kq_mat *up) { return launch_matvec_kq(W.type, args(W, y, resid, gate_in, in, o, up), s); };
     auto launch_img = [&](const img &in, int K) {
         if (in.src != LAUNCH) return 0;
         if (in.norm_w) return launch_norm_q8K(in.xf, K, in.norm_w, K, c.eps, 1, in.x, (K / 256) * 292, s);
@@ -637,15 +639,25 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         // layer 0's image A has no producing down: a launch when the plan hands it off
         const img in_a{srcA == HANDOFF && il == 0 ? LAUNCH : srcA, e->kq_x, KQP_NORM, e->x, L.attn_norm};
         if (launch_img(in_a, E)) return -1;
-        if (K.qk_fused) {  // q|k in one allocation (same type): one launch for both
+        const bool pair = e->kq_pair && K.qk_fused && E % 2048 == 0 && E <= 4096 && K.q.tiled == K.v.tiled &&
+                          (K.q.rows + K.k.rows) % 8 == 0;
+        if (pair) {  // q|k and v (their own types) in one launch
             kq_mat qk = K.q;
             qk.rows = K.q.rows + K.k.rows;
-            if (mv(qk, e->qkv, nullptr, nullptr, in_a, out{}, nullptr)) return -1;
-        } else if (mv(K.q, e->qkv, nullptr, nullptr, in_a, out{}, nullptr) ||
-                   mv(K.k, e->qkv + e->qw, nullptr, nullptr, in_a, out{}, nullptr)) {
-            return -1;
+            if (launch_matvec_kq2(qk.type, args(qk, e->qkv, nullptr, nullptr, in_a, out{}, nullptr), K.v.type,
+                                  args(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr, in_a, out{}, nullptr), s))
+                return -1;
+        } else {
+            if (K.qk_fused) {  // q|k in one allocation (same type): one launch for both
+                kq_mat qk = K.q;
+                qk.rows = K.q.rows + K.k.rows;
+                if (mv(qk, e->qkv, nullptr, nullptr, in_a, out{}, nullptr)) return -1;
+            } else if (mv(K.q, e->qkv, nullptr, nullptr, in_a, out{}, nullptr) ||
+                       mv(K.k, e->qkv + e->qw, nullptr, nullptr, in_a, out{}, nullptr)) {
+                return -1;
+            }
+            if (mv(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr, in_a, out{}, nullptr)) return -1;
         }
-        if (mv(K.v, e->qkv + e->qw + e->kvw, nullptr, nullptr, in_a, out{}, nullptr)) return -1;
         attn_args t;
         t.qkv = e->qkv;
         t.kc = kc_of(e, il);
@@ -954,6 +966,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     if (const char *v = getenv("GHIP_KQ_FUSE")) e->kq_fuse = atoi(v);
     if (const char *v = getenv("GHIP_KQ_DUAL")) e->kq_dual = atoi(v);
     if (const char *v = getenv("GHIP_KQ_ABL")) e->kq_abl = atoi(v);
+    if (const char *v = getenv("GHIP_KQ_PAIR")) e->kq_pair = atoi(v);
     if (const char *v = getenv("GHIP_ATT_DSPLIT")) e->att_dsplit = atoi(v);
     if (e->qw % 128 == 0) {  // whole 4-block groups
         GHIP_FATAL(hipMalloc(&e->att_act, (size_t)e->qw));

@@ -129,6 +129,8 @@ int launch_kq_retile(int wtype, const uint8_t *src, uint8_t *dst, int64_t rows, 
 enum kq_prologue_mode { KQP_COPY = 0, KQP_F32 = 1, KQP_NORM = 2 };
 enum kq_handoff_mode { KQO_NONE = 0, KQO_QUANT = 1, KQO_NORM = 2 };
 int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s);
+// two K-split matvecs over one input column in one launch (e.g. q|k and v; types may differ)
+int launch_matvec_kq2(int t1, const kq_args &a, int t2, const kq_args &b, hipStream_t s);
 // ggml quantize_row_q8_K of ncols rows of K floats (row stride ldx floats) -> Q8_K rows ld_out bytes apart
 int launch_quant_q8_K(const float *x, int64_t ldx, int64_t K, int ncols, uint8_t *out, int64_t ld_out,
                       hipStream_t s);

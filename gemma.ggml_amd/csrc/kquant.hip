@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matmul_kq(kq_args a) {
 // dmin]) in LDS; wave 0 runs its own segment, then continues ITS chain through the stash in
 // super-block order — the identical fmaf sequence (the Q4_0 path's ordered carry).
 template <int WT, int KS, int XJ, int PF, bool TL>
-__global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
+__device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
     const int col = blockIdx.y, nsb = a.nsb, seg = nsb / KS;
@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     float *st_d = (float *)(st_i + nsb * 64);   // [nsb][8]  per-row d
     int *st_p = (int *)(st_d + nsb * 8);        // [nsb][64] mins products (Q4_K)
     float *st_m = (float *)(st_p + nsb * 64);   // [nsb][8]  per-row dmin (Q4_K)
-    const int64_t row_raw = (int64_t)blockIdx.x * 8 + rr;
+    const int64_t row_raw = (int64_t)gx * 8 + rr;
     const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
     const uint8_t *wrow = a.w + row * a.row_bytes;
     // first round of weight loads before the Q8_K staging (as in k_matvec_kq)
@@ -637,7 +637,20 @@ __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
         if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(st_m[s * 8 + rr], (float)st_p[s * 64 + lane], accm);
     }
     kq_store<WT>(a, col, row_raw, l, acc, accm);
-    if (a.q8_mode != KQO_NONE) kq_handoff(a, col, blockIdx.x, lane, xs);  // waves 1.. are gone: LDS is free
+    if (a.q8_mode != KQO_NONE) kq_handoff(a, col, gx, lane, xs);  // waves 1.. are gone: LDS is free
+}
+
+template <int WT, int KS, int XJ, int PF, bool TL>
+__global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
+    kq_ks_body<WT, KS, XJ, PF, TL>(a, (int)blockIdx.x);
+}
+
+// Two matrices of one input column in one launch (a layer's q|k and v: Q4_K and Q6_K in Q4_K_M
+// files): workgroups [0, g1) run matrix a, the rest matrix b, each exactly as k_matvec_kq_ks would.
+template <int WT1, int WT2, int KS, int XJ, int PF, bool TL>
+__global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks2(kq_args a, kq_args b, int g1) {
+    if ((int)blockIdx.x < g1) kq_ks_body<WT1, KS, XJ, PF, TL>(a, (int)blockIdx.x);
+    else kq_ks_body<WT2, KS, XJ, PF, TL>(b, (int)blockIdx.x - g1);
 }
 
 }  // namespace
@@ -864,6 +877,36 @@ int launch_kq_retile(int wtype, const uint8_t *src, uint8_t *dst, int64_t rows, 
     else if (wtype == T_Q4_K) hipLaunchKernelGGL((k_kq_retile<T_Q4_K, false>), dim3(grid), dim3(256), 0, s, src, dst, rows, nsb);
     else if (to_tiled) hipLaunchKernelGGL((k_kq_retile<T_Q6_K, true>), dim3(grid), dim3(256), 0, s, src, dst, rows, nsb);
     else hipLaunchKernelGGL((k_kq_retile<T_Q6_K, false>), dim3(grid), dim3(256), 0, s, src, dst, rows, nsb);
+    GHIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_matvec_kq2(int t1, const kq_args &a, int t2, const kq_args &b, hipStream_t s) {
+    const bool ok = (t1 == T_Q4_K || t1 == T_Q6_K) && (t2 == T_Q4_K || t2 == T_Q6_K) && a.nsb == b.nsb &&
+                    a.nsb % 8 == 0 && a.nsb >= 8 && a.nsb <= 16 && a.ncols == 1 && b.ncols == 1 && a.pro == b.pro &&
+                    a.q8_mode == KQO_NONE && b.q8_mode == KQO_NONE && !a.w2 && !b.w2 && a.tiled == b.tiled &&
+                    a.rows % 8 == 0 && b.rows > 0 && (a.rows + 7) / 8 + (b.rows + 7) / 8 < 2048 &&
+                    (a.pro == KQP_COPY ? (a.x && b.x) : (a.xf && b.xf && !((uintptr_t)a.xf & 15) && a.xf_col_stride % 4 == 0 &&
+                                                           (a.pro != KQP_NORM || (a.norm_w && !((uintptr_t)a.norm_w & 15)))));
+    if (!ok) {
+        set_error("matvec_kq2: the pair needs one K <= 4096 (multiple of 2048), one column, the same prologue, no hand-off");
+        return -1;
+    }
+    const size_t img0 = (size_t)a.nsb * 292;
+    const size_t red = a.pro == KQP_NORM ? ((img0 + 15) & ~(size_t)15) + (size_t)a.nsb * 64 * sizeof(double) : 0;
+    const size_t lds = std::max((size_t)a.nsb * (292 + 64 * 4 * 2 + 8 * 4 * 2), red);
+    const int g1 = (int)((a.rows + 7) / 8), g2 = (int)((b.rows + 7) / 8);
+    const dim3 grid((unsigned)(g1 + g2), 1);
+#define GHIP_KQ2(A, B)                                                                                       \
+    do {                                                                                                     \
+        if (a.tiled) hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, 2, 2, true>), grid, dim3(512), lds, s, a, b, g1);  \
+        else hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, 2, 2, false>), grid, dim3(512), lds, s, a, b, g1);          \
+    } while (0)
+    if (t1 == T_Q4_K && t2 == T_Q4_K) GHIP_KQ2(T_Q4_K, T_Q4_K);
+    else if (t1 == T_Q4_K) GHIP_KQ2(T_Q4_K, T_Q6_K);
+    else if (t2 == T_Q4_K) GHIP_KQ2(T_Q6_K, T_Q4_K);
+    else GHIP_KQ2(T_Q6_K, T_Q6_K);
+#undef GHIP_KQ2
     GHIP_CHECK(hipGetLastError());
     return 0;
 }
