@@ -228,10 +228,9 @@ struct gemma_engine {
     // (DESIGN.md §Activation image); null when a shape does not allow them (then PRO_F32)
     // fused layer front (layer_front.hip): qkv -> attention -> attn-out in one launch per layer;
     // hand-off counters [n_layer][16] zeroed once per token (memset node), sticky timeout word
-    // K-quant layers: kq_fuse = the plan for where ggml's Q8_K INIT runs (enqueue_step_kq: 0 launches,
-    // 1 consumer prologues, 2 producer hand-offs, 3 norms in prologues + quantizations handed off);
+    // K-quant layers: kq_fuse = the plan for where ggml's Q8_K INIT runs (enqueue_step_kq, 0..6);
     // kq_dual: gate+up in one launch
-    int kq_fuse = 3, kq_dual = 1, kq_pair = 1;  // kq_pair: q|k and v in one launch (GHIP_KQ_PAIR)
+    int kq_fuse = 5, kq_dual = 1, kq_pair = 1, kq_gu2 = 0;  // kq_gu2: GHIP_KQ_GU2 (k_matvec_kq_gu2)  // kq_pair: q|k and v in one launch (GHIP_KQ_PAIR)
     // per-head decode attention: workgroups per head (each the KQ/softmax, 1/att_dsplit of the KQV
     // dims; GHIP_ATT_DSPLIT). Same box, decode tok/s: 1 / 2 / 4 -> 1,443 / 1,458 / 1,458
     int att_dsplit = 2;
@@ -582,14 +581,18 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
     // Images: A = attn-norm(x) -> q|k, v; B = attention out -> o; C = ffn-norm(sa) -> gate/up;
     // D = gelu(gate)*up -> down; each in its own buffer.  e->kq_fuse picks the plan:
     //   0 all LAUNCH; 1 all PROLOGUE; 2 all HANDOFF (measured: the norm tails cost more than a
-    //   launch); 3 (default) norms PROLOGUE, quantizations HANDOFF.
+    //   launch); 3 norms PROLOGUE, quantizations HANDOFF; 4 as 3 with C a LAUNCH; 5 (default) all
+    //   PROLOGUE but D (the attention then keeps two workgroups per head); 6 as 5 with B a LAUNCH.
+    //   Same box, Q4_K_M decode: plan 3 / 5 / 6 -> 997 / 1,017 / 980 tok/s.
     enum { LAUNCH, PROLOGUE, HANDOFF };
-    static const int plan[5][4] = {{LAUNCH, LAUNCH, LAUNCH, LAUNCH},
+    static const int plan[7][4] = {{LAUNCH, LAUNCH, LAUNCH, LAUNCH},
                                    {PROLOGUE, PROLOGUE, PROLOGUE, PROLOGUE},
                                    {HANDOFF, HANDOFF, HANDOFF, HANDOFF},
                                    {PROLOGUE, HANDOFF, PROLOGUE, HANDOFF},
-                                   {PROLOGUE, HANDOFF, LAUNCH, HANDOFF}};
-    const int mode = e->kq_fuse >= 0 && e->kq_fuse <= 4 ? e->kq_fuse : 3;
+                                   {PROLOGUE, HANDOFF, LAUNCH, HANDOFF},
+                                   {PROLOGUE, PROLOGUE, PROLOGUE, HANDOFF},
+                                   {PROLOGUE, LAUNCH, PROLOGUE, HANDOFF}};
+    const int mode = e->kq_fuse >= 0 && e->kq_fuse <= 6 ? e->kq_fuse : 5;
     int srcA = plan[mode][0], srcB = plan[mode][1], srcC = plan[mode][2], srcD = plan[mode][3];
     if (E > 2048) {  // the norm hand-off holds <= 2048 values in one wave
         if (srcA == HANDOFF) srcA = PROLOGUE;
@@ -623,6 +626,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
             k.q8_abl = e->kq_abl;
         }
         if (up) k.w2 = up->w;
+        k.gu2 = e->kq_gu2;
         return k;
     };
     auto mv = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in, const img &in, const out &o,
@@ -967,6 +971,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     if (const char *v = getenv("GHIP_KQ_DUAL")) e->kq_dual = atoi(v);
     if (const char *v = getenv("GHIP_KQ_ABL")) e->kq_abl = atoi(v);
     if (const char *v = getenv("GHIP_KQ_PAIR")) e->kq_pair = atoi(v);
+    if (const char *v = getenv("GHIP_KQ_GU2")) e->kq_gu2 = atoi(v);
     if (const char *v = getenv("GHIP_ATT_DSPLIT")) e->att_dsplit = atoi(v);
     if (e->qw % 128 == 0) {  // whole 4-block groups
         GHIP_FATAL(hipMalloc(&e->att_act, (size_t)e->qw));

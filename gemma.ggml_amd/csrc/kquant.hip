@@ -515,6 +515,87 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
     }
 }
 
+// gate and up (DUAL) with K split in two (K = 512..2048): a 4-wave workgroup takes 2 row groups,
+// wave 2j+h runs group j's super-blocks [h*nsb/2, (h+1)*nsb/2) of both matrices, its whole
+// segment's weight loads issued before the prologue (one round trip, overlapping it).  Wave 2j+1
+// stashes its exact terms; after one barrier wave 2j continues its own chains through them in
+// super-block order — the identical fmaf sequences — then stores gelu(gate)*up (+ the D hand-off).
+template <int WT, int XJ, bool TL>
+__global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq_gu2(kq_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
+    constexpr int HS = 4;  // super-blocks per half (nsb <= 8)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
+    const int col = blockIdx.y, nsb = a.nsb, half = wave & 1, pair = wave >> 1, hs = nsb >> 1;
+    const int64_t g = (int64_t)blockIdx.x * 2 + pair;
+    const int64_t n_groups = (a.rows + 7) / 8;
+    const int64_t gg = g < n_groups ? g : n_groups - 1;
+    const int64_t row_raw = gg * 8 + rr;
+    const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
+    const uint8_t *w1 = a.w + row * a.row_bytes, *w2 = a.w2 + row * a.row_bytes;
+    // stash after the image + norm scratch: [pair][mat][HS][64] sumi, prod; [pair][mat][HS][8] d, dmin
+    const size_t base = (((size_t)nsb * 292 + 15) & ~(size_t)15) + (size_t)nsb * 64 * sizeof(double);
+    int *st_i = (int *)(xs + base) + pair * (2 * HS * 64 * 2);
+    int *st_p = st_i + 2 * HS * 64;
+    float *st_d = (float *)(xs + base) + 2 * (2 * HS * 64 * 2) + pair * (2 * HS * 8 * 2);
+    float *st_m = st_d + 2 * HS * 8;
+    kq_pro_regs<XJ> pr;
+    kq_pro_load<XJ>(a, col, wave, KQ_THREADS / 64, lane, pr);
+    kq_raw<WT> r1[HS], r2[HS];
+#pragma unroll
+    for (int p = 0; p < HS; ++p) {
+        const int sb = half * hs + (p < hs ? p : 0);
+        r1[p] = kq_load<WT, TL>(w1, sb, l);
+        r2[p] = kq_load<WT, TL>(w2, sb, l);
+    }
+    kq_pro_build<XJ>(a, xs, kq_red(xs, nsb), col, tid, KQ_THREADS, pr);
+    __syncthreads();
+    float acc = 0.0f, accm = 0.0f, acc2 = 0.0f, accm2 = 0.0f;
+#pragma unroll
+    for (int p = 0; p < HS; ++p) {
+        if (p >= hs) break;
+        const int sb = half * hs + p;
+        const kq_term t = kq_terms<WT>(r1[p], xs, sb, l);
+        const kq_term u = kq_terms<WT>(r2[p], xs, sb, l);
+        if (half == 0) {
+            acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
+            acc2 = __builtin_fmaf(u.d, (float)u.sumi, acc2);
+            if (WT == T_Q4_K && l < 4) {
+                accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
+                accm2 = __builtin_fmaf(u.dmin, (float)u.prod, accm2);
+            }
+        } else {
+            st_i[p * 64 + lane] = t.sumi;
+            st_i[(HS + p) * 64 + lane] = u.sumi;
+            if (l == 0) {
+                st_d[p * 8 + rr] = t.d;
+                st_d[(HS + p) * 8 + rr] = u.d;
+            }
+            if (WT == T_Q4_K) {
+                st_p[p * 64 + lane] = t.prod;
+                st_p[(HS + p) * 64 + lane] = u.prod;
+                if (l == 0) {
+                    st_m[p * 8 + rr] = t.dmin;
+                    st_m[(HS + p) * 8 + rr] = u.dmin;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (half != 0 || g >= n_groups) return;
+#pragma unroll
+    for (int p = 0; p < HS; ++p) {
+        if (p >= hs) break;
+        acc = __builtin_fmaf(st_d[p * 8 + rr], (float)st_i[p * 64 + lane], acc);
+        acc2 = __builtin_fmaf(st_d[(HS + p) * 8 + rr], (float)st_i[(HS + p) * 64 + lane], acc2);
+        if (WT == T_Q4_K && l < 4) {
+            accm = __builtin_fmaf(st_m[p * 8 + rr], (float)st_p[p * 64 + lane], accm);
+            accm2 = __builtin_fmaf(st_m[(HS + p) * 8 + rr], (float)st_p[(HS + p) * 64 + lane], accm2);
+        }
+    }
+    kq_store_gu<WT>(a, col, row_raw, l, acc, accm, acc2, accm2);
+    if (a.q8_mode != KQO_NONE) kq_handoff(a, col, g, lane, xs);
+}
+
 // T-column form (the batched prefill): NC columns per workgroup share every weight load, so the
 // weights leave L2 / HBM once per NC prompt rows instead of once per row; each (row, column) is
 // still the decode dot in ggml's lane order (one fmaf chain per lane and column), so the result is
@@ -999,6 +1080,22 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     if (a.pro != KQP_COPY && a.nsb > 32) {
         set_error("matvec_kq: fused Q8_K prologue takes at most 32 super-blocks per row on this shape");
         return -1;
+    }
+    // gate/up (DUAL) with K split in two: 2 row groups per 4-wave workgroup (kq_args::gu2; measured
+    // 1,000 vs 1,010 tok/s for the one-wave-per-group form, so off by default)
+    if (a.w2 && a.gu2 && a.nsb % 2 == 0 && a.nsb >= 2 && a.nsb <= 8 && a.rows % 8 == 0) {
+        const size_t lds2 = std::max(((img0 + 15) & ~(size_t)15) + (size_t)a.nsb * 64 * sizeof(double) +
+                                         (size_t)2 * (2 * 4 * 64 * 2 * 4 + 2 * 4 * 8 * 2 * 4), img);
+        const dim3 grid((unsigned)((groups + 1) / 2), a.ncols);
+        if (a.tiled) {
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q4_K, 2, true>), grid, dim3(KQ_THREADS), lds2, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q6_K, 2, true>), grid, dim3(KQ_THREADS), lds2, s, a);
+        } else {
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q4_K, 2, false>), grid, dim3(KQ_THREADS), lds2, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q6_K, 2, false>), grid, dim3(KQ_THREADS), lds2, s, a);
+        }
+        GHIP_CHECK(hipGetLastError());
+        return 0;
     }
     const unsigned grid_x = (unsigned)std::min<int64_t>((groups + 3) / 4, 4096);
     const size_t lds = std::max(img, red);
