@@ -227,21 +227,30 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
     }
     const int nw = nth >> 6, lane = tid & 63, wave = tid >> 6;
     float scale = 1.0f;
+    // this wave holds super-blocks wave and wave + nw: the tree's first level (h = nw*64) pairs
+    // exactly them, so it runs in registers, and their two quantizations interleave
+    const bool two = XJ == 2 && a.nsb == 2 * nw;
     if (a.pro == KQP_NORM) {
+        double part[XJ];
 #pragma unroll
         for (int j = 0; j < XJ; ++j) {
-            const int sb = wave + nw * j;
-            if (sb < a.nsb) {
-                double part = 0.0;
-                part += (double)(r.x[j].x * r.x[j].x);
-                part += (double)(r.x[j].y * r.x[j].y);
-                part += (double)(r.x[j].z * r.x[j].z);
-                part += (double)(r.x[j].w * r.x[j].w);
-                red[sb * 64 + lane] = part;
-            }
+            double pj = 0.0;
+            pj += (double)(r.x[j].x * r.x[j].x);
+            pj += (double)(r.x[j].y * r.x[j].y);
+            pj += (double)(r.x[j].z * r.x[j].z);
+            pj += (double)(r.x[j].w * r.x[j].w);
+            part[j] = pj;
+        }
+        int n = a.nsb * 64;
+        if (two) {
+            red[wave * 64 + lane] = part[0] + part[XJ - 1];
+            n = nw * 64;
+        } else {
+#pragma unroll
+            for (int j = 0; j < XJ; ++j)
+                if (wave + nw * j < a.nsb) red[(wave + nw * j) * 64 + lane] = part[j];
         }
         __syncthreads();
-        int n = a.nsb * 64;
         while (n > 64) {  // cross-wave levels through LDS
             const int h = (n + 1) >> 1;
             for (int i = tid; i + h < n; i += nth) red[i] += red[i + h];
@@ -262,19 +271,25 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
         const float mean = (float)(red[0] / (double)(a.nsb * 256));
         scale = 1.0f / sqrtf(mean + a.eps);
     }
+    float y[XJ][4];
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+        y[j][0] = r.x[j].x; y[j][1] = r.x[j].y; y[j][2] = r.x[j].z; y[j][3] = r.x[j].w;
+        if (a.pro == KQP_NORM) {
+            y[j][0] = pin(y[j][0] * scale) * r.w[j].x;
+            y[j][1] = pin(y[j][1] * scale) * r.w[j].y;
+            y[j][2] = pin(y[j][2] * scale) * r.w[j].z;
+            y[j][3] = pin(y[j][3] * scale) * r.w[j].w;
+        }
+    }
+    if (two) {
+        q8K_store_n<XJ>(y, lane, xs + (int64_t)wave * 292, nw * 292);
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < XJ; ++j) {
         const int sb = wave + nw * j;
-        if (sb < a.nsb) {  // wave-uniform
-            float y[4] = {r.x[j].x, r.x[j].y, r.x[j].z, r.x[j].w};
-            if (a.pro == KQP_NORM) {
-                y[0] = pin(y[0] * scale) * r.w[j].x;
-                y[1] = pin(y[1] * scale) * r.w[j].y;
-                y[2] = pin(y[2] * scale) * r.w[j].z;
-                y[3] = pin(y[3] * scale) * r.w[j].w;
-            }
-            q8K_store(y, lane, xs + (int64_t)sb * 292);
-        }
+        if (sb < a.nsb) q8K_store(y[j], lane, xs + (int64_t)sb * 292);  // wave-uniform
     }
 }
 

@@ -50,11 +50,11 @@ __device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *
     if (lane == 0) *(float *)blk = d;
 }
 
-// q8K_store of N super-blocks at once by one wave (blk + k*292 for block k): the N reductions run
+// q8K_store of N super-blocks at once by one wave (blk + k*stride for block k): the N reductions run
 // interleaved level by level, so the cross-lane latency is paid once per level, not N times.
 // Bytes identical to N calls of q8K_store.
 template <int N>
-__device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, uint8_t *blk) {
+__device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, uint8_t *blk, int stride = 292) {
     float amax[N], mx[N];
     int idx[N];
 #pragma unroll
@@ -101,7 +101,7 @@ __device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, u
             d = (float)(1.0 / (double)iscale);
         }
         bs[k] = q[0] + q[1] + q[2] + q[3];
-        uint8_t *b = blk + k * 292;
+        uint8_t *b = blk + k * stride;
         *(uint32_t *)(b + 4 + lane * 4) =
             (uint32_t)(q[0] & 255) | ((uint32_t)(q[1] & 255) << 8) | ((uint32_t)(q[2] & 255) << 16) | ((uint32_t)q[3] << 24);
         if (lane == 0) *(float *)b = d;
@@ -112,7 +112,7 @@ __device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, u
     for (int k = 0; k < N; ++k) bs[k] += __shfl_xor(bs[k], 2);
 #pragma unroll
     for (int k = 0; k < N; ++k)
-        if ((lane & 3) == 0) *(int16_t *)(blk + k * 292 + 260 + (lane >> 2) * 2) = (int16_t)bs[k];
+        if ((lane & 3) == 0) *(int16_t *)(blk + k * stride + 260 + (lane >> 2) * 2) = (int16_t)bs[k];
 }
 
 }  // namespace ghip
