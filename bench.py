@@ -221,6 +221,10 @@ def main():
     eng.L.gemma_engine_sync(eng.h)
     barrier_sync()
     dt = time.perf_counter() - t0
+    try:  # kernel launches per decode token (the captured graph's kernel nodes; outside the timed region)
+        launches = eng.graph_kernels()
+    except Exception:  # reported as null, never fatal
+        launches = None
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -303,8 +307,10 @@ def main():
             ke.step(args.q8_steps, use_graph=True)
             ke.L.gemma_engine_sync(ke.h)
             kdt = time.perf_counter() - t0
+            k_launches = ke.graph_kernels()
             ke.close()
             kqm = {"model": "Gemma-2B Q4_K_M layout (Q4_K/Q6_K layers, Q6_K output; the reference's shipped format)",
+                   "launches_per_token": k_launches,
                    "tok_s": round(args.q8_steps / kdt, 2), "ms_per_token": round(kdt / args.q8_steps * 1e3, 4),
                    "steps": args.q8_steps, "token_weight_bytes": kbytes,
                    "weight_GB_s": round(kbytes * args.q8_steps / kdt / 1e9, 1),
@@ -412,6 +418,7 @@ def main():
                                    f"{args.prompt}-token prompt (BASELINE config 2); ordered bit-exact path",
                        "n_ctx": args.ctx, "prompt": args.prompt, "parallelism": f"replicas x{world}"},
             "decode_tok_s": round(n_tok / dt, 2),
+            "launches_per_token": launches,
             "prefill_tok_s": prefill["tok_s"] if prefill else None,
             "prefill": prefill,
             "kquant_matvec": kquant,

@@ -1601,6 +1601,28 @@ extern "C" int gemma_engine_plan(gemma_engine *e, int *out, int cap) {
     return n;
 }
 
+// kernel launches per decode token: the kernel nodes of the captured decode graph (captured on
+// first use if needed); -1 on error
+extern "C" int gemma_engine_graph_kernels(gemma_engine *e) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    if (!e->graph) {
+        set_error("gemma_engine_graph_kernels: no decode graph yet (run a gemma_engine_step with use_graph first)");
+        return -1;
+    }
+    size_t n = 0;
+    GHIP_CHECK(hipGraphGetNodes(e->graph, nullptr, &n));
+    std::vector<hipGraphNode_t> nodes(n);
+    GHIP_CHECK(hipGraphGetNodes(e->graph, nodes.data(), &n));
+    int k = 0;
+    for (size_t i = 0; i < n; ++i) {
+        hipGraphNodeType t;
+        GHIP_CHECK(hipGraphNodeGetType(nodes[i], &t));
+        k += t == hipGraphNodeTypeKernel;
+    }
+    return k;
+}
+
 // fused layer front on/off (tests, A/B); returns the sticky hand-off timeout word (0 = none seen)
 extern "C" int gemma_engine_set_fuse(gemma_engine *e, int fuse_front) {
     if (fuse_front >= 0) {

@@ -110,6 +110,7 @@ int gemma_engine_tune(gemma_engine *e, int iters);
 int gemma_engine_plan(gemma_engine *e, int *out, int cap);
 int gemma_engine_set_plan(gemma_engine *e, const int *in, int n);
 int gemma_engine_set_fuse(gemma_engine *e, int fuse_front); /* fused layer front on/off (-1 = keep); returns the hand-off timeout word */
+int gemma_engine_graph_kernels(gemma_engine *e);            /* kernel launches per decode token (captured graph) */
 /* debugging: one eager step with per-layer taps [n_layer][qkv | attn_out | layer_out] */
 int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
 /* diagnostics: prefill (exact != 0: the exact path) with the residual stream after each layer
