@@ -2144,6 +2144,15 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
 }
 
 int gemma_engine_ext_prefill(gemma_engine *e, const int32_t *tokens, int T, float *logits_all) {
+    if (T <= 0 || T >= e->cfg.n_ctx) {
+        set_error("gemma_engine_ext_prefill: prompt length out of range");
+        return -1;
+    }
+    for (int i = 0; i < T; ++i)
+        if (tokens[i] < 0 || tokens[i] >= e->cfg.n_vocab) {
+            set_error("gemma_engine_ext_prefill: token id out of range");
+            return -1;
+        }
     if (!e->graph_exec) {
         // the decode step's first launches (code-object loading, LDS attributes) and its graph
         // capture happen here, in the prompt's call, instead of in the first generated token: one
