@@ -22,6 +22,14 @@ def kind(name):
     """decode matvec instance -> bench kernel id (0 gate/up, 1 down, 2 qkv, 3 attn-out, 4 logits)."""
     if "k_matvec" not in name:
         return None
+    if "k_matvec_rr<" in name:  # round-pipelined form: k_matvec_rr<WT, PRO, EPI, NR, ...>
+        args = name[name.index("<") + 1:name.index(">")].split(",")
+        epi, nr = int(args[2]), int(args[3])
+        if epi == 0:
+            return 2
+        if epi == 1:
+            return 1 if nr >= 8 else 3
+        return None
     # k_matvec<WT, KS, PRO, EPI, ...>: PRO 0 F32, 1 NORM, 2 Q8, 3 EMBED; EPI 0 STORE, 1 ADD, 2 GELU_MUL, 3 ARGMAX
     args = name[name.index("<") + 1:name.index(">")].split(",")
     ks, pro, epi = int(args[1]), int(args[2]), int(args[3])
