@@ -442,7 +442,8 @@ def main():
                                                        "frac": round(v[1] / (v[0] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                                                        "frac_of_measured": (round(v[1] / (v[0] * 1e-6) / 1e9 / hbm_measured, 4)
                                                                             if hbm_measured > 0 else None),
-                                                       "launches_per_token": KERNEL_CALLS_PER_TOKEN[k]}
+                                                       "launches_per_token": KERNEL_CALLS_PER_TOKEN[k],
+                                                       "traffic": load_traffic(k)}
                                      for k, v in kern.items()}},
             "kernels_us": {KERNEL_NAMES[k]: round(v[0], 3) for k, v in kern.items()},
             "token_weight_bytes": 1409679360 if args.wtype == "q4_0" else 2662727680,
