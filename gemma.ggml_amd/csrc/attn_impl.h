@@ -327,7 +327,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         float e = 0.0f;
         if (w != -INFINITY) e = h2f(exp_f16_of(f2h(w - mx)));
         // e is fp16 in [0,1]: an exact multiple of 2^-24, so the integer sum is the exact sum
-        isum += (unsigned long long)(e * 16777216.0f);
+        isum += (unsigned long long)(uint32_t)(e * 16777216.0f);  // e*2^24 <= 2^24: exact in u32 (one v_cvt_u32_f32)
         const int r = k - wave;
         if (r >= 0 && r % nwave == 0) {
             const int m = r / nwave;

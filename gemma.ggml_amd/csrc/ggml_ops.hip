@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(256) k_g_soft_max(gt_desc a, gt_desc mask, int
     for (int64_t k = threadIdx.x; k < n; k += 256) {
         const float w = w_at(k);
         const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
-        isum += (unsigned long long)(e * 16777216.0f);
+        isum += (unsigned long long)(uint32_t)(e * 16777216.0f);  // e*2^24 <= 2^24: exact in u32 (one v_cvt_u32_f32)
     }
     isum = wave_sum_u64(isum);
     if (lane == 0) redu[wave] = isum;

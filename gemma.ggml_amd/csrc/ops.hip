@@ -441,7 +441,7 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
             uint16_t e16 = 0;
             if (w != -INFINITY) e16 = (uint16_t)exp_f16_of(f2h(w - mx));
             prow[j] = e16;
-            isum += (unsigned long long)(h2f(e16) * 16777216.0f);
+            isum += (unsigned long long)(uint32_t)(h2f(e16) * 16777216.0f);
         }
         const unsigned long long tot = wave_sum_u64(isum);
         const double sum = (double)tot * (1.0 / 16777216.0);
@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
         for (int j = lane; j < n_kv; j += 64) {
             const float w = Sr[j];
             const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
-            isum += (unsigned long long)(e * 16777216.0f);
+            isum += (unsigned long long)(uint32_t)(e * 16777216.0f);  // e*2^24 <= 2^24: exact in u32 (one v_cvt_u32_f32)
         }
         const unsigned long long tot = wave_sum_u64(isum);
         const double sum = (double)tot * (1.0 / 16777216.0);

@@ -790,7 +790,7 @@ __global__ void __launch_bounds__(256) k_attn_prefill(attnp_args a) {
                         uint32_t e16 = 0;
                         if (live) e16 = exp_f16_of(f2h(w - mx[v]));
                         if (pass == 1) {
-                            isum[v] += (unsigned long long)(h2f(e16) * 16777216.0f);
+                            isum[v] += (unsigned long long)(uint32_t)(h2f(e16) * 16777216.0f);
                         } else {
                             Ps[(16 * wave + kg * 4 + v) * AP_VS + c * 16 + l16] = (uint16_t)f2h(h2f(e16) * inv[v]);
                         }
