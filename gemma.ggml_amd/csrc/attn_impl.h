@@ -316,7 +316,33 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     __syncthreads();
     AH_STAMP(2);
     // ---- soft_max_ext: every wave reduces the whole row (DPP) and writes P16 for its
-    // own slice j = 64*wave + lane + NTH*m: one barrier for the whole softmax
+    // own slice j = 64*wave + lane + NTH*m: one barrier for the whole softmax.  Rows of up to 512
+    // positions: the lane's 8 scores are read in one batch (one LDS round trip, not one per step)
+    if (n_kv <= 512 && NTH >= 512) {
+        float sv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sv[k] = lane + 64 * k < n_kv ? S[lane + 64 * k] : -INFINITY;
+        float mx = sv[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) mx = fmaxf(mx, sv[k]);
+        mx = wave_max(mx);
+        unsigned long long isum = 0;
+        float own = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float e = sv[k] != -INFINITY ? h2f(exp_f16_of(f2h(sv[k] - mx))) : 0.0f;
+            isum += (unsigned long long)(uint32_t)(e * 16777216.0f);  // exact: e*2^24 <= 2^24
+            if (k == wave) own = e;  // this thread's P16 element j = tid = 64*wave + lane
+        }
+        const unsigned long long tot = wave_sum_u64(isum);
+        const double sum = (double)tot * (1.0 / 16777216.0);
+        const float inv = (float)(1.0 / sum);
+        if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
+        if (tid < n_kv) {
+            P16[tid] = f2h(own * inv);
+            if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + tid] = P16[tid];
+        }
+    } else {
     float mx = -INFINITY;
     for (int j = lane; j < n_kv; j += 64) mx = fmaxf(mx, S[j]);
     mx = wave_max(mx);
@@ -348,6 +374,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         }
         P16[j] = f2h(e * inv);
         if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
+    }
     }
     __syncthreads();
     AH_STAMP(3);
