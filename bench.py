@@ -309,13 +309,30 @@ def main():
             kdt = time.perf_counter() - t0
             k_launches = ke.graph_kernels()
             ke.close()
+            # BASELINE config 3's prompt length in the shipped format: the batched exact prefill at
+            # T = args.prefill (one untimed pass, then one timed)
+            kp2 = None
+            if args.prefill > 0:
+                kpe = G.Engine(GEMMA_2B, n_ctx=args.prefill + 64, wtype=G.GGML_TYPE_Q4_K, device=local_rank)
+                kpp = make_prompt(args.prefill, GEMMA_2B["n_vocab"], seed=2)
+                kpe.begin(kpp)
+                kpe.prefill(args.prefill)
+                kpe.begin(kpp)
+                kpe.L.gemma_engine_sync(kpe.h)
+                tp0 = time.perf_counter()
+                kpe.prefill(args.prefill)
+                kp2_s = time.perf_counter() - tp0
+                kpe.close()
+                kp2 = {"T": args.prefill, "ms": round(kp2_s * 1e3, 3), "tok_s": round(args.prefill / kp2_s, 1),
+                       "exact": True}
             kqm = {"model": "Gemma-2B Q4_K_M layout (Q4_K/Q6_K layers, Q6_K output; the reference's shipped format)",
                    "launches_per_token": k_launches,
                    "tok_s": round(args.q8_steps / kdt, 2), "ms_per_token": round(kdt / args.q8_steps * 1e3, 4),
                    "steps": args.q8_steps, "token_weight_bytes": kbytes,
                    "weight_GB_s": round(kbytes * args.q8_steps / kdt / 1e9, 1),
                    "prefill": {"T": args.prompt, "ms": round(kpf_s * 1e3, 3),
-                               "tok_s": round(args.prompt / kpf_s, 1), "exact": True}}
+                               "tok_s": round(args.prompt / kpf_s, 1), "exact": True},
+                   "prefill_long": kp2}
         except Exception as ex:  # reported, never fatal to the headline line
             kqm = {"error": str(ex)[:300]}
 
