@@ -673,6 +673,33 @@ int try_fast(ggml_cgraph *g) {
 extern "C" {
 
 // ---- context and sizes -------------------------------------------------------------------------
+// Arenas of freed contexts are kept (up to 4) and handed to the next ggml_init of the same size:
+// the reference re-creates its compute context every token (src/gemma_model.cpp), and a fresh
+// mmap'ed arena page-faults on every first write (the logits row alone is 256 pages).  ggml_init
+// never promised zeroed memory.
+namespace {
+std::mutex arena_mu;
+std::vector<std::pair<size_t, char *>> arena_pool;
+char *arena_get(size_t bytes) {
+    std::lock_guard<std::mutex> lk(arena_mu);
+    for (size_t i = 0; i < arena_pool.size(); ++i)
+        if (arena_pool[i].first == bytes) {
+            char *p = arena_pool[i].second;
+            arena_pool.erase(arena_pool.begin() + (long)i);
+            return p;
+        }
+    return (char *)aligned_alloc(64, bytes);
+}
+void arena_put(size_t bytes, char *p) {
+    std::lock_guard<std::mutex> lk(arena_mu);
+    if (arena_pool.size() >= 4) {
+        free(arena_pool.front().second);
+        arena_pool.erase(arena_pool.begin());
+    }
+    arena_pool.emplace_back(bytes, p);
+}
+}  // namespace
+
 struct ggml_context *ggml_init(struct ggml_init_params params) {
     ggml_context *c = new ggml_context();
     c->mem_size = params.mem_size;
@@ -680,7 +707,7 @@ struct ggml_context *ggml_init(struct ggml_init_params params) {
     if (params.mem_buffer) {
         c->mem = (char *)params.mem_buffer;
     } else if (params.mem_size) {
-        c->mem = (char *)aligned_alloc(64, (params.mem_size + 63) & ~(size_t)63);
+        c->mem = arena_get((params.mem_size + 63) & ~(size_t)63);
         c->owns_mem = true;
     }
     return c;
@@ -712,7 +739,7 @@ void ggml_free(struct ggml_context *ctx) {
         delete[] g->leafs;
         delete g;
     }
-    if (ctx->owns_mem) free(ctx->mem);
+    if (ctx->owns_mem) arena_put((ctx->mem_size + 63) & ~(size_t)63, ctx->mem);
     delete ctx;
 }
 
