@@ -232,8 +232,9 @@ struct gemma_engine {
     // kq_dual: gate+up in one launch
     int kq_fuse = 5, kq_dual = 1, kq_pair = 1, kq_gu2 = 0;  // kq_gu2: GHIP_KQ_GU2 (k_matvec_kq_gu2)  // kq_pair: q|k and v in one launch (GHIP_KQ_PAIR)
     // per-head decode attention: workgroups per head (each the KQ/softmax, 1/att_dsplit of the KQV
-    // dims; GHIP_ATT_DSPLIT). Same box, decode tok/s: 1 / 2 / 4 -> 1,443 / 1,458 / 1,458
-    int att_dsplit = 2;
+    // dims; GHIP_ATT_DSPLIT). Same box, decode tok/s: 1 / 2 / 4 -> 1,443 / 1,458 / 1,458; after the
+    // batched K/V step loads 2 / 4 / 8 -> 1,470-1,482 / 1,491 / 1,355-1,369 (scripts/env_ab.sh)
+    int att_dsplit = 4;
     int kq_abl = 0;  // GHIP_KQ_ABL: hand-off timing ablation (kq_args::q8_abl; wrong results)
     int fuse_front = 0;  // measured: 727 vs 672 us/token (the in-launch hand-offs cost as much as the
                          // launch boundaries they replace; DESIGN.md perf log) — kept as an option
