@@ -158,6 +158,35 @@ __device__ __forceinline__ void image_put_quad_sc1(uint32_t *act, float *da, int
     if (q == 0) st_sc1(da + b, h2f(d16));
 }
 
+// image_put_quad publishing {payload, tag} granules (the persistent token launch's hand-off,
+// MI355X_MICROARCH handoff-1to1): granule i of act is dword i of the image, da[b] the block scale
+typedef __attribute__((address_space(1))) unsigned long long gull_t;
+__device__ __forceinline__ void put_granule(unsigned long long *g, uint32_t tag, uint32_t v) {
+    __hip_atomic_store((gull_t *)g, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void image_put_quad_gran(unsigned long long *act, unsigned long long *da, uint32_t tag, int64_t b,
+                                                    int q, const float v[8]) {
+    float amax = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    amax = fmaxf(amax, dpp_f<0xB1>(amax));
+    amax = fmaxf(amax, dpp_f<0x4E>(amax));
+    const float d = amax / 127.f;
+    const uint32_t d16 = f2h(d);
+    const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        const int l = 2 * q + hh;
+        int qi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qi[k] = (int)__builtin_rintf(v[4 * hh + k] * id);
+        const uint32_t packed = (uint32_t)(qi[0] & 0xFF) | ((uint32_t)(qi[1] & 0xFF) << 8) |
+                                ((uint32_t)(qi[2] & 0xFF) << 16) | ((uint32_t)(qi[3] & 0xFF) << 24);
+        put_granule(act + ((b >> 2) * 8 + l) * 4 + (b & 3), tag, packed);
+    }
+    if (q == 0) put_granule(da + b, tag, __builtin_bit_cast(uint32_t, h2f(d16)));
+}
+
 constexpr int AH_THREADS = 1024;  // per-head form: 256 quads = 256 KQ positions / KQV dims per pass
 #ifndef GHIP_AH_PF
 #define GHIP_AH_PF 4
@@ -179,8 +208,8 @@ struct attn_pre {
 };
 template <int NTH, int KPF, int VPF>
 __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, attn_pre<KPF, VPF> &p, int d_lo = 0,
-                                              int d_hi = 1 << 30) {
-    const int hd = a.hd, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
+                                              int d_hi = 1 << 30, int tid_in = -1) {
+    const int hd = a.hd, tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, t4 = tid & 3, quad = tid >> 2;
     const int G = a.H / a.Hkv, kvh = h / G, kvw = a.Hkv * hd;
     p.pos_v = ((const int *)a.rope_cur)[hd];  // published with the row (k_advance / begin)
     {
@@ -204,8 +233,10 @@ __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, a
 // each CU streams.
 template <int NTH, bool SC1, int KPF = AH_KPF, int VPF = AH_VPF, bool PRE = false>
 __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, const attn_pre<KPF, VPF> *pre = nullptr,
-                              const int sp = 0) {
-    const int hd = a.hd, half = hd / 2, tid = threadIdx.x, t4 = tid & 3, quad = tid >> 2;
+                              const int sp = 0, const int tid_in = -1) {
+    // tid_in: the caller's (opaque) thread index, so that a persistent caller's loop does not keep
+    // this function's per-lane addresses live across its other phases
+    const int hd = a.hd, half = hd / 2, tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, t4 = tid & 3, quad = tid >> 2;
     const int dsz = hd / (a.dsplit > 1 ? a.dsplit : 1), d_lo = sp * dsz, d_hi = d_lo + dsz;
     const int lane = tid & 63, wave = tid >> 6, nwave = NTH / 64;
     const int G = a.H / a.Hkv, kvh = h / G;
@@ -226,7 +257,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         ca = *(const float4 *)(cs + i4); sa = *(const float4 *)(sn + i4);
     }
     attn_pre<KPF, VPF> own;
-    if (!PRE) attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi);
+    if (!PRE) attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi, tid);
     const attn_pre<KPF, VPF> &P = PRE ? *pre : own;
     const int pos_v = P.pos_v;
     const uint4 *kpre = P.k, *vpre = P.v;
@@ -443,7 +474,18 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         const float o = quad_reduce_f16(acc);
         if (t4 == 0) {
             a.out[(int64_t)h * hd + d] = o;
-            if (a.out_act || a.out_q8k) ((float *)smem)[d] = o;  // q16|k16 (hd floats) are dead after KQ
+            if (a.out_act || a.out_q8k || a.out_gran) ((float *)smem)[d] = o;  // q16|k16 (hd floats) are dead after KQ
+        }
+    }
+    if (a.out_gran) {  // the same image, handed on as granules inside the persistent launch
+        __syncthreads();
+        if (tid < dsz / 8) {
+            const int b = d_lo / 32 + (tid >> 2);
+            const float *o = (const float *)smem + b * 32 + (tid & 3) * 8;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = o[j];
+            image_put_quad_gran(a.out_gran, a.out_gran_da, a.gran_tag, (int64_t)h * (hd / 32) + b, tid & 3, v);
         }
     }
     if (a.out_act) {

@@ -236,6 +236,17 @@ struct gemma_engine {
     // batched K/V step loads 2 / 4 / 8 -> 1,470-1,482 / 1,491 / 1,355-1,369 (scripts/env_ab.sh)
     int att_dsplit = 4;
     int kq_abl = 0;  // GHIP_KQ_ABL: hand-off timing ablation (kq_args::q8_abl; wrong results)
+    // the whole token's layers as ONE persistent launch (token.hip) when the shapes
+    // allow it (GHIP_PERSIST=1 or gemma_engine_set_persist(e, 1)); off by default until it beats
+    // the per-layer launches on the bench
+    int persist = 0;
+    std::string persist_why;           // why the persistent launch cannot run ("" = it can)
+    tok_args tok{};                    // its arguments (host copy; tok_dev: the copy the kernel reads)
+    tok_args *tok_dev = nullptr;
+    tok_layer *tok_tab = nullptr;      // per-layer pointer table
+    unsigned long long *tok_gran = nullptr;  // hand-off granules (zeroed once; tags carry the epoch)
+    unsigned *epoch = nullptr;         // bumped by k_advance / k_set_position once per token
+    int *tok_err = nullptr;            // sticky hand-off timeout [flag, site, layer]
     int fuse_front = 0;  // measured: 727 vs 672 us/token (the in-launch hand-offs cost as much as the
                          // launch boundaries they replace; DESIGN.md perf log) — kept as an option
     unsigned *front_cnt = nullptr;
@@ -364,6 +375,58 @@ static int warm_join(gemma_engine *e) {
 
 static int enqueue_step_kq(gemma_engine *e, const rope_row &rr);
 
+// the persistent token launch's arguments and per-layer table (device copies the kernel reads);
+// sets persist_why to the reason when the launch cannot run this engine
+static int tok_prepare(gemma_engine *e) {
+    const gemma_hip_config &c = e->cfg;
+    e->persist_why.clear();
+    if (e->kq) e->persist_why = "K-quant layers";
+    else if (e->out_type == T_Q6_K) e->persist_why = "Q6_K token_embd (the launch dequantizes the layer type)";
+    else if (e->tp_n != 1 || e->n_virtual != 1) e->persist_why = "row-split TP";
+    if (!e->persist_why.empty() || !e->tok_gran) {
+        if (e->persist_why.empty()) e->persist_why = "no buffers";
+        return 0;
+    }
+    std::vector<tok_layer> tab(c.n_layer);
+    for (int il = 0; il < c.n_layer; ++il) {
+        const layer_dev &L = e->layers[il];
+        tok_layer &T = tab[il];
+        T.qkv_qs = L.qkv.qs; T.qkv_sc = L.qkv.sc; T.o_qs = L.o.qs; T.o_sc = L.o.sc;
+        T.g_qs = L.gate.qs; T.g_sc = L.gate.sc; T.u_qs = L.up.qs; T.u_sc = L.up.sc; T.d_qs = L.down.qs; T.d_sc = L.down.sc;
+        T.attn_norm = L.attn_norm; T.ffn_norm = L.ffn_norm;
+        T.kc = kc_of(e, il); T.vc = vc_of(e, il);
+    }
+    GHIP_CHECK(hipMemcpy(e->tok_tab, tab.data(), tab.size() * sizeof(tok_layer), hipMemcpyHostToDevice));
+    tok_args &a = e->tok;
+    a = tok_args{};
+    a.layers = e->tok_tab;
+    a.n_layer = c.n_layer;
+    a.E = c.n_embd; a.F = c.n_ff; a.H = c.n_head; a.Hkv = c.n_head_kv; a.hd = c.head_dim; a.ctx = c.n_ctx;
+    a.qkv_rows = e->qkv_rows;
+    a.att_split = e->att_dsplit;
+    a.eps = c.eps; a.emb_scale = sqrtf((float)c.n_embd); a.q_scale = 1.0f / sqrtf((float)c.head_dim);
+    a.emb_qs = e->embd.qs; a.emb_sc = e->embd.sc; a.emb_n_bt = e->embd.n_bt;
+    a.hist = e->hist; a.pos = e->pos; a.rope_cur = e->rope_cur;
+    a.exp_tab = e->exp_tab; a.gelu_tab = e->gelu_tab; a.gelu_clamp = c.gelu_clamp;
+    const tok_gran_sizes g = token_gran_sizes(c.n_embd, c.n_ff, e->qkv_rows);
+    unsigned long long *p = e->tok_gran;
+    a.gx = p; p += g.gx;
+    a.gqkv = p; p += g.gqkv;
+    a.gatt = p; p += g.gatt;
+    a.gatt_da = p; p += g.gatt_da;
+    a.gsa = p; p += g.gsa;
+    a.gh = p; p += g.gh;
+    a.gh_da = p;
+    a.epoch = e->epoch; a.x_out = e->x; a.att_out = e->attn; a.err = e->tok_err;
+    e->persist_why = token_unsupported(c.wtype, a);
+    GHIP_CHECK(hipMemcpy(e->tok_dev, &a, sizeof(tok_args), hipMemcpyHostToDevice));
+    return 0;
+}
+static bool persist_on(const gemma_engine *e) {
+    return e->persist && e->persist_why.empty() && !e->dbg && !e->stamp && e->att_mode == ATTN_PER_HEAD && !e->warm &&
+           !e->fuse_front;
+}
+
 static int enqueue_step(gemma_engine *e) {
     const gemma_hip_config &c = e->cfg;
     const int wt = c.wtype;
@@ -372,11 +435,17 @@ static int enqueue_step(gemma_engine *e) {
     if (e->kq) {
         rope_row rr;
         rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+        rr.epoch = e->epoch;
         return enqueue_step_kq(e, rr);
     }
     if (e->out_type == T_Q6_K &&
         launch_embed_q6K(e->embd_q6k, e->embd_row_bytes, e->hist, e->pos, 1, E, sqrtf((float)E), e->x, s, e->embd_tiled))
         return -1;
+    if (persist_on(e)) {  // every layer in one launch (token.hip), then the logits below
+        if (launch_token(wt, e->tok, e->tok_dev, s)) return -1;
+        goto logits;
+    }
+    {
     const bool front_ok = e->front_cnt && e->fuse_front && e->tp_n == 1 && e->n_virtual == 1 && !e->warm &&
                           e->att_mode == ATTN_PER_HEAD && e->att_act && e->plan[MC_QKV].ks == KS_RR &&
                           e->plan[MC_O].ks == KS_RR && e->plan[MC_O].img;
@@ -523,11 +592,14 @@ static int enqueue_step(gemma_engine *e) {
             GHIP_CHECK(hipMemcpyAsync(e->dbg + (size_t)il * (e->qkv_rows + e->qw + E) + e->qkv_rows + e->qw, e->x,
                                       (size_t)E * 4, hipMemcpyDeviceToDevice, s));
     }
+    }
+logits:
     // K6: rms_norm*output_norm + quantize -> tied output -> logits + argmax  (:736-740, :532-546)
     // K7: token feedback (greedy_sample -> input.push_back, :282-285), position += 1; the prompt is
     // never overwritten: hist writes only land at positions >= n_prompt
     rope_row rr;
     rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+    rr.epoch = e->epoch;
     if (e->out_type == T_Q6_K) {  // rms_norm*out_norm -> Q8_K -> Q6_K tied output -> argmax
         if (launch_norm_q8K(e->x, E, e->out_norm, E, c.eps, 1, e->xq8k, (E / 256) * 292, s)) return -1;
         kq_args k;
@@ -1000,6 +1072,21 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         GHIP_FATAL(hipMemset(e->kq_cnt, 0, (size_t)e->kq_cnt_cap * 128));
         GHIP_FATAL(hipMalloc(&e->kq_g, (size_t)c.n_ff * 4));
     }
+    {  // the persistent token launch: granules, epoch, error word, argument copies
+        const tok_gran_sizes g = token_gran_sizes(c.n_embd, c.n_ff, e->qkv_rows);
+        const size_t n = g.gx + g.gqkv + g.gatt + g.gatt_da + g.gsa + g.gh + g.gh_da;
+        GHIP_FATAL(hipMalloc(&e->tok_gran, n * 8));
+        GHIP_FATAL(hipMemset(e->tok_gran, 0, n * 8));
+        GHIP_FATAL(hipMalloc(&e->epoch, 64));
+        const unsigned one = 1;
+        GHIP_FATAL(hipMemset(e->epoch, 0, 64));
+        GHIP_FATAL(hipMemcpy(e->epoch, &one, 4, hipMemcpyHostToDevice));
+        GHIP_FATAL(hipMalloc(&e->tok_err, 64));
+        GHIP_FATAL(hipMemset(e->tok_err, 0, 64));
+        GHIP_FATAL(hipMalloc(&e->tok_dev, sizeof(tok_args)));
+        GHIP_FATAL(hipMalloc(&e->tok_tab, (size_t)c.n_layer * sizeof(tok_layer)));
+        if (const char *v = getenv("GHIP_PERSIST")) e->persist = atoi(v);
+    }
     GHIP_FATAL(hipMalloc(&e->key, (size_t)e->grid_big * 8));  // per-workgroup argmax keys
     GHIP_FATAL(hipMalloc(&e->pos, 4));
     GHIP_FATAL(hipMalloc(&e->token, 4));
@@ -1024,6 +1111,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         e->plan[MC_DOWN] = {pick_ks(wt, L0.down.n_bt, e->ks_down), 1, 0};
         e->plan[MC_LOGITS] = {1, 1, 0};
     }
+    if (last_error().empty() && !kq_layers) (void)tok_prepare(e);
     if (!last_error().empty()) {
         gemma_engine_free(e);
         return nullptr;
@@ -1195,7 +1283,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
             (void)hipFree(L.ffn_norm);
         }
     }
-    void *bufs[] = {e->front_cnt, e->front_err, e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
+    void *bufs[] = {e->tok_gran, e->epoch, e->tok_err, e->tok_dev, e->tok_tab, e->front_cnt, e->front_err, e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
                     e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf.X, e->pf.SA, e->pf.QKV, e->pf.ATT, e->pf.G, e->pf.U,
                     e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.XH, e->pf.keys};
     for (void *p : bufs)
@@ -1624,6 +1712,31 @@ extern "C" int gemma_engine_graph_kernels(gemma_engine *e) {
     return k;
 }
 
+// the persistent token launch on/off (-1 = keep); returns 1 when it runs this engine's decode
+// steps, 0 when not (hpc_last_error says why if it was asked for)
+extern "C" int gemma_engine_set_persist(gemma_engine *e, int on) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    if (on >= 0 && on != e->persist) {
+        e->persist = on;
+        drop_graph(e);
+    }
+    if (!e->kq && tok_prepare(e)) return -1;
+    if (e->persist && !e->persist_why.empty()) set_error("persistent token launch: " + e->persist_why);
+    return persist_on(e) ? 1 : 0;
+}
+
+// the persistent launch's sticky hand-off timeout words [flag, site, layer] (0 = none seen);
+// reset = 1 clears them
+extern "C" int gemma_engine_persist_err(gemma_engine *e, int *out3, int reset) {
+    (void)hipSetDevice(e->device);
+    int w[3] = {0, 0, 0};
+    if (e->tok_err) GHIP_CHECK(hipMemcpy(w, e->tok_err, 12, hipMemcpyDeviceToHost));
+    if (out3) memcpy(out3, w, 12);
+    if (reset && e->tok_err) GHIP_CHECK(hipMemset(e->tok_err, 0, 64));
+    return w[0];
+}
+
 // fused layer front on/off (tests, A/B); returns the sticky hand-off timeout word (0 = none seen)
 extern "C" int gemma_engine_set_fuse(gemma_engine *e, int fuse_front) {
     if (fuse_front >= 0) {
@@ -1786,6 +1899,7 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
     GHIP_CHECK(hipMemcpyAsync(e->pos, &last, 4, hipMemcpyHostToDevice, s));
     rope_row rr;
     rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+    rr.epoch = e->epoch;
     return launch_advance((const unsigned long long *)p.keys, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s);
 }
 
@@ -1917,6 +2031,39 @@ extern "C" int gemma_engine_stamp_step(gemma_engine *e, int layer, unsigned long
     (void)hipFree(e->stamp);
     e->stamp = nullptr;
     e->stamp_layer = -1;
+    return r;
+}
+
+// diagnostics: one eager step through the persistent token launch with its phase stamps
+// (s_memrealtime, 100 MHz) -> out [grid = n_embd / 8][n_layer][16]; needs a -DGHIP_STAMPS=1 build
+// of token.hip and engine.cpp (scripts/build_variant.sh)
+extern "C" int gemma_engine_token_stamps(gemma_engine *e, unsigned long long *out) {
+    set_error("");
+    if (!GHIP_STAMPS) {
+        set_error("gemma_engine_token_stamps: library built without -DGHIP_STAMPS=1 (scripts/build_variant.sh)");
+        return -1;
+    }
+    (void)hipSetDevice(e->device);
+    if (!persist_on(e)) {
+        set_error("gemma_engine_token_stamps: the persistent launch is not active: " + e->persist_why);
+        return -1;
+    }
+    const size_t n = (size_t)(e->cfg.n_embd / 8) * e->cfg.n_layer * 16;
+    unsigned long long *buf = nullptr;
+    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    GHIP_CHECK(hipMalloc(&buf, n * 8));
+    GHIP_CHECK(hipMemset(buf, 0, n * 8));
+    tok_args a = e->tok;
+    a.dbg_t = buf;
+    GHIP_CHECK(hipMemcpy(e->tok_dev, &a, sizeof(a), hipMemcpyHostToDevice));
+    const int r = enqueue_step(e);
+    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    GHIP_CHECK(hipMemcpy(e->tok_dev, &e->tok, sizeof(e->tok), hipMemcpyHostToDevice));
+    if (r == 0) {
+        GHIP_CHECK(hipMemcpy(out, buf, n * 8, hipMemcpyDeviceToHost));
+        e->host_pos += 1;
+    }
+    (void)hipFree(buf);
     return r;
 }
 
@@ -2108,6 +2255,7 @@ static int ext_set_position(gemma_engine *e, int token, int pos) {
     const gemma_hip_config &c = e->cfg;
     rope_row rr;
     rr.cos = e->rope_cos; rr.sin = e->rope_sin; rr.cur = e->rope_cur; rr.half = c.head_dim / 2; rr.ctx = c.n_ctx;
+    rr.epoch = e->epoch;
     // n_fixed past the history: k_advance must not overwrite hist (the host supplies every token)
     return launch_set_position(token, pos, e->pos, e->hist, e->nfix, c.n_ctx + 1, rr, e->stream);
 }

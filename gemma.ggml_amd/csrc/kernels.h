@@ -240,6 +240,10 @@ struct attn_args {
     float *sbuf = nullptr;
     int *sync = nullptr;
     int *err = nullptr;
+    // per-head mode inside the persistent token launch: the output's Q8_0 image published as
+    // {payload, tag} granules (act dwords in the image's dword order, block scales) instead of stores
+    unsigned long long *out_gran = nullptr, *out_gran_da = nullptr;
+    uint32_t gran_tag = 0;
 };
 // the front half of a decode layer in one launch (layer_front.hip): qkv (rr, PRO_NORM, EPI_STORE)
 // -> per-head attention -> attn-out (rr, PRO_IMG from the attention's image, EPI_ADD)
@@ -253,6 +257,46 @@ struct front_args {
 };
 bool layer_front_supported(int wtype, const mv_args &q, const attn_args &t, const mv_args &o);
 int launch_layer_front(int wtype, const front_args &f, hipStream_t s);
+
+// ---- the whole decode token's layers as ONE persistent launch (token.hip) ----------
+// per layer: device pointers of the tiled matrices, norms and KV caches (a table in device memory,
+// read through the scalar cache: immutable for the launch)
+struct tok_layer {
+    const uint8_t *qkv_qs = nullptr, *qkv_sc = nullptr, *o_qs = nullptr, *o_sc = nullptr;
+    const uint8_t *g_qs = nullptr, *g_sc = nullptr, *u_qs = nullptr, *u_sc = nullptr, *d_qs = nullptr, *d_sc = nullptr;
+    const float *attn_norm = nullptr, *ffn_norm = nullptr;
+    uint16_t *kc = nullptr, *vc = nullptr;
+};
+struct tok_args {
+    const tok_layer *layers = nullptr;
+    int n_layer = 0;
+    int E = 0, F = 0, H = 0, Hkv = 0, hd = 0, ctx = 0, qkv_rows = 0;
+    int att_split = 0;  // workgroups per query head (each the KQ / softmax and hd / att_split KQV dims)
+    float eps = 0.f, emb_scale = 1.f, q_scale = 1.f;
+    const uint8_t *emb_qs = nullptr, *emb_sc = nullptr;  // tied embedding (tiled, layer type)
+    int64_t emb_n_bt = 0;
+    const int *hist = nullptr, *pos = nullptr;
+    const float *rope_cur = nullptr;
+    const uint16_t *exp_tab = nullptr, *gelu_tab = nullptr;
+    int gelu_clamp = 0;
+    // in-launch hand-offs: 8-byte {payload, tag} granules (MI355X_MICROARCH handoff-1to1 / allgather)
+    unsigned long long *gx = nullptr, *gqkv = nullptr, *gatt = nullptr, *gatt_da = nullptr, *gsa = nullptr,
+                       *gh = nullptr, *gh_da = nullptr;
+    const unsigned *epoch = nullptr;  // bumped by k_advance / k_set_position: tags are unique per token
+    float *x_out = nullptr;           // the last layer's output x (the logits launch's input)
+    float *att_out = nullptr;         // attention output scratch (written, unused)
+    int *err = nullptr;               // [0] sticky hand-off timeout, [1] site, [2] layer
+    unsigned long long *dbg_t = nullptr;  // stamps build: [grid][n_layer][16] s_memrealtime
+};
+// granules each buffer holds for shapes (E, F, qkv_rows)
+struct tok_gran_sizes {
+    size_t gx, gqkv, gatt, gatt_da, gsa, gh, gh_da;
+};
+tok_gran_sizes token_gran_sizes(int E, int F, int qkv_rows);
+// "" if the shapes / device allow the persistent token launch, else the reason
+std::string token_unsupported(int wtype, const tok_args &a);
+// a: the args on the host (checked), ap: the same args in device memory (what the kernel reads)
+int launch_token(int wtype, const tok_args &a, const tok_args *ap, hipStream_t s);
 
 struct attn_geom {
     int nwg = 0, grid = 0;
@@ -271,6 +315,7 @@ struct rope_row {  // k_advance also publishes the new position's RoPE row: cur 
     const float *cos = nullptr, *sin = nullptr;
     float *cur = nullptr;
     int half = 0, ctx = 0;
+    unsigned *epoch = nullptr;  // if set, incremented (the persistent token launch's granule tags)
 };
 // read `n` weight regions with allocating loads (MALL warm-up for a later kernel), `grid` workgroups
 int launch_mall_warm(const void *const *ptrs, const int64_t *bytes, int n, int grid, hipStream_t s);

@@ -716,6 +716,7 @@ __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys,
         if (hist && p < hist_cap && p >= *n_fixed) hist[p] = idx;  // never overwrite the prompt
         *pos = p;
         sp = p;
+        if (r.epoch) ++*r.epoch;  // a new token: fresh granule tags for the persistent launch
     }
     __syncthreads();
     // the RoPE row of the next position, at a fixed address (attention loads it without *pos)
@@ -738,6 +739,7 @@ __global__ void __launch_bounds__(256) k_set_position(int token, int p, int *pos
         *pos = p;
         *n_fixed = fixed;
         ((int *)r.cur)[2 * r.half] = p;
+        if (r.epoch) ++*r.epoch;
     }
     for (int i = threadIdx.x; i < r.half; i += 256) {
         r.cur[i] = r.cos[(int64_t)p * r.half + i];

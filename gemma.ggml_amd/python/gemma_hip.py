@@ -23,7 +23,7 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact", "gemma_kq_time", "hpc_graph_compute",
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
-           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs",
+           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs",
            "gemma_tp_unique_id", "gemma_engine_create_tp",
            "gguf_init_from_file", "gguf_free", "gguf_get_n_kv", "gguf_get_key", "gguf_get_kv_type",
            "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
@@ -111,6 +111,8 @@ def lib():
     L.gemma_engine_plan.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     L.gemma_engine_set_plan.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     L.gemma_engine_set_fuse.argtypes = [vp, C.c_int]
+    L.gemma_engine_set_persist.argtypes = [vp, C.c_int]
+    L.gemma_engine_persist_err.argtypes = [vp, vp, C.c_int]
     L.gemma_engine_graph_kernels.argtypes = [vp]
     L.gemma_engine_time.restype = C.c_double
     L.gemma_engine_time.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double)]
@@ -303,6 +305,17 @@ class Engine:
         """fused layer front on (1) / off (0) / unchanged (-1); returns the sticky hand-off timeout
         word (0 = every in-launch hand-off completed in time)"""
         return self.L.gemma_engine_set_fuse(self.h, front)
+
+    def set_persist(self, on=-1):
+        """The decode step's layers as one persistent launch (token.hip): on 1/0, -1 keep; returns
+        True when it runs this engine's steps."""
+        return self.L.gemma_engine_set_persist(self.h, on) == 1
+
+    def persist_err(self, reset=False):
+        """Sticky hand-off timeout words [flag, site, layer] of the persistent launch."""
+        out = (C.c_int * 3)()
+        self.L.gemma_engine_persist_err(self.h, out, 1 if reset else 0)
+        return list(out)
 
     def graph_kernels(self):
         """kernel launches per decode token (the captured decode graph's kernel nodes)"""

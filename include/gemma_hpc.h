@@ -111,6 +111,11 @@ int gemma_engine_plan(gemma_engine *e, int *out, int cap);
 int gemma_engine_set_plan(gemma_engine *e, const int *in, int n);
 int gemma_engine_set_fuse(gemma_engine *e, int fuse_front); /* fused layer front on/off (-1 = keep); returns the hand-off timeout word */
 int gemma_engine_graph_kernels(gemma_engine *e);            /* kernel launches per decode token (captured graph) */
+/* the decode step's layers as ONE persistent launch (default where the shapes allow it; -1 = keep):
+ * returns 1 when it runs this engine's steps, 0 when not (hpc_last_error says why) */
+int gemma_engine_set_persist(gemma_engine *e, int on);
+/* its sticky hand-off timeout words [flag, site, layer]; returns the flag (0 = none); reset clears */
+int gemma_engine_persist_err(gemma_engine *e, int *out3, int reset);
 /* debugging: one eager step with per-layer taps [n_layer][qkv | attn_out | layer_out] */
 int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
 /* diagnostics: prefill (exact != 0: the exact path) with the residual stream after each layer
@@ -120,6 +125,9 @@ int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps, int exact);
  * kernels (regions 0..4: qkv, attention, attn-out, gate/up, down) and the logits kernel (region 5);
  * out = 6 * 4096 * 16 u64, slot [region][workgroup][phase], unused slots 0 */
 int gemma_engine_stamp_step(gemma_engine *e, int layer, unsigned long long *out);
+/* diagnostics: one eager step through the persistent launch with its phase stamps
+ * -> out [n_embd / 8][n_layer][16] u64 (GHIP_STAMPS build) */
+int gemma_engine_token_stamps(gemma_engine *e, unsigned long long *out);
 /* per-op test entry: one decode-attention block on host buffers (caches updated in place);
  * mode 0 = one workgroup per head, 1 = position-split form with the in-kernel hand-off */
 int gemma_test_attn_decode(const float *qkv, uint16_t *kc, uint16_t *vc, int pos, int H, int Hkv, int hd, int ctx,
