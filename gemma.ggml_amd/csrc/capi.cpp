@@ -17,6 +17,7 @@
 #include <tuple>
 
 #include "../../include/gemma_hpc.h"
+#include "ggml_impl.h"
 #include "kernels.h"
 
 namespace ghip {
@@ -173,6 +174,7 @@ extern "C" int hpc_weight_cache_entries(void) { return (int)(st().weights.size()
 // The cache is keyed by the host pointer: a caller that frees or rewrites a src0 buffer calls this
 // first, or a later buffer at the same address would be served the stale device copy.
 extern "C" int hpc_unregister_weight(const void *host) {
+    ggml_fast_drop(host);
     hpc_state &s = st();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (s.inited) (void)hipStreamSynchronize(s.stream);  // no launch may still read a freed copy
@@ -199,6 +201,7 @@ extern "C" int hpc_unregister_weight(const void *host) {
 }
 
 extern "C" void hpc_flush_weights(void) {
+    ggml_fast_drop(nullptr);
     hpc_state &s = st();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
     if (s.inited) (void)hipStreamSynchronize(s.stream);

@@ -1046,6 +1046,10 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     if (const char *v = getenv("GHIP_KQ_PAIR")) e->kq_pair = atoi(v);
     if (const char *v = getenv("GHIP_KQ_GU2")) e->kq_gu2 = atoi(v);
     if (const char *v = getenv("GHIP_ATT_DSPLIT")) e->att_dsplit = atoi(v);
+    // launch_attn_decode needs head_dim % (32 * dsplit) == 0: the largest of 4 / 2 / 1 that divides
+    // (head_dim 32 / 64 / 96 / 160 / ... take fewer workgroups per head, never a failing step)
+    if (e->att_dsplit < 1) e->att_dsplit = 1;
+    while (e->att_dsplit > 1 && (c.head_dim % (32 * e->att_dsplit) || (e->att_dsplit & (e->att_dsplit - 1)))) --e->att_dsplit;
     if (e->qw % 128 == 0) {  // whole 4-block groups
         GHIP_FATAL(hipMalloc(&e->att_act, (size_t)e->qw));
         GHIP_FATAL(hipMalloc(&e->att_da, (size_t)e->qw / 32 * 4));
@@ -2048,7 +2052,7 @@ extern "C" int gemma_engine_token_stamps(gemma_engine *e, unsigned long long *ou
         set_error("gemma_engine_token_stamps: the persistent launch is not active: " + e->persist_why);
         return -1;
     }
-    const size_t n = (size_t)(e->cfg.n_embd / 8) * e->cfg.n_layer * 16;
+    const size_t n = (size_t)(e->cfg.n_embd / 8) * e->cfg.n_layer * 16 + 256;  // + per-pop probes
     unsigned long long *buf = nullptr;
     GHIP_CHECK(hipStreamSynchronize(e->stream));
     GHIP_CHECK(hipMalloc(&buf, n * 8));

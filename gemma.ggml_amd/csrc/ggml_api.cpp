@@ -434,6 +434,7 @@ struct gemma_match {
     std::vector<int32_t> tokens;
     int T = 0;
     int pos0 = 0;
+    std::vector<const ggml_tensor *> stores;  // the matched K / V cache CPY nodes
 };
 
 bool op_is(const ggml_tensor *t, int op) { return t && t->op == op; }
@@ -549,6 +550,14 @@ bool match_gemma(ggml_cgraph *g, gemma_match &m, std::string &why) {
         const int kh = (int)(off_k / (kvw * 2));
         if (kvhead >= 0 && kh != kvhead) return fail("kv head");
         kvhead = kh;
+        // the V store: view_2d(v, T, kvw, n_ctx * 2, kv_head * 2) of the transposed cache
+        // (src/gemma_model.cpp:510-512): element kv_head of every dimension row
+        const ggml_tensor *vview = vs->second->src[1];
+        const int64_t vctx = ggml_nelements(vroot) / kvw;
+        if ((int64_t)((char *)vview->data - (char *)vroot->data) != (int64_t)kh * 2 || vview->nb[1] != (size_t)vctx * 2)
+            return fail("v store view");
+        m.stores.push_back(ks->second);
+        m.stores.push_back(vs->second);
         const int types[7] = {(int)qm->src[0]->type, (int)km->src[0]->type, (int)vm->src[0]->type, (int)sa->src[0]->src[0]->type,
                               (int)gt->src[0]->type, (int)ut->src[0]->type, (int)dn->src[0]->type};
         for (int t : types)
@@ -599,18 +608,47 @@ bool match_gemma(ggml_cgraph *g, gemma_match &m, std::string &why) {
         }
     }
     if (last->ne[1] != m.T || !last->data || !is_contiguous(last)) return fail("output rows");
+    // exactly that graph: every node is an ancestor of the logits or one of the matched cache
+    // stores (an extra side node, e.g. a second output or another CPY, would be skipped otherwise)
+    std::unordered_set<const ggml_tensor *> seen(m.stores.begin(), m.stores.end());
+    std::vector<const ggml_tensor *> stack{last};
+    for (const ggml_tensor *st : m.stores) stack.push_back(st);
+    std::unordered_set<const ggml_tensor *> anc;
+    while (!stack.empty()) {
+        const ggml_tensor *t = stack.back();
+        stack.pop_back();
+        if (!t || !anc.insert(t).second) continue;
+        for (int k = 0; k < GGML_MAX_SRC; ++k) stack.push_back(t->src[k]);
+    }
+    for (int i = 0; i < g->n_nodes; ++i)
+        if (!anc.count(g->nodes[i])) return fail("extra node");
     return true;
 }
 
 struct fast_engine {
     gemma_engine *e = nullptr;
     const void *key_embd = nullptr, *key_q0 = nullptr;
+    uint64_t fp = 0;  // fingerprint of the first bytes of token_embd and layer 0's q
     int n_ctx = 0, n_layer = 0;
     std::vector<const void *> kv_keys;
+    std::vector<const void *> weights;  // every host weight the engine copied
 };
 fast_engine &fast() {
     static fast_engine f;
     return f;
+}
+uint64_t fingerprint(const void *a, const void *b) {
+    uint64_t h = 1469598103934665603ull;
+    for (const void *p : {a, b}) {
+        const unsigned char *c = (const unsigned char *)p;
+        for (int i = 0; i < 256; ++i) h = (h ^ c[i]) * 1099511628211ull;
+    }
+    return h;
+}
+void drop_fast() {
+    fast_engine &f = fast();
+    if (f.e) gemma_engine_free(f.e);
+    f = fast_engine{};
 }
 
 // 1 = ran on the engine, 0 = not the Gemma graph (run generically), -1 = error
@@ -642,24 +680,37 @@ int try_fast(ggml_cgraph *g) {
     }
     GHIP_CHECK(hipStreamSynchronize(ex_.stream));
     fast_engine &f = fast();
-    if (!f.e || f.key_embd != m.hw.embd || f.key_q0 != m.hw.layers[0].q || f.n_ctx != m.cfg.n_ctx ||
+    // the engine serves positions below n_ctx - 1 (its RoPE / history tables); the last slot runs
+    // node by node
+    if (m.T == 1 && m.pos0 + 1 >= m.cfg.n_ctx) return 0;
+    const uint64_t fp = fingerprint(m.hw.embd, m.hw.layers[0].q);
+    if (!f.e || f.key_embd != m.hw.embd || f.key_q0 != m.hw.layers[0].q || f.fp != fp || f.n_ctx != m.cfg.n_ctx ||
         f.n_layer != m.cfg.n_layer || f.kv_keys != kv_keys) {
-        if (f.e) gemma_engine_free(f.e);
+        drop_fast();
         int dev = 0;
         (void)hipGetDevice(&dev);
         f.e = gemma_engine_create_ext(&m.cfg, dev, m.hw, kc, vc);
         if (!f.e) return -1;
         f.key_embd = m.hw.embd;
         f.key_q0 = m.hw.layers[0].q;
+        f.fp = fp;
         f.n_ctx = m.cfg.n_ctx;
         f.n_layer = m.cfg.n_layer;
         f.kv_keys = kv_keys;
+        f.weights = {m.hw.embd, m.hw.out_norm};
+        for (const host_weights::layer &L : m.hw.layers)
+            for (const void *w : {L.q, L.k, L.v, L.o, L.gate, L.up, L.down, (const void *)L.attn_norm, (const void *)L.ffn_norm})
+                f.weights.push_back(w);
     }
     ggml_tensor *last = g->nodes[g->n_nodes - 1];
     const double t1 = prof ? now_us() : 0.0;
     const int rc = m.T == 1 ? gemma_engine_ext_decode(f.e, m.tokens[0], m.pos0, (float *)last->data)
                             : gemma_engine_ext_prefill(f.e, m.tokens.data(), m.T, (float *)last->data);
-    if (rc) return -1;
+    if (rc) {  // the engine could not serve this graph: node by node instead (same results)
+        if (getenv("GHIP_GGML_FAST_WHY")) fprintf(stderr, "[gemma_hip] ggml fast path failed: %s\n", last_error().c_str());
+        set_error("");
+        return 0;
+    }
     if (prof) fprintf(stderr, "[gemma_hip] fast path T=%d: match+sync %.1f us, engine %.1f us\n", m.T, t1 - t0, now_us() - t1);
     for (int il = 0; il < m.cfg.n_layer; ++il) {
         ex_.leaves[m.kc[il]->data].valid = true;
@@ -669,6 +720,16 @@ int try_fast(ggml_cgraph *g) {
 }
 
 }  // namespace
+
+// hpc_flush_weights / hpc_unregister_weight (capi.cpp): the fast path's engine holds device copies of
+// the graph's host weights; drop it when they go (host == nullptr: always)
+void ggml_fast_drop(const void *host) {
+    std::lock_guard<std::recursive_mutex> lk(ex().mu);
+    fast_engine &f = fast();
+    if (!f.e) return;
+    if (host && std::find(f.weights.begin(), f.weights.end(), host) == f.weights.end()) return;
+    drop_fast();
+}
 
 extern "C" {
 
@@ -691,6 +752,10 @@ char *arena_get(size_t bytes) {
     return (char *)aligned_alloc(64, bytes);
 }
 void arena_put(size_t bytes, char *p) {
+    if (bytes > ((size_t)256 << 20)) {  // weight contexts (the whole GGUF blob): give the memory back
+        free(p);
+        return;
+    }
     std::lock_guard<std::mutex> lk(arena_mu);
     if (arena_pool.size() >= 4) {
         free(arena_pool.front().second);
@@ -730,6 +795,17 @@ void ggml_free(struct ggml_context *ctx) {
                 free_tiled(tt->second);
                 ex().tiled.erase(tt);
             }
+        }
+    }
+    {  // a freed weight context takes the fast path's device copy of its weights with it
+        fast_engine &f = fast();
+        if (f.e) {
+            const std::unordered_set<const void *> ws(f.weights.begin(), f.weights.end());
+            for (ggml_tensor *t : ctx->tensors)
+                if (t->data && ws.count(t->data)) {
+                    drop_fast();
+                    break;
+                }
         }
     }
     for (ggml_tensor *t : ctx->tensors) delete t;

@@ -33,3 +33,6 @@ int64_t blck_size(int t);
 ggml_tensor *new_tensor_impl(ggml_context *ctx, ggml_type type, int n_dims, const int64_t *ne, ggml_tensor *view_src,
                              size_t view_offs);
 }  // namespace ggml_impl
+
+// drops the ggml executor's fast-path engine when it holds a copy of `host` (nullptr: always)
+void ggml_fast_drop(const void *host);

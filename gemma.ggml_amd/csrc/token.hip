@@ -56,6 +56,9 @@ constexpr int TK_TABB = (int)sizeof(tok_layer);  // bytes per layer in that tabl
 // scalar loads (lgkmcnt), never a vector load that a term wave's counted wait would also drain
 typedef const __attribute__((address_space(4))) tok_args ctok;
 constexpr int TK_MAXCTX = 1024;              // the attention scratch overlays the down image
+#ifndef TK_DEFER
+#define TK_DEFER 0
+#endif
 
 enum { EDGE_X = 0, EDGE_QKV = 1, EDGE_ATT = 2, EDGE_SA = 3, EDGE_H = 4 };
 
@@ -360,14 +363,17 @@ __global__ void __launch_bounds__(TK_NTH) k_token(const tok_args *ap) {
 
     const int nq = c + G < fresh(ap)->qkv_rows / 8 ? 2 : 1;  // qkv row tiles of this workgroup
     const int per_layer = nq * NRQ + NRQ + 2 * NBE + NRD;      // ring tiles per term wave per layer
-#define TK_STAMP(L, i)                                                                              \
-    if (GHIP_STAMPS && tid == 0 && fresh(ap)->dbg_t)                                                \
-    fresh(ap)->dbg_t[((int64_t)c * n_layer + (L)) * 16 + (i)] = __builtin_amdgcn_s_memrealtime()
+    unsigned long long *const dbg = GHIP_STAMPS ? fresh(ap)->dbg_t : nullptr;  // stamps build only
+#define TK_STAMP(L, i) \
+    if (GHIP_STAMPS && tid == 0 && dbg) dbg[((int64_t)c * n_layer + (L)) * 16 + (i)] = __builtin_amdgcn_s_memrealtime()
 
     // ---- the term wave's weight ring ------------------------------------------------------------
     const uint32_t ring0 = lds_u32(smem + LY::RING) + (uint32_t)(term ? wave : 0) * NR * TK_SLOT;
     int i_layer = 0, i_k = 0;  // issue cursor (wave-uniform)
-    auto issue = [&](int slot) {
+    // the next tile's source addresses, prepared one refill ahead: the pointer-table read and the
+    // address arithmetic overlap the tile compute instead of stalling the refill (~0.25 us each)
+    const uint8_t *nx_q = nullptr, *nx_s = nullptr;
+    auto prep = [&]() {
         const bool past = i_layer >= n_layer;
         const int layer = past ? n_layer - 1 : i_layer;
         int k = past ? per_layer - 1 : i_k;  // past the end: re-read the last tile
@@ -388,19 +394,57 @@ __global__ void __launch_bounds__(TK_NTH) k_token(const tok_args *ap) {
             mat = 4;
         }
         const uint64_t *tp = (const uint64_t *)(small + SM_TAB + layer * TK_TABB) + 2 * mat;
-        const uint8_t *qs = (const uint8_t *)tp[0], *sc = (const uint8_t *)tp[1];
-        const uint32_t dst = ring0 + (uint32_t)slot * TK_SLOT;
-        dma16(qs + (size_t)tile * 1024 + lane * 16, dst);
-        if (lane < SB / 2) dma16(sc + (size_t)tile * 8 * SB + lane * 16, dst + 1024);  // 8 rows x SB bytes
+        nx_q = (const uint8_t *)tp[0] + (size_t)tile * 1024 + lane * 16;
+        nx_s = (const uint8_t *)tp[1] + (size_t)tile * 8 * SB + lane * 16;
         if (++i_k == per_layer) {
             i_k = 0;
             ++i_layer;
         }
     };
-    int slot = 0;
-    // pop the oldest tile: its 16 B of quants and its row's scales for this lane, then refill
+    // ring state (wave-uniform): tiles issued / popped so far; tile t lives in slot t % NR.  A slot
+    // is refilled (tile t + NR) only after tile t was popped.  Refills of tiles the current phase
+    // still needs go out at once; the others wait for the phase's end (flush), where the term wave
+    // idles at an edge anyway: a DMA issue costs a computing wave ~0.2 us.
+    int issued = 0, popped = 0, islot = 0, slot = 0, phase_end = 1 << 30;
+    auto issue_next = [&]() {  // the prepared tile into its slot, then prepare the next
+        const uint32_t dst = ring0 + (uint32_t)islot * TK_SLOT;
+        dma16(nx_q, dst);
+        if (lane < SB / 2) dma16(nx_s, dst + 1024);  // 8 rows x SB bytes
+        prep();
+        ++issued;
+        islot = islot + 1 == NR ? 0 : islot + 1;
+    };
+    auto flush = [&]() {  // every free slot refilled (after the reads of the popped tiles)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        while (issued < popped + NR) issue_next();
+    };
+    // TK_DEFER 0: every pop refills at once (measured faster: the flushes at the edges slowed the
+    // gathers that share the CU's memory pipe)
+    auto begin_phase = [&](int pops) { phase_end = TK_DEFER ? popped + pops : 1 << 30; };
+    int stamp_layer = 0;
+    int pop_i = 0;  // stamps build: per-pop timing of workgroup 0's wave 0 (layer 1)
+    auto pstamp = [&](int k) {
+        if (GHIP_STAMPS && c == 0 && wave == 0 && lane == 0 && stamp_layer == 1 && pop_i < 64 && dbg)
+            dbg[(int64_t)G * n_layer * 16 + pop_i * 4 + k] = __builtin_amdgcn_s_memrealtime();
+    };
+    // pop the next tile: its 16 B of quants and its row's scales for this lane
     auto pop = [&](uint4 &q, uint4 &s) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (NR - 1)) : "memory");
+        pstamp(0);
+        if (issued < phase_end && issued < popped + NR) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous pop's reads done
+            do issue_next();
+            while (issued < phase_end && issued < popped + NR);
+        }
+        pstamp(1);
+        // tiles popped+1 .. issued-1 may stay in flight: 2 DMA instructions each
+        switch (issued - popped - 1) {
+#define TK_VM(n) case n: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * n) : "memory"); break;
+            TK_VM(0) TK_VM(1) TK_VM(2) TK_VM(3) TK_VM(4) TK_VM(5) TK_VM(6) TK_VM(7) TK_VM(8) TK_VM(9) TK_VM(10)
+            TK_VM(11) TK_VM(12) TK_VM(13) TK_VM(14) TK_VM(15)
+#undef TK_VM
+            default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        pstamp(2);
         const uint8_t *p = smem + LY::RING + (wave * NR + slot) * TK_SLOT;
         q = *(const uint4 *)(p + lane * 16);
         if (WT == T_Q4_0) {
@@ -409,8 +453,8 @@ __global__ void __launch_bounds__(TK_NTH) k_token(const tok_args *ap) {
             const uint2 v = *(const uint2 *)(p + 1024 + rr * 8);
             s = make_uint4(v.x, v.y, 0, 0);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads done before its refill
-        issue(slot);
+        ++pop_i;
+        ++popped;
         slot = slot + 1 == NR ? 0 : slot + 1;
     };
     // the ring's address table into LDS, and layer 0's x = the embedding row (every workgroup: the
@@ -429,17 +473,17 @@ __global__ void __launch_bounds__(TK_NTH) k_token(const tok_args *ap) {
     }
     lds_barrier();
     if (term) {
-#pragma unroll
-        for (int k = 0; k < NR; ++k) issue(k);
+        prep();
+        for (int k = 0; k < NR; ++k) issue_next();
     }
 
     // ---- round-pipelined matvec phase (k_matvec_rr's arithmetic): nround rounds of 8 tiles, a row
     // tile every per_rt rounds; the carrier chains round r-1 while the term waves stash round r
     auto slot_base = [&](int r) { return smem + LY::STASH + (r & 1) * ST::SLOT; };
-    int stamp_layer = 0;
     auto rr_phase = [&](int nround, int per_rt, const lds_map &m, auto nsa, auto epi) {
         constexpr bool NSA = decltype(nsa)::value;
         if (term) {
+            begin_phase(nround);
             for (int r = 0; r < nround; ++r) {
                 uint4 q, s;
                 pop(q, s);
@@ -455,6 +499,7 @@ __global__ void __launch_bounds__(TK_NTH) k_token(const tok_args *ap) {
                 if (nround > 4 && r == nround - 1) TK_STAMP(stamp_layer, 15);
                 lds_barrier();
             }
+            flush();  // the phase's deferred refills: the term waves idle at the next edge
         } else {
             if (carrier) __builtin_amdgcn_s_setprio(3);
             float acc = 0.0f;
@@ -594,6 +639,7 @@ __global__ void __launch_bounds__(TK_NTH) k_token(const tok_args *ap) {
         fresh_lane();
         if (term) {
             float accg = 0.0f, accu = 0.0f;
+            begin_phase(2 * NBE);
             for (int bt = 0; bt < NBE; ++bt) {
                 uint4 qg, sg, qu, su;
                 if (bt == NBE - 3) TK_STAMP(il, 13);
@@ -614,6 +660,7 @@ __global__ void __launch_bounds__(TK_NTH) k_token(const tok_args *ap) {
         lds_barrier();
         TK_STAMP(il, 10);
         fresh_lane();
+        if (term) flush();  // gate/up's deferred refills (down tiles first) while the aux waves hand h on
         // this workgroup's 64 rows of h = Q8_0 blocks 2c, 2c+1 -> granules; the h image -> LDS
         if (aux) {
             ctok &a = *fresh(ap);

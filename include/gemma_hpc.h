@@ -126,7 +126,7 @@ int gemma_engine_prefill_taps(gemma_engine *e, float *host_taps, int exact);
  * out = 6 * 4096 * 16 u64, slot [region][workgroup][phase], unused slots 0 */
 int gemma_engine_stamp_step(gemma_engine *e, int layer, unsigned long long *out);
 /* diagnostics: one eager step through the persistent launch with its phase stamps
- * -> out [n_embd / 8][n_layer][16] u64 (GHIP_STAMPS build) */
+ * -> out [n_embd / 8][n_layer][16] u64 + 256 per-pop probes (GHIP_STAMPS build) */
 int gemma_engine_token_stamps(gemma_engine *e, unsigned long long *out);
 /* per-op test entry: one decode-attention block on host buffers (caches updated in place);
  * mode 0 = one workgroup per head, 1 = position-split form with the in-kernel hand-off */

@@ -36,11 +36,12 @@ def main():
     e.step(len(prompt) + 4, use_graph=True)
     nl = GEMMA_2B["n_layer"]
     grid = GEMMA_2B["n_embd"] // 8
-    out = np.zeros((grid, nl, 16), dtype=np.uint64)
+    out = np.zeros(grid * nl * 16 + 256, dtype=np.uint64)
     for rep in range(2):
         r = L.gemma_engine_token_stamps(e.h, out.ctypes.data_as(C.c_void_p))
         assert r == 0, G.last_error()
-    t = out.astype(np.int64)
+    probes = out[grid * nl * 16:].astype(np.int64).reshape(64, 4)
+    t = out[: grid * nl * 16].reshape(grid, nl, 16).astype(np.int64)
     t0 = t[:, 0, 0].min()
     att = np.array([(c & 7) == 0 and (c >> 3) < 32 for c in range(grid)])
     print("per layer: phase -> max over workgroups (us from the layer's earliest start); attention rows: the 32 attention WGs")
@@ -65,15 +66,20 @@ def main():
     for l in range(1, nl - 1):
         base = starts[l]
         prev = 0.0
-        for i, nm in zip(ORDER, NAMES):
+        for jj, (i, nm) in enumerate(zip(ORDER, NAMES)):
             v = t[:, l, i]
             sel = v[att] if nm in ("att_in", "att") else v
             sel = sel[sel > 0]
             m = (sel.max() - base) / 100 if sel.size else prev
-            acc[j] += m - prev
+            acc[jj] += m - prev
             prev = m
     acc /= max(nl - 2, 1)
     print("mean critical-path increments (us): " + "  ".join(f"{nm} {x:.2f}" for nm, x in zip(NAMES, acc)))
+    nz = [i for i in range(64) if probes[i, 0] != 0]
+    p0 = probes[nz[0], 0] if nz else 0
+    print("workgroup 0 wave 0 layer 1 pops (us from its first pop): start / after refill issue / after vmcnt wait")
+    for i in nz:
+        print(f"  pop {i:2d}: {(probes[i, 0] - p0) / 100:7.2f} {(probes[i, 1] - p0) / 100:7.2f} {(probes[i, 2] - p0) / 100:7.2f}")
     e.close()
 
 

@@ -308,19 +308,15 @@ int32_t greedy_sample(const ggml_tensor *out) {  // :532-546
 
 }  // namespace
 
-int main(int argc, char **argv) {
-    const size_t alen = argc > 1 ? strlen(argv[1]) : 0;
-    const bool gguf = alen > 5 && strcmp(argv[1] + alen - 5, ".gguf") == 0;
-    if ((gguf && argc < 6) || (!gguf && argc < 14)) {
-        fprintf(stderr, "usage: %s model.gguf prompt out ctx n_decode\n"
-                        "       %s weights prompt out n_layer n_embd n_head n_head_kv head_dim n_ff n_vocab ctx wtype n_decode\n",
-                argv[0], argv[0]);
-        return 2;
-    }
+// one model's whole run (load, generate, free every context); wpath / opath stand in for argv[1] /
+// argv[3], the other arguments as in main
+int run_one(int argc, char **argv, const char *wpath, const char *opath) {
+    const size_t alen = strlen(wpath);
+    const bool gguf = alen > 5 && strcmp(wpath + alen - 5, ".gguf") == 0;
     model m;
     int n_decode;
     if (gguf) {
-        if (!load_model_from_file(m, argv[1])) {
+        if (!load_model_from_file(m, wpath)) {
             fprintf(stderr, "gguf: load failed\n");
             return 1;
         }
@@ -330,7 +326,7 @@ int main(int argc, char **argv) {
         m.hp = {atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8]), atoi(argv[9]), atoi(argv[10]),
                 atoi(argv[11]), atoi(argv[12])};
         n_decode = atoi(argv[13]);
-        if (!load_weights(m, argv[1])) {
+        if (!load_weights(m, wpath)) {
             fprintf(stderr, "weights: read failed\n");
             return 1;
         }
@@ -350,7 +346,7 @@ int main(int argc, char **argv) {
     const size_t per_tok = m.hp.n_vocab + 2 * E + L * (6 * F + 16 * E + 8 * qw + 6 * kvw);
     const size_t mid = (T * per_tok + L * T * (size_t)m.hp.ctx * m.hp.n_head * 4) * 4 + (64u << 20);
     m.compute_mem.resize(ggml_tensor_overhead() * 4096 + ggml_graph_overhead() + mid);
-    FILE *out = fopen(argv[3], "wb");
+    FILE *out = fopen(opath, "wb");
     std::vector<int32_t> toks;
     // timing as begin_one_round_inference reports it (src/gemma_model.cpp:552-572): prefill, then decode
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -392,7 +388,7 @@ int main(int argc, char **argv) {
     fclose(out);
     if (gguf) {  // the sequence as text, through the GGUF tokenizer table
         const std::string txt = detokenize(m, input);
-        FILE *tf = fopen((std::string(argv[3]) + ".txt").c_str(), "wb");
+        FILE *tf = fopen((std::string(opath) + ".txt").c_str(), "wb");
         if (tf) {
             fwrite(txt.data(), 1, txt.size(), tf);
             fclose(tf);
@@ -405,4 +401,19 @@ int main(int argc, char **argv) {
     ggml_free(m.kv_ctx);
     ggml_free(m.weight_ctx);
     return 0;
+}
+
+int main(int argc, char **argv) {
+    const size_t alen = argc > 1 ? strlen(argv[1]) : 0;
+    const bool gguf = alen > 5 && strcmp(argv[1] + alen - 5, ".gguf") == 0;
+    if ((gguf && argc < 6) || (!gguf && argc < 14)) {
+        fprintf(stderr, "usage: %s model.gguf prompt out ctx n_decode\n"
+                        "       %s weights prompt out n_layer n_embd n_head n_head_kv head_dim n_ff n_vocab ctx wtype n_decode\n"
+                        "  DRIVER_SECOND=<weights2>: then a second model of the same shapes in the same process (out.2)\n",
+                argv[0], argv[0]);
+        return 2;
+    }
+    int r = run_one(argc, argv, argv[1], argv[3]);
+    if (r == 0 && getenv("DRIVER_SECOND")) r = run_one(argc, argv, getenv("DRIVER_SECOND"), (std::string(argv[3]) + ".2").c_str());
+    return r;
 }

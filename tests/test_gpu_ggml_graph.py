@@ -69,38 +69,20 @@ def write_gguf(m, shape, path, kmix):
     w.write(str(path))
 
 
-def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fast=1):
-    """fast=1: the executor recognises the Gemma graph and runs the device-resident engine over the
-    graph's weights and KV-cache mirrors (ggml_api.cpp try_fast); fast=0: node by node."""
-    m = O.Model(O.make_config(shape, n_ctx=ctx, wtype=wtype, kmix=kmix))
-    wpath, ppath, opath = tmp_path / ("m.gguf" if gguf else "w.bin"), tmp_path / "p.bin", tmp_path / "o.bin"
-    if gguf:
-        write_gguf(m, shape, wpath, kmix)
-    else:
-        with open(wpath, "wb") as f:
-            f.write(m.tensor(0).tobytes())  # token_embd (also the tied output)
-            f.write(m.tensor(1).tobytes())  # output_norm
-            for il in range(shape["n_layer"]):
-                for k in range(9):  # attn_norm q k v o ffn_norm gate up down
-                    f.write(m.tensor(16 + il * 16 + k).tobytes())
-    prompt = np.array(O.make_prompt(n_prompt, shape["n_vocab"]), dtype=np.int32)
-    prompt.tofile(ppath)
-    if gguf:
-        args = [DRIVER, str(wpath), str(ppath), str(opath), str(ctx), str(n_decode)]
-    else:
-        args = [DRIVER, str(wpath), str(ppath), str(opath)] + [str(shape[k]) for k in
-                ("n_layer", "n_embd", "n_head", "n_head_kv", "head_dim", "n_ff", "n_vocab")] + [str(ctx), str(wtype),
-                                                                                              str(n_decode)]
-    env = dict(os.environ, GHIP_GGML_FAST=str(fast), GHIP_GGML_FAST_WHY="1")
-    r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
-    if fast and not kmix:  # the Gemma graph must take the engine path (K-quant layers: node by node)
-        assert "fast path not taken" not in r.stderr, r.stderr[-500:]
+def _write_weights(m, shape, path):
+    with open(path, "wb") as f:
+        f.write(m.tensor(0).tobytes())  # token_embd (also the tied output)
+        f.write(m.tensor(1).tobytes())  # output_norm
+        for il in range(shape["n_layer"]):
+            for k in range(9):  # attn_norm q k v o ffn_norm gate up down
+                f.write(m.tensor(16 + il * 16 + k).tobytes())
+
+
+def _check_out(m, prompt, n_decode, V, opath):
+    """the driver's logits rows and tokens against the oracle's inference() sequence"""
     raw = np.fromfile(opath, dtype=np.float32)
-    V = shape["n_vocab"]
     logits = raw[: (n_decode + 1) * V].reshape(n_decode + 1, V)
     toks = raw[(n_decode + 1) * V:].view(np.int32)
-    # oracle: the reference's inference() sequence (PREFILL, then DECODE per token)
     seq = list(prompt)
     t0, l0, _ = m.inference(seq, 0)
     refs, rtoks = [l0], [t0]
@@ -110,10 +92,49 @@ def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fa
         refs.append(lg)
         rtoks.append(t)
         seq.append(t)
-    m.close()
     for i, ref in enumerate(refs):
         assert np.array_equal(logits[i].view(np.uint32), ref.view(np.uint32)), (i, np.abs(logits[i] - ref).max())
     assert list(toks) == rtoks
+    return seq
+
+
+def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fast=1, second_seed=None):
+    """fast=1: the executor recognises the Gemma graph and runs the device-resident engine over the
+    graph's weights and KV-cache mirrors (ggml_api.cpp try_fast); fast=0: node by node.
+    second_seed: a second model of the same shapes (other weights) run after the first in the same
+    driver process, whose pooled host arenas likely land at the first model's addresses."""
+    m = O.Model(O.make_config(shape, n_ctx=ctx, wtype=wtype, kmix=kmix))
+    wpath, ppath, opath = tmp_path / ("m.gguf" if gguf else "w.bin"), tmp_path / "p.bin", tmp_path / "o.bin"
+    if gguf:
+        write_gguf(m, shape, wpath, kmix)
+    else:
+        _write_weights(m, shape, wpath)
+    m2 = None
+    if second_seed is not None:
+        m2 = O.Model(O.make_config(shape, n_ctx=ctx, wtype=wtype, kmix=kmix, seed=second_seed))
+        _write_weights(m2, shape, tmp_path / "w2.bin")
+    prompt = np.array(O.make_prompt(n_prompt, shape["n_vocab"]), dtype=np.int32)
+    prompt.tofile(ppath)
+    if gguf:
+        args = [DRIVER, str(wpath), str(ppath), str(opath), str(ctx), str(n_decode)]
+    else:
+        args = [DRIVER, str(wpath), str(ppath), str(opath)] + [str(shape[k]) for k in
+                ("n_layer", "n_embd", "n_head", "n_head_kv", "head_dim", "n_ff", "n_vocab")] + [str(ctx), str(wtype),
+                                                                                              str(n_decode)]
+    env = dict(os.environ, GHIP_GGML_FAST=str(fast), GHIP_GGML_FAST_WHY="1")
+    if m2 is not None:
+        env["DRIVER_SECOND"] = str(tmp_path / "w2.bin")
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    if fast and not kmix:  # the Gemma graph must take the engine path (K-quant layers: node by node)
+        assert "fast path not taken" not in r.stderr, r.stderr[-500:]
+    # oracle: the reference's inference() sequence (PREFILL, then DECODE per token)
+    V = shape["n_vocab"]
+    seq = _check_out(m, prompt, n_decode, V, opath)
+    m.close()
+    if m2 is not None:
+        _check_out(m2, prompt, n_decode, V, str(opath) + ".2")
+        m2.close()
     if gguf:  # print_tokens through the GGUF tokenizer table
         want = "".join(_token_text(int(i)) for i in seq).replace("<bos>", "", 1).replace("\u2581", " ")
         assert open(str(opath) + ".txt", encoding="utf-8").read() == want
@@ -156,3 +177,10 @@ def test_ggml_graph_gguf_kquant_mix_tiny(tmp_path, fast):
 def test_ggml_graph_gguf_kquant_mix_gemma2b_layers(tmp_path, fast):
     shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
     _run(tmp_path, shape, O.Q4_0, 33, 2, 128, gguf=True, kmix=1, fast=fast)
+
+
+@gpu
+def test_ggml_graph_two_models_one_process(tmp_path):
+    """a second model of the same size in the same process: the fast path's engine (keyed by the
+    graph's host weight addresses) must not serve the first model's device copy"""
+    _run(tmp_path, dict(O.TINY), O.Q4_0, 12, 3, 128, fast=1, second_seed=0x1234567)

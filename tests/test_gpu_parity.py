@@ -87,6 +87,15 @@ def test_decode_gemma2b_bitexact():
     _check_decode(O.GEMMA_2B, n_prompt=6, n_decode=4, n_ctx=256)
 
 
+@gpu
+@pytest.mark.parametrize("head_dim", [64, 96, 160])
+def test_decode_head_dims_bitexact(head_dim):
+    """head_dim not a multiple of 128: the per-head attention takes fewer workgroups per head
+    (att_dsplit 2 or 1) instead of failing every step"""
+    shape = dict(O.TINY, n_head=4, n_head_kv=2, head_dim=head_dim, n_embd=512)
+    _check_decode(shape, n_prompt=5, n_decode=10, n_ctx=64)
+
+
 GEMMA_7B_LAYERS = dict(n_layer=3, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, n_ff=24576, n_vocab=8192)
 
 
