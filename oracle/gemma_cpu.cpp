@@ -365,18 +365,21 @@ extern "C" int orc_model_hidden(orc_model *m, int il, float *out, int64_t max_fl
 // bounded sample: PREFILL of `prompt_len` tokens (logits for every row, as the reference's graph
 // computes them at :740), then n_decode greedy DECODE steps, std::chrono timed.  tokens_out gets
 // prompt_len + 1 + n_decode ids.  Returns decode seconds; *prefill_s gets prefill seconds.
+// prof6 (nullable) gets the decode steps' mul_mat profile (orc_prof layout, hpc_cpu.cpp).
 extern "C" double orc_bench_run(orc_model *m, const int32_t *prompt, int prompt_len, int n_decode, int n_threads,
-                                int32_t *tokens_out, double *prefill_s) {
+                                int32_t *tokens_out, double *prefill_s, double *prof6) {
     orc_set_threads(n_threads);
     orc_model_reset_kv(m);
     std::vector<int32_t> seq(prompt, prompt + prompt_len);
     std::vector<float> all((size_t)prompt_len * m->cfg.n_vocab);
     auto t0 = std::chrono::steady_clock::now();
     seq.push_back(orc_model_inference(m, seq.data(), (int)seq.size(), 0, nullptr, all.data(), 1));
+    if (prof6) orc_prof(1, nullptr);
     auto t1 = std::chrono::steady_clock::now();
     for (int s = 0; s < n_decode; ++s)
         seq.push_back(orc_model_inference(m, seq.data(), (int)seq.size(), 1, nullptr, nullptr, 1));
     auto t2 = std::chrono::steady_clock::now();
+    if (prof6) orc_prof(0, prof6);
     for (size_t i = 0; i < seq.size(); ++i) tokens_out[i] = seq[i];
     if (prefill_s) *prefill_s = std::chrono::duration<double>(t1 - t0).count();
     return std::chrono::duration<double>(t2 - t1).count();

@@ -34,7 +34,9 @@ inline float bitsf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 }  // namespace
 
 // ---------------------------------------------------------------- fp16 (RNE)
-extern "C" float orc_fp16_to_fp32(uint16_t h) {
+// Portable restatements (_sw) and the F16C forms ggml's x86 build uses (GGML_FP16_TO_FP32 /
+// GGML_FP32_TO_FP16 = _cvtsh_ss / _cvtss_sh); test_oracle_kat checks they agree bitwise.
+extern "C" float orc_fp16_to_fp32_sw(uint16_t h) {
     const uint32_t sign = (uint32_t)(h & 0x8000) << 16;
     uint32_t exp = (h >> 10) & 0x1f, mant = h & 0x3ff;
     if (exp == 0) {
@@ -47,7 +49,7 @@ extern "C" float orc_fp16_to_fp32(uint16_t h) {
     return bitsf(sign | ((exp + 112) << 23) | (mant << 13));
 }
 
-extern "C" uint16_t orc_fp32_to_fp16(float f) {
+extern "C" uint16_t orc_fp32_to_fp16_sw(float f) {
     const uint32_t x = fbits(f);
     const uint16_t sign = (uint16_t)((x >> 16) & 0x8000);
     const uint32_t ax = x & 0x7fffffffu;
@@ -70,6 +72,29 @@ extern "C" uint16_t orc_fp32_to_fp16(float f) {
     const uint32_t rem = ax & 0x1fff;
     if (rem > 0x1000 || (rem == 0x1000 && (r & 1))) r++;
     return (uint16_t)(sign | r);
+}
+
+extern "C" float orc_fp16_to_fp32(uint16_t h) { return _cvtsh_ss(h); }
+extern "C" uint16_t orc_fp32_to_fp16(float f) { return (uint16_t)_cvtss_sh(f, _MM_FROUND_TO_NEAREST_INT); }
+
+// mismatches between the F16C and portable forms: every fp16 pattern, and every `stride`-th fp32
+// bit pattern plus each exponent's rounding boundaries (ties, +-1 ulp around them)
+extern "C" int64_t orc_fp16_selfcheck(uint32_t stride) {
+    int64_t bad = 0;
+    for (uint32_t h = 0; h < 65536; ++h) {  // F16C quiets signalling NaNs; NaN-ness must match
+        const float a = orc_fp16_to_fp32((uint16_t)h), b = orc_fp16_to_fp32_sw((uint16_t)h);
+        bad += (a != a && b != b) ? 0 : fbits(a) != fbits(b);
+    }
+    auto one = [&](uint32_t u) { bad += orc_fp32_to_fp16(bitsf(u)) != orc_fp32_to_fp16_sw(bitsf(u)); };
+    for (uint64_t u = 0; u <= 0xffffffffull; u += stride ? stride : 1) one((uint32_t)u);
+    for (uint32_t sgn = 0; sgn < 2; ++sgn)
+        for (uint32_t e = 0; e < 256; ++e)
+            for (uint32_t m = 0; m < (1u << 13); m += 0x1000 / 8) {
+                const uint32_t base = (sgn << 31) | (e << 23);
+                for (uint32_t hi = 0; hi < 1024; hi += 37)
+                    for (int d = -1; d <= 1; ++d) one(base | ((((hi << 13) | m) + d) & 0x7fffff));
+            }
+    return bad;
 }
 
 // ---------------------------------------------------------------- fp16 lookup tables

@@ -9,6 +9,8 @@
 //     dst address (c % ne1)*nb1 + (c / ne1)*nb2 + r*4.
 // ratio is fixed at 1.0 (every row on the CPU): the shipped 0.9 split leaves GPU rows unwritten
 // because the OpenCL kernels only verify, so 1.0 is the only valid reference path.
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <future>
@@ -71,7 +73,80 @@ class task_pool {
     bool stop_ = false;
 };
 
+// Fork-join pool for the bench's "fixed" leg (NOT the reference's design): workers spin on a
+// generation counter (then yield), the caller runs share 0 itself, completion is one atomic count.
+// No allocation, lock or futex per mul_mat; the reference pool above pays a packaged_task, a
+// mutex round trip and a condvar wake per task, N tasks per call, ~415 calls per decode token.
+std::mutex &g_pool_mu_spin() {
+    static std::mutex m;
+    return m;
+}
+
+class spin_pool {
+  public:
+    explicit spin_pool(int n) : n_(n) {
+        for (int i = 1; i < n; ++i)
+            workers_.emplace_back([this, i] {
+                unsigned seen = 0;
+                for (;;) {
+                    unsigned g;
+                    int spins = 0;
+                    while ((g = gen_.load(std::memory_order_acquire)) == seen) {
+                        if (++spins > 20000) std::this_thread::yield();
+                    }
+                    seen = g;
+                    if (stop_.load(std::memory_order_relaxed)) return;
+                    (*fn_)(i);
+                    done_.fetch_add(1, std::memory_order_acq_rel);
+                }
+            });
+    }
+    ~spin_pool() {
+        stop_.store(true);
+        gen_.fetch_add(1, std::memory_order_release);
+        for (auto &w : workers_) w.join();
+    }
+    void run(const std::function<void(int)> &fn) {
+        fn_ = &fn;
+        done_.store(0, std::memory_order_relaxed);
+        gen_.fetch_add(1, std::memory_order_release);
+        fn(0);
+        while (done_.load(std::memory_order_acquire) != n_ - 1) {
+        }
+    }
+    int size() const { return n_; }
+
+  private:
+    int n_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int)> *fn_ = nullptr;
+    std::atomic<unsigned> gen_{0};
+    std::atomic<int> done_{0};
+    std::atomic<bool> stop_{false};
+};
+
 int g_threads = 4;  // src/macro.h:21 N_THREADS_MUL_MAT_CPU
+int g_pool_kind = 0;  // 0 = reference task pool, 1 = spin fork-join pool (bench "fixed" leg)
+std::unique_ptr<spin_pool> g_spin;
+
+spin_pool &spool() {
+    std::lock_guard<std::mutex> lk(g_pool_mu_spin());
+    if (!g_spin || g_spin->size() != g_threads) {
+        g_spin.reset();
+        g_spin = std::make_unique<spin_pool>(g_threads);
+    }
+    return *g_spin;
+}
+
+// mul_mat profile (orc_prof): [0] calls, [1] wall ns, [2] sum over calls of the slowest share's
+// compute ns, [3]-[5] the same three for the F16 (attention) calls alone.
+std::atomic<int64_t> g_prof[6];
+bool g_prof_on = false;
+
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 std::unique_ptr<task_pool> g_pool;
 std::mutex g_pool_mu;
 
@@ -130,21 +205,48 @@ extern "C" void orc_mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb
     const int N = g_threads;
     const int64_t cpu_row_num = (int64_t)ceil(((double)ne01 * 1.0) / (double)N) * N;
     const int64_t row_per_core = cpu_row_num / N;
-    if (N == 1) {
-        mul_mat_sub(0, ne01, shared_edge, col_num, ne01, ne1, nb01, nb1, nb2, (int64_t)row_size,
-                    (const char *)src0, wdata, (char *)dst, vd);
-        return;
-    }
-    task_pool &p = pool();
-    std::vector<std::future<void>> futs;
-    for (int t = 0; t < N; ++t) {
+    const int64_t t0 = g_prof_on ? now_ns() : 0;
+    std::atomic<int64_t> slowest{0};
+    auto share = [&, row_per_core](int t) {
+        const int64_t a = g_prof_on ? now_ns() : 0;
         const int64_t s = t * row_per_core, e = (t + 1) * row_per_core;
-        futs.push_back(p.submit([=] {
-            mul_mat_sub(s, e, shared_edge, col_num, ne01, ne1, nb01, nb1, nb2, (int64_t)row_size,
-                        (const char *)src0, wdata, (char *)dst, vd);
-        }));
+        mul_mat_sub(s, e, shared_edge, col_num, ne01, ne1, nb01, nb1, nb2, (int64_t)row_size,
+                    (const char *)src0, wdata, (char *)dst, vd);
+        if (g_prof_on) {
+            const int64_t d = now_ns() - a;
+            int64_t cur = slowest.load();
+            while (d > cur && !slowest.compare_exchange_weak(cur, d)) {
+            }
+        }
+    };
+    if (N == 1) {
+        share(0);
+    } else if (g_pool_kind == 1) {
+        spool().run(share);
+    } else {
+        task_pool &p = pool();
+        std::vector<std::future<void>> futs;
+        for (int t = 0; t < N; ++t) futs.push_back(p.submit([&share, t] { share(t); }));
+        for (auto &f : futs) f.get();
     }
-    for (auto &f : futs) f.get();
+    if (g_prof_on) {
+        const int64_t w = now_ns() - t0, k = src0_type == ORC_F16 ? 3 : 0;
+        g_prof[k] += 1;
+        g_prof[k + 1] += w;
+        g_prof[k + 2] += slowest.load();
+    }
+}
+
+// bench.py cpu_baseline diagnostics: pool kind (0 reference task pool, 1 spin fork-join) and the
+// mul_mat profile (see g_prof); out[6] = {calls, wall_s, slowest-share_s, f16 calls, f16 wall_s,
+// f16 slowest-share_s}.
+extern "C" void orc_set_pool(int kind) { g_pool_kind = kind == 1 ? 1 : 0; }
+extern "C" void orc_prof(int enable, double *out) {
+    if (out) {
+        for (int i = 0; i < 6; ++i) out[i] = (i % 3 == 0) ? (double)g_prof[i].load() : g_prof[i].load() * 1e-9;
+    }
+    for (auto &c : g_prof) c = 0;
+    g_prof_on = enable != 0;
 }
 
 // ggml MUL_MAT INIT [ext]: every src1 row (ne10 f32) -> vec_dot_type row.

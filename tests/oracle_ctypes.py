@@ -43,6 +43,8 @@ def lib():
     L.orc_fp32_to_fp16.argtypes = [C.c_float]
     L.orc_fp16_to_fp32.restype = C.c_float
     L.orc_fp16_to_fp32.argtypes = [C.c_uint16]
+    L.orc_fp16_selfcheck.restype = C.c_int64
+    L.orc_fp16_selfcheck.argtypes = [C.c_uint32]
     L.orc_init_tables.argtypes = [C.c_int]
     L.orc_table_exp_f16.restype = vp
     L.orc_table_gelu_f16.restype = vp
@@ -81,7 +83,9 @@ def lib():
     L.orc_model_hidden.restype = C.c_int
     L.orc_model_hidden.argtypes = [vp, C.c_int, vp, i64]
     L.orc_bench_run.restype = C.c_double
-    L.orc_bench_run.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.POINTER(C.c_double)]
+    L.orc_bench_run.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.POINTER(C.c_double), vp]
+    L.orc_set_pool.argtypes = [C.c_int]
+    L.orc_prof.argtypes = [C.c_int, vp]
     L.orc_make_prompt.argtypes = [C.c_uint64, C.c_int, C.c_int, vp]
     L.orc_synth_value.restype = C.c_float
     L.orc_synth_value.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_double]

@@ -22,6 +22,12 @@ def test_fp16_conversion_matches_numpy():
     assert same.all()
 
 
+def test_fp16_f16c_matches_portable_restatement():
+    """the F16C conversions (ggml's x86 GGML_FP32_TO_FP16 / GGML_FP16_TO_FP32) and the portable RNE
+    restatement agree on every fp16 pattern and a strided sweep of fp32 patterns + rounding edges"""
+    assert O.lib().orc_fp16_selfcheck(4099) == 0
+
+
 def test_q4_0_constant_block_known_answer():
     # all-constant weights w: max = w, d = -w/8 -> every code = min(15, (int)(-8 + 8.5)) = 0 -> value -8*d = w
     x = np.full((1, 64), 0.75, dtype=np.float32)
@@ -133,16 +139,19 @@ def test_gelu_table():
 
 
 def test_mul_mat_thread_split_invariant():
-    """src/hpc.cpp:245-273 row split: results independent of the worker count."""
+    """src/hpc.cpp:245-273 row split: results independent of the worker count and pool kind."""
     rng = np.random.default_rng(3)
     rows, k, ncols = 37, 256, 3
     W = O.quantize((rng.standard_normal((rows, k)) * 0.05).astype(np.float32), "q4_0_ref")
     X = rng.standard_normal((ncols, k)).astype(np.float32)
     wdata, rs = O.mul_mat_init(O.Q4_0, X)
     outs = []
-    for nt in (1, 4, 7):
-        O.lib().orc_set_threads(nt)
-        outs.append(O.mul_mat(W, O.Q4_0, rows, W.shape[1], k, wdata, rs, ncols))
+    for pool in (0, 1):  # the reference task pool and the bench's spin fork-join pool
+        O.lib().orc_set_pool(pool)
+        for nt in (1, 4, 7):
+            O.lib().orc_set_threads(nt)
+            outs.append(O.mul_mat(W, O.Q4_0, rows, W.shape[1], k, wdata, rs, ncols))
+    O.lib().orc_set_pool(0)
     O.lib().orc_set_threads(4)
     assert all(np.array_equal(outs[0], o) for o in outs[1:])
     # and equals the per-element vec_dot
