@@ -408,9 +408,21 @@ def main():
             try:
                 r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ggml_path_bench.py"), str(args.ggml_steps), td],
                                    capture_output=True, text=True, timeout=600)
-                mt = re.search(r"prefill_ms ([0-9.]+) prompt (\d+) decode_ms ([0-9.]+) steps (\d+) decode_tok_s ([0-9.]+)", r.stdout)
+                mt = re.search(r"prefill_ms ([0-9.]+) prompt (\d+) decode_ms ([0-9.]+) steps (\d+) decode_tok_s ([0-9.]+)"
+                               r"(?: upload_ms ([0-9.]+))?(?: first_prefill_ms ([0-9.]+) rounds (\d+))?", r.stdout)
                 if mt:
                     ggml_leg = {"decode_tok_s": float(mt.group(5)), "prefill_tok_s": round(int(mt.group(2)) / float(mt.group(1)) * 1e3, 1),
+                                "prefill_ms": float(mt.group(1)),
+                                "upload_ms": float(mt.group(6)) if mt.group(6) else None,
+                                "first_round_prefill_ms": float(mt.group(7)) if mt.group(7) else None,
+                                "rounds": int(mt.group(8)) if mt.group(8) else 1,
+                                "prefill_timing": "the last of `rounds` begin_one_round_inference rounds on the loaded model "
+                                                  "(compute: graph build, executor, the 128 x 256000 logits rows written to the "
+                                                  "host tensor); the first round also creates the device engine "
+                                                  "(first_round_prefill_ms)",
+                                "upload": "hpc_register_weight of every quantized weight at model load (INTEGRATION.md §1), "
+                                          "outside the reference loop's prefill timer; the first graph's engine copies them "
+                                          "device to device",
                                 "prompt": int(mt.group(2)), "steps": int(mt.group(4)),
                                 "path": "ggml_graph_compute_with_ctx recognises the Gemma graph and runs the device-resident engine "
                                         "over the graph's weights and KV-cache mirrors (ggml_api.cpp try_fast); includes the "

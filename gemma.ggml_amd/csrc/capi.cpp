@@ -213,6 +213,22 @@ extern "C" void hpc_flush_weights(void) {
 
 extern "C" void hpc_set_matvec_ks(int ks) { st().ks = ks > 0 ? ks : 1; }
 
+namespace ghip {
+// the tiled device copy of a registered (or already mul_mat'ed) Q4_0 / Q8_0 host weight with rows
+// of K values, any row count: the ggml fast path's engine copies its weights from here, device to
+// device, instead of uploading them from the host a second time
+bool registered_tiled(const void *host, int type, int64_t K, tiled_mat *out) {
+    hpc_state &s = st();
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    for (const auto &kv : s.weights)
+        if (kv.first.host == host && kv.first.type == type && kv.first.ne00 == K) {
+            *out = kv.second;
+            return true;
+        }
+    return false;
+}
+}  // namespace ghip
+
 extern "C" int hpc_register_weight(const void *host, int type, int64_t ne00, int64_t ne01, size_t nb01) {
     hpc_state &s = st();
     std::lock_guard<std::recursive_mutex> lk(s.mu);

@@ -794,8 +794,18 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
 
 // real weights in ggml row-major layout (a GGUF file's tensors, src/gemma_model.cpp:145-182)
 
-// rows [r0, r0 + dst.rows) of a host row-major Q4_0 / Q8_0 matrix into the tiled layout
+// rows [r0, r0 + dst.rows) of a host row-major Q4_0 / Q8_0 matrix into the tiled layout; from the
+// C-ABI weight cache's tiled copy (device to device) when the host weight was registered
+// (hpc_register_weight at model load), else uploaded and re-tiled
 static int upload_rows(const tiled_mat &dst, const void *host, int64_t r0, hipStream_t s) {
+    tiled_mat reg;
+    if (r0 % 8 == 0 && dst.rows % 8 == 0 && registered_tiled(host, dst.type, dst.K, &reg) && reg.n_bt == dst.n_bt &&
+        r0 + dst.rows <= reg.n_rt * 8) {
+        const tiled_mat src = sub_rows(reg, r0, dst.rows);
+        GHIP_CHECK(hipMemcpyAsync(dst.qs, src.qs, dst.qs_bytes(), hipMemcpyDeviceToDevice, s));
+        GHIP_CHECK(hipMemcpyAsync(dst.sc, src.sc, dst.sc_bytes(), hipMemcpyDeviceToDevice, s));
+        return 0;  // stream-ordered; engine_create synchronises before the first use
+    }
     const int64_t rb = dst.nb * (dst.type == T_Q4_0 ? 18 : 34);
     uint8_t *tmp = nullptr;
     GHIP_CHECK(hipMalloc(&tmp, (size_t)(rb * dst.rows)));
@@ -830,6 +840,9 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         set_error("gemma_engine_create: hipSetDevice failed");
         return nullptr;
     }
+    static const bool cprof = getenv("GHIP_CREATE_PROF") != nullptr;
+    auto cnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double ct0 = cprof ? cnow() : 0.0;
     auto *e = new gemma_engine();
     e->cfg = c;
     e->device = device;
@@ -869,17 +882,18 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     bool up_fail = false;  // a host-weight upload failed (last_error says which)
     e->kq = kq_layers;
     e->out_type = (c.out_type == T_Q6_K || kq_layers) ? T_Q6_K : wt;
-    if (e->out_type == T_Q6_K) {  // oracle make_kmat(TID_EMBD, Q6_K, 1/sqrt(E)) on the device
+    const double emb_std = (c.out_gain > 0.0f ? (double)c.out_gain : 1.0) / sqrt((double)c.n_embd);
+    if (e->out_type == T_Q6_K) {  // oracle make_kmat(TID_EMBD, Q6_K, out_gain/sqrt(E)) on the device
         e->embd_row_bytes = (int64_t)c.n_embd / 256 * 210;
         GHIP_FATAL(hipMalloc(&e->embd_q6k, (size_t)(e->embd_row_bytes * c.n_vocab)));
         GHIP_FATAL(hipMalloc(&e->xq8k, (size_t)c.n_embd / 256 * 292));
         e->xq8k_rows = 1;
         if (!hw)
             launch_synth_kquant(T_Q6_K, e->embd_q6k, c.n_vocab, c.n_embd, tensor_key(seed, TID_EMBD),
-                                (float)(1.0 / sqrt((double)c.n_embd) / 0.68), s);
+                                (float)(emb_std / 0.68), s);
     } else {
         e->embd = alloc_tiled(wt, c.n_vocab, c.n_embd, s);
-        if (!hw) launch_synth_tiled(e->embd, tensor_key(seed, TID_EMBD), synth_scale(1.0 / sqrt((double)c.n_embd)), 0, s);
+        if (!hw) launch_synth_tiled(e->embd, tensor_key(seed, TID_EMBD), synth_scale(emb_std), 0, s);
     }
     GHIP_FATAL(hipMalloc(&e->out_norm, (size_t)c.n_embd * 4));
     if (hw) {
@@ -998,6 +1012,10 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     if (up_fail) {
         gemma_engine_free(e);
         return nullptr;
+    }
+    if (cprof) {
+        (void)hipStreamSynchronize(s);
+        fprintf(stderr, "[gemma_hip] engine create: weights %.2f ms\n", cnow() - ct0);
     }
     // caches, tables, activations
     const size_t kv_elems = (size_t)c.n_layer * c.n_ctx * e->kvw;
@@ -1120,6 +1138,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         gemma_engine_free(e);
         return nullptr;
     }
+    if (cprof) fprintf(stderr, "[gemma_hip] engine create: total %.2f ms\n", cnow() - ct0);
     return e;
 }
 

@@ -667,6 +667,7 @@ int try_fast(ggml_cgraph *g) {
         if (getenv("GHIP_GGML_FAST_WHY")) fprintf(stderr, "[gemma_hip] ggml fast path not taken: %s\n", why.c_str());
         return 0;
     }
+    const double tm = prof ? now_us() : 0.0;
     executor &ex_ = ex();
     // the caches' device mirrors (device-authoritative: the graph writes them)
     std::vector<uint16_t *> kc, vc;
@@ -679,6 +680,7 @@ int try_fast(ggml_cgraph *g) {
         kv_keys.push_back(vc.back());
     }
     GHIP_CHECK(hipStreamSynchronize(ex_.stream));
+    const double ts = prof ? now_us() : 0.0;
     fast_engine &f = fast();
     // the engine serves positions below n_ctx - 1 (its RoPE / history tables); the last slot runs
     // node by node
@@ -704,6 +706,8 @@ int try_fast(ggml_cgraph *g) {
     }
     ggml_tensor *last = g->nodes[g->n_nodes - 1];
     const double t1 = prof ? now_us() : 0.0;
+    if (prof) fprintf(stderr, "[gemma_hip] fast path T=%d: match %.1f us, cache mirrors %.1f us, engine setup %.1f us\n", m.T,
+                      tm - t0, ts - tm, t1 - ts);
     const int rc = m.T == 1 ? gemma_engine_ext_decode(f.e, m.tokens[0], m.pos0, (float *)last->data)
                             : gemma_engine_ext_prefill(f.e, m.tokens.data(), m.T, (float *)last->data);
     if (rc) {  // the engine could not serve this graph: node by node instead (same results)

@@ -85,6 +85,8 @@ int launch_g_mul_mat_f16(const gt_desc &a, const uint16_t *b16, int64_t ne10, co
 void build_f16_tables(std::vector<uint16_t> &exp_t, std::vector<uint16_t> &gelu_t);
 void build_rope(int ctx, int hd, float base, std::vector<float> &c, std::vector<float> &s);
 tiled_mat alloc_tiled(int type, int64_t rows, int64_t K, hipStream_t s);
+// capi.cpp: the C-ABI weight cache's tiled copy of a host weight (hpc_register_weight / mul_mat)
+bool registered_tiled(const void *host, int type, int64_t K, tiled_mat *out);
 void free_tiled(tiled_mat &m);
 
 // ---- K-quant matvec (kquant.hip) -----------------------------------------------------------------

@@ -41,7 +41,7 @@ class GemmaConfig(C.Structure):
     _fields_ = [("n_layer", C.c_int), ("n_embd", C.c_int), ("n_head", C.c_int), ("n_head_kv", C.c_int),
                 ("head_dim", C.c_int), ("n_ff", C.c_int), ("n_vocab", C.c_int), ("n_ctx", C.c_int),
                 ("wtype", C.c_int), ("eps", C.c_float), ("rope_base", C.c_float), ("seed", C.c_uint64),
-                ("gelu_clamp", C.c_int), ("out_type", C.c_int)]
+                ("gelu_clamp", C.c_int), ("out_type", C.c_int), ("out_gain", C.c_float)]
 
 
 class GgmlTensor(C.Structure):
@@ -194,11 +194,11 @@ def mul_mat(src0_bytes, src0_type, ne01, nb01, shared_edge, wdata, row_size, nco
 
 class Engine:
     def __init__(self, shape, n_ctx=512, wtype=GGML_TYPE_Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0,
-                 gelu_clamp=0, device=0, tp=None, out_type=0):
+                 gelu_clamp=0, device=0, tp=None, out_type=0, out_gain=0.0):
         """tp = (n_ranks, rank, rccl_id_bytes) for the row-split engine (one process per GPU);
         rccl_id_bytes None = all ranks' shards virtual in this engine (single-GPU parity mode)."""
         self.cfg = GemmaConfig(n_ctx=n_ctx, wtype=wtype, eps=eps, rope_base=rope_base, seed=seed,
-                               gelu_clamp=gelu_clamp, out_type=out_type, **shape)
+                               gelu_clamp=gelu_clamp, out_type=out_type, out_gain=out_gain, **shape)
         self.L = lib()
         if tp is not None and tp[0] > 1:
             idbuf = C.create_string_buffer(bytes(tp[2]), len(tp[2])) if tp[2] is not None else None

@@ -60,6 +60,8 @@ typedef struct gemma_hip_config {
     uint64_t seed;
     int gelu_clamp;
     int out_type; /* token_embd / tied output: 0 = wtype, or GGML_TYPE_Q6_K (llama.cpp's Q4_0 / Q8_0 files) */
+    float out_gain; /* synthetic weights: token_embd / output std x out_gain (0 = 1; SURVEY §8(d) uses 4 for
+                       peaked logits in the Gemma-7B TP leg); ignored for GGUF weights */
 } gemma_hip_config;
 
 typedef struct gemma_engine gemma_engine;

@@ -151,8 +151,9 @@ extern "C" orc_model *orc_model_create(const orc_config *cfg) {
         delete m;
         return nullptr;
     }
-    m->embd = c.kmix ? make_kmat(c.seed, TID_EMBD, c.n_vocab, c.n_embd, ORC_Q6_K, 1.0 / sqrt((double)c.n_embd))
-                     : make_qmat(c.seed, TID_EMBD, c.n_vocab, c.n_embd, c.wtype, 1.0 / sqrt((double)c.n_embd));
+    const double emb_std = (c.out_gain > 0.0f ? (double)c.out_gain : 1.0) / sqrt((double)c.n_embd);
+    m->embd = c.kmix ? make_kmat(c.seed, TID_EMBD, c.n_vocab, c.n_embd, ORC_Q6_K, emb_std)
+                     : make_qmat(c.seed, TID_EMBD, c.n_vocab, c.n_embd, c.wtype, emb_std);
     m->out_norm = make_norm(c.seed, TID_OUT_NORM, c.n_embd);
     m->layers.resize(c.n_layer);
     for (int il = 0; il < c.n_layer; ++il) {

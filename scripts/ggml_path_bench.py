@@ -56,7 +56,9 @@ print(f"gguf written ({os.path.getsize(path) / 1e9:.2f} GB, {time.time() - t0:.1
 if os.environ.get("GGML_PATH_WRITE_ONLY"):  # keep the file for an external (profiled) driver run
     sys.exit(0)
 drv = os.path.join(ROOT, "tests", "ggml_driver", "gemma_graph_driver")
-env = dict(os.environ, DRIVER_BENCH="1")  # logits rows not written out per step (not part of the reference loop)
+# logits rows not written out per step (not part of the reference loop); two rounds of the reference's
+# begin_one_round_inference on the loaded model: the second round's prefill is compute only
+env = dict(os.environ, DRIVER_BENCH="1", DRIVER_ROUNDS=os.environ.get("DRIVER_ROUNDS", "2"))
 r = subprocess.run([drv, path, os.path.join(out, "prompt.bin"), os.path.join(out, "o.bin"), "512", str(n_decode)],
                    capture_output=True, text=True, timeout=900, env=env)
 open(os.path.join(out, "driver.err"), "w").write(r.stderr)

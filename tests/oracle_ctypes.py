@@ -25,7 +25,7 @@ class OrcConfig(C.Structure):
     _fields_ = [("n_layer", C.c_int), ("n_embd", C.c_int), ("n_head", C.c_int), ("n_head_kv", C.c_int),
                 ("head_dim", C.c_int), ("n_ff", C.c_int), ("n_vocab", C.c_int), ("n_ctx", C.c_int),
                 ("wtype", C.c_int), ("eps", C.c_float), ("rope_base", C.c_float), ("seed", C.c_uint64),
-                ("gelu_clamp", C.c_int), ("kmix", C.c_int)]
+                ("gelu_clamp", C.c_int), ("kmix", C.c_int), ("out_gain", C.c_float)]
 
 
 _lib = None
@@ -183,9 +183,10 @@ GEMMA_7B = dict(n_layer=28, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, 
 TINY = dict(n_layer=2, n_embd=512, n_head=2, n_head_kv=1, head_dim=256, n_ff=2048, n_vocab=4096)
 
 
-def make_config(shape, n_ctx=512, wtype=Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0, gelu_clamp=0, kmix=0):
+def make_config(shape, n_ctx=512, wtype=Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0, gelu_clamp=0, kmix=0,
+                out_gain=0.0):
     return OrcConfig(n_ctx=n_ctx, wtype=wtype, eps=eps, rope_base=rope_base, seed=seed, gelu_clamp=gelu_clamp,
-                     kmix=kmix, **shape)
+                     kmix=kmix, out_gain=out_gain, **shape)
 
 
 def dequantize(wtype, row_bytes, k):

@@ -98,11 +98,13 @@ def _check_out(m, prompt, n_decode, V, opath):
     return seq
 
 
-def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fast=1, second_seed=None):
+def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fast=1, second_seed=None, register=1):
     """fast=1: the executor recognises the Gemma graph and runs the device-resident engine over the
     graph's weights and KV-cache mirrors (ggml_api.cpp try_fast); fast=0: node by node.
     second_seed: a second model of the same shapes (other weights) run after the first in the same
-    driver process, whose pooled host arenas likely land at the first model's addresses."""
+    driver process, whose pooled host arenas likely land at the first model's addresses.
+    register (GGUF): the driver pre-uploads every quantized weight at load (hpc_register_weight) and
+    the fast path's engine copies them device to device; 0: the engine uploads from the host."""
     m = O.Model(O.make_config(shape, n_ctx=ctx, wtype=wtype, kmix=kmix))
     wpath, ppath, opath = tmp_path / ("m.gguf" if gguf else "w.bin"), tmp_path / "p.bin", tmp_path / "o.bin"
     if gguf:
@@ -121,7 +123,7 @@ def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fa
         args = [DRIVER, str(wpath), str(ppath), str(opath)] + [str(shape[k]) for k in
                 ("n_layer", "n_embd", "n_head", "n_head_kv", "head_dim", "n_ff", "n_vocab")] + [str(ctx), str(wtype),
                                                                                               str(n_decode)]
-    env = dict(os.environ, GHIP_GGML_FAST=str(fast), GHIP_GGML_FAST_WHY="1")
+    env = dict(os.environ, GHIP_GGML_FAST=str(fast), GHIP_GGML_FAST_WHY="1", DRIVER_NO_REGISTER=str(1 - register))
     if m2 is not None:
         env["DRIVER_SECOND"] = str(tmp_path / "w2.bin")
     r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
@@ -161,8 +163,9 @@ def test_ggml_graph_gemma2b_layers(tmp_path, fast):
 
 @gpu
 @pytest.mark.parametrize("fast", [1, 0])
-def test_ggml_graph_gguf_q4_0(tmp_path, fast):
-    _run(tmp_path, dict(O.TINY), O.Q4_0, 20, 4, 128, gguf=True, fast=fast)
+@pytest.mark.parametrize("register", [1, 0])
+def test_ggml_graph_gguf_q4_0(tmp_path, fast, register):
+    _run(tmp_path, dict(O.TINY), O.Q4_0, 20, 4, 128, gguf=True, fast=fast, register=register)
 
 
 @gpu

@@ -31,11 +31,23 @@ def test_synthetic_weights_match_oracle(wtype):
         assert np.array_equal(got, ref), f"tensor {tid} differs"
 
 
-def _check_decode(shape, n_prompt, n_decode, n_ctx, wtype=O.Q4_0, use_graph=True):
-    m = O.Model(O.make_config(shape, n_ctx=n_ctx, wtype=wtype))
+@gpu
+def test_synthetic_out_gain_matches_oracle():
+    """the TP leg's x4 token_embd / output: same bytes on both sides, and decode
+    stays bit-exact through the scaled embedding and logits"""
+    m = O.Model(O.make_config(O.TINY, n_ctx=128, out_gain=4.0))
+    e = _engine(O.TINY, n_ctx=128, out_gain=4.0)
+    ref = m.tensor(0)
+    assert np.array_equal(e.tensor(0, ref.size), ref)
+    e.close()
+    _check_decode(O.TINY, n_prompt=7, n_decode=12, n_ctx=128, out_gain=4.0)
+
+
+def _check_decode(shape, n_prompt, n_decode, n_ctx, wtype=O.Q4_0, use_graph=True, out_gain=0.0):
+    m = O.Model(O.make_config(shape, n_ctx=n_ctx, wtype=wtype, out_gain=out_gain))
     prompt = O.make_prompt(n_prompt, shape["n_vocab"])
     seq_ref, lg_ref = m.generate(prompt, n_decode)
-    e = _engine(shape, n_ctx=n_ctx, wtype=wtype)
+    e = _engine(shape, n_ctx=n_ctx, wtype=wtype, out_gain=out_gain)
     e.begin(prompt)
     lg = e.step(n_prompt + n_decode, want_logits=True, use_graph=use_graph)
     toks = e.tokens()
