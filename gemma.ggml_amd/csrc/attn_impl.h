@@ -191,9 +191,18 @@ constexpr int AH_THREADS = 1024;  // per-head form: 256 quads = 256 KQ positions
 #ifndef GHIP_AH_PF
 #define GHIP_AH_PF 4
 #endif
-constexpr int AH_KPF = GHIP_AH_PF;  // K steps (of 32 elements) prefetched per lane: hd <= 256
-constexpr int AH_VPF = GHIP_AH_PF;  // V steps (of 32 positions) prefetched per lane: n_kv <= 256
+#ifndef GHIP_AH_KPF
+#define GHIP_AH_KPF GHIP_AH_PF
+#endif
+#ifndef GHIP_AH_VPF
+#define GHIP_AH_VPF GHIP_AH_PF
+#endif
+constexpr int AH_KPF = GHIP_AH_KPF;  // K steps (of 32 elements) prefetched per lane: hd <= 256
+constexpr int AH_VPF = GHIP_AH_VPF;  // V steps (of 32 positions) prefetched per lane: n_kv <= 256
 
+#ifndef GHIP_AH_ABL
+#define GHIP_AH_ABL 0  // timing ablation only (wrong results): every K load reads row 0
+#endif
 #define AH_STAMP(i)                                                                                         \
     do {                                                                                                    \
         if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[(int64_t)h * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
@@ -213,7 +222,7 @@ __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, a
     const int G = a.H / a.Hkv, kvh = h / G, kvw = a.Hkv * hd;
     p.pos_v = ((const int *)a.rope_cur)[hd];  // published with the row (k_advance / begin)
     {
-        const int j = quad < a.ctx ? quad : 0;  // no dependency on pos: rows >= pos are masked
+        const int j = GHIP_AH_ABL ? 0 : quad < a.ctx ? quad : 0;  // no dependency on pos: rows >= pos are masked
         const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
 #pragma unroll
         for (int s = 0; s < KPF; ++s) p.k[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
@@ -272,6 +281,11 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     uint16_t *k16 = q16 + hd;          // hd (this token's k, post-rope)
     float *S = (float *)(smem + ((2 * hd * 2 + 15) & ~15));  // ctx
     uint16_t *P16 = (uint16_t *)(S + a.ctx);                 // ctx
+    // softmax reduction words (8-aligned, after P16): the row max as an order-preserving key, and
+    // the exact integer sum of the e values (both order-independent, so partial results combine in
+    // any order and the bits equal a one-wave reduction's)
+    uint32_t *mx_key = (uint32_t *)(smem + ((((2 * hd * 2 + 15) & ~15) + a.ctx * 6 + 7) & ~7));
+    unsigned long long *e_sum = (unsigned long long *)(mx_key + 2);
 
     // RoPE NEOX on q (then * q_scale) and on k; f32 -> f16 (ggml_cpy / MUL_MAT INIT conversions)
     auto rope4 = [&](float4 x0v, float4 x1v, float scale, bool scaled, uint16_t *lo, uint16_t *hi) {
@@ -294,6 +308,10 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         rope4(qa, qb, a.q_scale, true, q16 + i4, q16 + i4 + half);
         rope4(ka, kb, 1.0f, false, k16 + i4, k16 + i4 + half);
     }
+    if (tid == 0) {
+        *mx_key = 0u;  // below the key of every float, -inf included
+        *e_sum = 0ull;
+    }
     __syncthreads();
     AH_STAMP(1);
     // this token's cache entries (src/gemma_model.cpp:506-517), by the group's first head; readers
@@ -304,18 +322,25 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             if (t4 == 0) a.vc[((int64_t)kvh * hd + d) * a.ctx + pos] = f2h(d == d0 ? vx0 : ld1<SC1>(vh + d));
     }
     // ---- KQ (vec_dot_f16 over hd per kv position) + mask (j > pos -> -inf), scale 1.0
+    float lmax = -INFINITY;
+    // q in registers: every position's dot reads the same hd/32 steps (one LDS round trip here
+    // instead of one per step and position)
+    uint4 qr[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qr[s] = *(const uint4 *)(q16 + (s * 32 < hd ? s * 32 : 0) + t4 * 8);
     for (int j0 = 0; j0 < n_kv; j0 += NTH / 4) {
         const int j = j0 + quad;
         float acc[8];
 #pragma unroll
         for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
         if (j == pos) {
-            for (int s = 0; s * 32 < hd; ++s)
-                f16_step8(acc, *(const uint4 *)(k16 + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s * 32 < hd) f16_step8(acc, *(const uint4 *)(k16 + s * 32 + t4 * 8), qr[s]);
         } else if (j0 == 0) {
             // the row's remaining K steps (hd <= 256: at most 8 - KPF) issued together before the
             // prefetched steps' arithmetic: one round trip, not one per step
-            const uint16_t *krow = a.kc + (int64_t)(j < a.ctx ? j : 0) * kvw + (int64_t)kvh * hd;
+            const uint16_t *krow = a.kc + (int64_t)(GHIP_AH_ABL ? 0 : j < a.ctx ? j : 0) * kvw + (int64_t)kvh * hd;
             constexpr int KR = 8 - KPF > 0 ? 8 - KPF : 1;
             uint4 krest[KR];
 #pragma unroll
@@ -325,87 +350,65 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             }
 #pragma unroll
             for (int s = 0; s < KPF; ++s)
-                if (s * 32 < hd) f16_step8(acc, kpre[s], *(const uint4 *)(q16 + s * 32 + t4 * 8));
+                if (s * 32 < hd) f16_step8(acc, kpre[s], qr[s < 8 ? s : 0]);
 #pragma unroll
             for (int r = 0; r < KR; ++r) {
                 const int s = KPF + r;
-                if (KPF < 8 && s * 32 < hd) f16_step8(acc, krest[r], *(const uint4 *)(q16 + s * 32 + t4 * 8));
+                if (KPF < 8 && s * 32 < hd) f16_step8(acc, krest[r], qr[s < 8 ? s : 0]);
             }
         } else {
             const int jc = j < pos ? j : 0;  // j > pos is masked below
             const uint16_t *krow = a.kc + (int64_t)jc * kvw + (int64_t)kvh * hd;
-            for (int s = 0; s * 32 < hd; ++s)
-                f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), *(const uint4 *)(q16 + s * 32 + t4 * 8));
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s * 32 < hd) f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), qr[s]);
         }
         const float kq = quad_reduce_f16(acc);
         if (t4 == 0 && j < n_kv) {
             const float w = (j > pos) ? -INFINITY : kq * 1.0f + 0.0f;
             S[j] = w;
+            lmax = fmaxf(lmax, w);
             if (a.dbg_w) a.dbg_w[(int64_t)h * a.ctx + j] = w;
         }
     }
+    // the row max, partial per wave (DPP) then one LDS max per wave, in the same barrier as S
+    lmax = wave_max(lmax);
+    if (lane == 0) {
+        const uint32_t b = __builtin_bit_cast(uint32_t, lmax);
+        atomicMax(mx_key, (b & 0x80000000u) ? ~b : (b | 0x80000000u));
+    }
     __syncthreads();
     AH_STAMP(2);
-    // ---- soft_max_ext: every wave reduces the whole row (DPP) and writes P16 for its
-    // own slice j = 64*wave + lane + NTH*m: one barrier for the whole softmax.  Rows of up to 512
-    // positions: the lane's 8 scores are read in one batch (one LDS round trip, not one per step)
-    if (n_kv <= 512 && NTH >= 512) {
-        float sv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sv[k] = lane + 64 * k < n_kv ? S[lane + 64 * k] : -INFINITY;
-        float mx = sv[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) mx = fmaxf(mx, sv[k]);
-        mx = wave_max(mx);
+    // ---- soft_max_ext: e = f16(exp(f16(w - max))) per position, its exact integer
+    // sum, P16 = f16(e * (float)(1 / sum)).  The position's quad lane 0 (which formed S[j]) forms e;
+    // the sum is exact in any order (e = k * 2^-24, k <= 2^24), reduced per wave by DPP and across
+    // waves by one LDS add per wave: the bits equal a serial pass, and no wave repeats the row
+    {
+        const uint32_t key = *mx_key;
+        const float mx = __builtin_bit_cast(float, (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key);
+        AH_STAMP(5);
         unsigned long long isum = 0;
-        float own = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float e = sv[k] != -INFINITY ? h2f(exp_f16_of(f2h(sv[k] - mx))) : 0.0f;
-            isum += (unsigned long long)(uint32_t)(e * 16777216.0f);  // exact: e*2^24 <= 2^24
-            if (k == wave) own = e;  // this thread's P16 element j = tid = 64*wave + lane
-        }
-        const unsigned long long tot = wave_sum_u64(isum);
-        const double sum = (double)tot * (1.0 / 16777216.0);
-        const float inv = (float)(1.0 / sum);
-        if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
-        if (tid < n_kv) {
-            P16[tid] = f2h(own * inv);
-            if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + tid] = P16[tid];
-        }
-    } else {
-    float mx = -INFINITY;
-    for (int j = lane; j < n_kv; j += 64) mx = fmaxf(mx, S[j]);
-    mx = wave_max(mx);
-    unsigned long long isum = 0;
-    float mine[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int j = lane, k = 0; j < n_kv; j += 64, ++k) {
-        const float w = S[j];
-        float e = 0.0f;
-        if (w != -INFINITY) e = h2f(exp_f16_of(f2h(w - mx)));
-        // e is fp16 in [0,1]: an exact multiple of 2^-24, so the integer sum is the exact sum
-        isum += (unsigned long long)(uint32_t)(e * 16777216.0f);  // e*2^24 <= 2^24: exact in u32 (one v_cvt_u32_f32)
-        const int r = k - wave;
-        if (r >= 0 && r % nwave == 0) {
-            const int m = r / nwave;
-            if (m == 0) mine[0] = e; else if (m == 1) mine[1] = e; else if (m == 2) mine[2] = e; else if (m == 3) mine[3] = e;
-        }
-    }
-    const unsigned long long tot = wave_sum_u64(isum);
-    const double sum = (double)tot * (1.0 / 16777216.0);
-    const float inv = (float)(1.0 / sum);
-    if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
-    for (int j = tid, m = 0; j < n_kv; j += NTH, ++m) {
-        float e;
-        if (m < 4) {
-            e = m == 0 ? mine[0] : m == 1 ? mine[1] : m == 2 ? mine[2] : mine[3];
-        } else {  // long rows: recompute (same table lookup, same value)
+        for (int j = quad; j < n_kv; j += NTH / 4) {
+            if (t4 != 0) break;
             const float w = S[j];
-            e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
+            const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
+            isum += (unsigned long long)(uint32_t)(e * 16777216.0f);  // e*2^24 <= 2^24: exact
         }
-        P16[j] = f2h(e * inv);
-        if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
-    }
+        isum = wave_sum_u64(isum);
+        if (lane == 0 && isum) atomicAdd(e_sum, isum);
+        __syncthreads();
+        AH_STAMP(6);
+        const double sum = (double)*e_sum * (1.0 / 16777216.0);
+        const float inv = (float)(1.0 / sum);
+        AH_STAMP(7);
+        if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
+        for (int j = quad; j < n_kv; j += NTH / 4) {
+            if (t4 != 0) break;
+            const float w = S[j];
+            const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
+            P16[j] = f2h(e * inv);
+            if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
+        }
     }
     __syncthreads();
     AH_STAMP(3);
@@ -430,8 +433,9 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         };
         if (n_kv <= 256) {
             // every step's V load issued before the first step's arithmetic (one round trip);
-            // the prefetched steps of the first dimension come from the early loads
-            uint4 xs8[8];
+            // the prefetched steps of the first dimension come from the early loads; P16 (the same
+            // for every dimension) read into registers once
+            uint4 xs8[8], pr8[8];
             const bool first = d == d0;
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
@@ -440,12 +444,14 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
                 else xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
             }
 #pragma unroll
+            for (int s = 0; s < 8; ++s) pr8[s] = *(const uint4 *)(P16 + (s * 32 < n_kv ? s * 32 : 0) + t4 * 8);
+#pragma unroll
             for (int s = 0; s < 8; ++s) {
                 if (s * 32 >= n_kv) break;
                 const int e0 = s * 32 + t4 * 8;
                 uint4 xv = xs8[s];
                 patch(xv, e0);
-                f16_step8(acc, xv, *(const uint4 *)(P16 + e0));
+                f16_step8(acc, xv, pr8[s]);
             }
         } else
         for (int st = 0, s = 0; st < n_kv; st += 32, ++s) {

@@ -116,7 +116,7 @@ struct tok_layout {
     // image maps (offsets inside IMG): K = E (with ns) and K = F (no ns plane)
     static constexpr uint32_t E_ACT = 0, E_NS = E, E_DA = WT == T_Q4_0 ? 2 * E : E;
     static constexpr uint32_t F_ACT = 0, F_NS = 0, F_DA = F;
-    static constexpr uint32_t ATT_QKV(int ctx) { return ((uint32_t)(1024 + 6 * ctx) + 15) & ~15u; }
+    static constexpr uint32_t ATT_QKV(int ctx) { return ((uint32_t)(1024 + 6 * ctx + 16) + 15) & ~15u; }
     static constexpr bool att_fits(int ctx, int qkv_rows) {
         return ATT_QKV(ctx) + (uint32_t)qkv_rows * 4 <= IMG_F && E_DA + E / 8 <= IMG_F;
     }
