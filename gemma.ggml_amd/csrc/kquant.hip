@@ -465,7 +465,7 @@ __device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t r
     }
 }
 
-template <int WT, bool DUAL, int XJ, bool TL>
+template <int WT, bool DUAL, int XJ, bool TL, int PF = KQ_PF>
 __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];  // the column's Q8_K blocks
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
@@ -478,12 +478,12 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
     // gate rows, each in its own ordered chain; the epilogue forms gelu(gate) * up in registers
     kq_pro_regs<XJ> pr;
     kq_pro_load<XJ>(a, col, wave, KQ_THREADS / 64, lane, pr);
-    kq_raw<WT> r[KQ_PF], r2[DUAL ? KQ_PF : 1];
+    kq_raw<WT> r[PF], r2[DUAL ? PF : 1];
 #if GHIP_KQ_EARLY
     {
         const int64_t row0 = g0 * 8 + rr < a.rows ? g0 * 8 + rr : a.rows - 1;
 #pragma unroll
-        for (int p = 0; p < KQ_PF; ++p) {
+        for (int p = 0; p < PF; ++p) {
             r[p] = kq_load<WT, TL>(a.w + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
             if (DUAL) r2[p] = kq_load<WT, TL>(a.w2 + row0 * a.row_bytes, p < a.nsb ? p : 0, l);
         }
@@ -500,10 +500,10 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
         const uint8_t *wrow = a.w + row * a.row_bytes;
         const uint8_t *wrow2 = DUAL ? a.w2 + row * a.row_bytes : nullptr;
         float acc = 0.0f, accm = 0.0f, acc2 = 0.0f, accm2 = 0.0f;
-        for (int s0 = 0; s0 < a.nsb; s0 += KQ_PF) {
+        for (int s0 = 0; s0 < a.nsb; s0 += PF) {
             if (!early) {
 #pragma unroll
-                for (int p = 0; p < KQ_PF; ++p) {
+                for (int p = 0; p < PF; ++p) {
                     r[p] = kq_load<WT, TL>(wrow, s0 + p < a.nsb ? s0 + p : s0, l);
                     if (DUAL) r2[p] = kq_load<WT, TL>(wrow2, s0 + p < a.nsb ? s0 + p : s0, l);
                 }
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
             early = false;
 #endif
 #pragma unroll
-            for (int p = 0; p < KQ_PF; ++p) {
+            for (int p = 0; p < PF; ++p) {
                 if (s0 + p >= a.nsb) break;
                 const kq_term t = kq_terms<WT>(r[p], xs, s0 + p, l);
                 acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
@@ -739,6 +739,84 @@ __device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
 template <int WT, int KS, int XJ, int PF, bool TL>
 __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks(kq_args a) {
     kq_ks_body<WT, KS, XJ, PF, TL>(a, (int)blockIdx.x);
+}
+
+// Round-pipelined K split (matvec_rr.hip's form, for the K-quant down shape: 8 x NR super-blocks
+// per row, a precomputed Q8_K column).  One row group per workgroup; 8 loader waves interleave over
+// K by rounds (round r: loader w takes super-block w + 8r, so a round is 8 consecutive
+// super-blocks), each keeping D rounds of its weight loads in flight; a loader turns its
+// super-block into the exact terms (sumi, d [, prod, dmin]) of kq_terms and stashes them in one of
+// two LDS slots; the 9th wave, the carrier, chains round r-1's eight super-blocks in order while
+// the loaders convert round r.  The carrier's chain is the same fmaf sequence over super-blocks
+// 0, 1, ... as k_matvec_kq_ks's wave 0 (own segment, then the stash): identical bits.  The column
+// goes out first (its loads are the oldest, so its wait never waits for a weight load).
+constexpr int KR_NL = 8, KR_NTH = 64 * (KR_NL + 1);
+__device__ __forceinline__ void kr_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int WT, int NR, int D>
+__global__ void __launch_bounds__(KR_NTH) k_matvec_kq_rr(kq_args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rr = lane >> 3, l = lane & 7, col = blockIdx.y;
+    constexpr int NSB = KR_NL * NR;
+    const bool loader = wave < KR_NL;
+    const int64_t row_raw = (int64_t)blockIdx.x * 8 + rr;
+    const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
+    const uint8_t *wrow = a.w + row * a.row_bytes;
+    constexpr size_t IMG = ((size_t)NSB * 292 + 15) & ~(size_t)15;
+    int *st_i = (int *)(xs + IMG);        // [2][8][64] lane sums
+    float *st_d = (float *)(st_i + 1024); // [2][8][8]  per-row d
+    int *st_p = (int *)(st_d + 128);      // [2][8][64] mins products (Q4_K)
+    float *st_m = (float *)(st_p + 1024); // [2][8][8]  per-row dmin (Q4_K)
+    // 0) the column (oldest loads), then D rounds of weights, then the column into LDS
+    constexpr int N16 = NSB * 292 / 16, CPN = (N16 + KR_NTH - 1) / KR_NTH;
+    const uint4 *src = (const uint4 *)(a.x + (int64_t)col * a.x_col_stride);
+    uint4 cv[CPN];
+#pragma unroll
+    for (int k = 0; k < CPN; ++k) {
+        const int i = tid + k * KR_NTH;
+        cv[k] = src[i < N16 ? i : 0];
+    }
+    const int w8 = loader ? wave : 0;  // the carrier re-reads loader 0's rounds (L2 hits, unused)
+    kq_raw<WT> r[D];
+#pragma unroll
+    for (int p = 0; p < D; ++p) r[p] = kq_load<WT, true>(wrow, w8 + KR_NL * (p < NR ? p : 0), l);
+#pragma unroll
+    for (int k = 0; k < CPN; ++k) {
+        const int i = tid + k * KR_NTH;
+        if (i < N16) ((uint4 *)xs)[i] = cv[k];
+    }
+    kr_barrier();
+    float acc = 0.0f, accm = 0.0f;
+    auto chain = [&](int rc) {
+        const int sl = rc & 1;
+#pragma unroll
+        for (int w = 0; w < KR_NL; ++w) {
+            acc = __builtin_fmaf(st_d[(sl * 8 + w) * 8 + rr], (float)st_i[(sl * 8 + w) * 64 + lane], acc);
+            if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(st_m[(sl * 8 + w) * 8 + rr], (float)st_p[(sl * 8 + w) * 64 + lane], accm);
+        }
+    };
+    if (!loader) __builtin_amdgcn_s_setprio(3);  // the chain is the critical path
+#pragma unroll
+    for (int r0 = 0; r0 < NR; ++r0) {
+        if (loader) {
+            const kq_term t = kq_terms<WT>(r[r0 % D], xs, wave + KR_NL * r0, l);
+            if (r0 + D < NR) r[r0 % D] = kq_load<WT, true>(wrow, wave + KR_NL * (r0 + D), l);
+            const int sl = r0 & 1;
+            st_i[(sl * 8 + wave) * 64 + lane] = t.sumi;
+            if (l == 0) st_d[(sl * 8 + wave) * 8 + rr] = t.d;
+            if (WT == T_Q4_K) {
+                st_p[(sl * 8 + wave) * 64 + lane] = t.prod;
+                if (l == 0) st_m[(sl * 8 + wave) * 8 + rr] = t.dmin;
+            }
+        } else if (r0 > 0) {
+            chain(r0 - 1);
+        }
+        kr_barrier();
+    }
+    if (loader) return;
+    chain(NR - 1);
+    kq_store<WT>(a, col, row_raw, l, acc, accm);
 }
 
 // Two matrices of one input column in one launch (a layer's q|k and v: Q4_K and Q6_K in Q4_K_M
@@ -1069,6 +1147,26 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         }
         if (a.tiled) return d ? go((const void *)k_matmul_kq<T_Q6_K, true, 4, true>) : go((const void *)k_matmul_kq<T_Q6_K, false, 4, true>);
         return d ? go((const void *)k_matmul_kq<T_Q6_K, true, 4, false>) : go((const void *)k_matmul_kq<T_Q6_K, false, 4, false>);
+    }
+    // the down shape (64 super-blocks per row, precomputed column, engine layout): round-pipelined
+    // (GHIP_KQ_RR=0: the K-split form below; GHIP_KQ_RRD: rounds in flight per loader, 4 or 8;
+    // Q4_K_M decode, same box: K-split 1,013-1,015 tok/s; rounds 2 / 3 / 4 / 6 / 8 in flight:
+    // 1,032-1,038 / 1,042-1,047 / 1,052 / 1,041-1,044 / 1,017-1,020)
+    static const int kq_rr = getenv("GHIP_KQ_RR") ? atoi(getenv("GHIP_KQ_RR")) : 1;
+    static const int kq_rrd = getenv("GHIP_KQ_RRD") ? atoi(getenv("GHIP_KQ_RRD")) : 4;
+    if (kq_rr && !a.w2 && a.tiled && a.nsb == 64 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && a.x_col_stride % 16 == 0 &&
+        ((uintptr_t)a.x & 15) == 0) {
+        const size_t lds_rr = (((size_t)64 * 292 + 15) & ~(size_t)15) + 2 * (1024 + 128) * 4;
+        const dim3 grid((unsigned)groups, a.ncols);
+        if (kq_rrd == 8) {
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_rr<T_Q4_K, 8, 8>), grid, dim3(KR_NTH), lds_rr, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_rr<T_Q6_K, 8, 8>), grid, dim3(KR_NTH), lds_rr, s, a);
+        } else {
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_rr<T_Q4_K, 8, 4>), grid, dim3(KR_NTH), lds_rr, s, a);
+            else hipLaunchKernelGGL((k_matvec_kq_rr<T_Q6_K, 8, 4>), grid, dim3(KR_NTH), lds_rr, s, a);
+        }
+        GHIP_CHECK(hipGetLastError());
+        return 0;
     }
     if (!a.w2 && groups < 2048 && a.nsb % 8 == 0 && a.nsb >= ks_min && a.nsb <= 64 && lds_ks <= 64 * 1024) {
         const dim3 grid((unsigned)groups, a.ncols);
