@@ -247,6 +247,8 @@ extern "C" int hpc_register_weight(const void *host, int type, int64_t ne00, int
     return get_weight({host, type, ne00, ne01, nb01}) ? 0 : -1;
 }
 
+extern "C" void hpc_set_kq_gemm_min(int min_cols) { set_kq_gemm_min(min_cols); }
+
 extern "C" void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, int64_t ne1, int64_t nb1, int64_t nb2,
                         size_t row_size, int64_t shared_edge, struct ggml_tensor *src0, struct ggml_tensor *src1,
                         struct ggml_tensor *dst, ggml_vec_dot_t vec_dot, enum ggml_type src0_type,
@@ -289,16 +291,39 @@ extern "C" void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, 
             return fail("K-quant mul_mat needs shared_edge % 256 == 0 and Q8_K wdata rows");
         const uint8_t *W = get_raw_weight({src0->data, type, shared_edge, ne01, (size_t)nb01});
         if (!W) return fail(last_error());
-        if (ensure_scratch(dst_bytes + w_bytes + 256)) return fail(last_error());
+        // >= kq_gemm_min() (default 8) columns: the MFMA GEMM (prefill_kq.hip) against the f16 image
+        // of the Q8_K columns; fewer: the dot4 matvec / T-column kernel
+        const bool mfma = col_num >= kq_gemm_min();
+        const int64_t nsb = shared_edge / 256;
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t xh_bytes = mfma ? (size_t)col_num * shared_edge * 2 : 0, xd_bytes = mfma ? (size_t)col_num * nsb * 4 : 0;
+        const size_t xm_bytes = mfma ? (size_t)col_num * nsb * 32 : 0;
+        if (ensure_scratch(al(dst_bytes) + al(w_bytes) + al(xh_bytes) + al(xd_bytes) + xm_bytes + 256)) return fail(last_error());
         dev_dst = (float *)s.scratch;
-        dev_w = (const char *)s.scratch + ((dst_bytes + 255) & ~(size_t)255);
+        dev_w = (const char *)s.scratch + al(dst_bytes);
         if (hipMemcpyAsync((void *)dev_w, wdata, w_bytes, hipMemcpyHostToDevice, s.stream) != hipSuccess)
             return fail("mul_mat: wdata upload failed");
+        if (mfma) {
+            uint8_t *base = (uint8_t *)dev_w + al(w_bytes);
+            q8kx_args x;
+            x.x = (const uint8_t *)dev_w; x.x_col_stride = (int64_t)row_size; x.nsb = (int)nsb; x.T = (int)col_num;
+            x.xh = (uint16_t *)base; x.ldh = shared_edge;
+            x.xd = (float *)(base + al(xh_bytes)); x.ldd = nsb;
+            x.xm = (uint16_t *)(base + al(xh_bytes) + al(xd_bytes)); x.ldm = nsb;
+            if (launch_q8k_expand(x, s.stream)) return fail(last_error());
+            kqg_args g;
+            g.w = W; g.row_bytes = kq_row_bytes(type, shared_edge); g.rows = ne01; g.nsb = (int)nsb; g.T = (int)col_num;
+            g.tiled = 0;
+            g.xh = x.xh; g.ldh = x.ldh; g.xd = x.xd; g.ldd = x.ldd; g.xm = x.xm; g.ldm = x.ldm;
+            g.y = dev_dst; g.ldy = ne01;
+            if (launch_gemm_kq(type, g, s.stream)) return fail(last_error());
+        } else {
         kq_args a;
         a.w = W; a.row_bytes = kq_row_bytes(type, shared_edge); a.rows = ne01; a.nsb = (int)(shared_edge / 256);
         a.x = (const uint8_t *)dev_w; a.x_col_stride = (int64_t)row_size;
         a.y = dev_dst; a.y_col_stride = ne01; a.ncols = (int)col_num;
         if (launch_matvec_kq(type, a, s.stream)) return fail(last_error());
+        }
     } else if (type == T_F16) {
         // src0 (e.g. a KV-cache view) changes between calls: upload the ne01 rows every time
         const size_t K = (size_t)shared_edge;

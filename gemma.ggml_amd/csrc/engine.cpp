@@ -273,6 +273,7 @@ struct gemma_engine {
         uint16_t *Q16 = nullptr;
         int8_t *XQ = nullptr;
         uint16_t *XH = nullptr;  // f16 image of the quantized activations (exact GEMM operand)
+        uint16_t *XM = nullptr;  // K-quant prefill: the Q4_K mins operand of the Q8_K image (k_q8k_expand)
         void *keys = nullptr;
     } pf;
     float *dbg = nullptr;  // per-layer taps [L][qkv_rows + qw + E] (debug steps only)
@@ -1308,7 +1309,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     }
     void *bufs[] = {e->tok_gran, e->epoch, e->tok_err, e->tok_dev, e->tok_tab, e->front_cnt, e->front_err, e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
                     e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf.X, e->pf.SA, e->pf.QKV, e->pf.ATT, e->pf.G, e->pf.U,
-                    e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.XH, e->pf.keys};
+                    e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.XH, e->pf.XM, e->pf.keys};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (e->embd_q6k) (void)hipFree(e->embd_q6k);
@@ -1816,7 +1817,7 @@ extern "C" int gemma_engine_set_plan(gemma_engine *e, const int *in, int n) {
 static int prefill_alloc(gemma_engine *e, int T) {
     auto &p = e->pf;
     if (p.T >= T) return 0;
-    void *bufs[] = {p.X, p.SA, p.QKV, p.ATT, p.G, p.U, p.LG, p.DA, p.Q16, p.XQ, p.XH, p.keys};
+    void *bufs[] = {p.X, p.SA, p.QKV, p.ATT, p.G, p.U, p.LG, p.DA, p.Q16, p.XQ, p.XH, p.XM, p.keys};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     const gemma_hip_config &c = e->cfg;
@@ -1835,12 +1836,24 @@ static int prefill_alloc(gemma_engine *e, int T) {
     // K-quant layers: XQ holds T Q8_K columns (292 B per 256 values) instead of the int8 image
     GHIP_CHECK(hipMalloc(&p.XQ, (size_t)T * (e->kq ? p.ldq / 256 * 292 : p.ldq)));
     GHIP_CHECK(hipMalloc(&p.XH, (size_t)T * p.ldq * 2));
+    GHIP_CHECK(hipMalloc(&p.XM, (size_t)T * (p.ldq / 256) * 32));
     GHIP_CHECK(hipMalloc(&p.keys, 256 * 8));
     p.T = T;
     return 0;
 }
 
 static int enqueue_prefill_kq(gemma_engine *e, int T);
+
+// the K-quant prefill's MFMA GEMM (prefill_kq.hip) for T prompt rows (kq_gemm_min: default 8)
+static bool kq_prefill_mfma(int T) { return T >= kq_gemm_min(); }
+// T Q8_K columns of K values (ld bytes apart) -> the GEMM's f16 image in the prefill scratch
+static int kq_expand(gemma_engine *e, const uint8_t *x, int64_t ld, int64_t K, int T) {
+    auto &p = e->pf;
+    q8kx_args a;
+    a.x = x; a.x_col_stride = ld; a.nsb = (int)(K / 256); a.T = T;
+    a.xh = p.XH; a.ldh = p.ldq; a.xd = p.DA; a.ldd = p.ldd; a.xm = p.XM; a.ldm = p.ldq / 256;
+    return launch_q8k_expand(a, e->stream);
+}
 
 static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nullptr) {
     const gemma_hip_config &c = e->cfg;
@@ -1908,10 +1921,19 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
             e->xq8k_rows = T;
         }
         if (launch_norm_q8K(p.X, E, e->out_norm, (int)E, c.eps, T, e->xq8k, ld, s)) return -1;
-        kq_args k;
-        k.w = e->embd_q6k; k.tiled = e->embd_tiled; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = (int)(E / 256);
-        k.x = e->xq8k; k.x_col_stride = ld; k.y = p.LG; k.y_col_stride = c.n_vocab; k.ncols = T;
-        if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
+        if (exact && kq_prefill_mfma(T) && e->embd_tiled && E % 2048 == 0) {  // the MFMA GEMM (prefill_kq.hip)
+            if (kq_expand(e, e->xq8k, ld, E, T)) return -1;
+            kqg_args g;
+            g.w = e->embd_q6k; g.row_bytes = e->embd_row_bytes; g.rows = c.n_vocab; g.nsb = (int)(E / 256); g.T = T;
+            g.xh = p.XH; g.ldh = p.ldq; g.xd = p.DA; g.ldd = p.ldd; g.xm = p.XM; g.ldm = p.ldq / 256;
+            g.y = p.LG; g.ldy = c.n_vocab;
+            if (launch_gemm_kq(T_Q6_K, g, s)) return -1;
+        } else {
+            kq_args k;
+            k.w = e->embd_q6k; k.tiled = e->embd_tiled; k.row_bytes = e->embd_row_bytes; k.rows = c.n_vocab; k.nsb = (int)(E / 256);
+            k.x = e->xq8k; k.x_col_stride = ld; k.y = p.LG; k.y_col_stride = c.n_vocab; k.ncols = T;
+            if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
+        }
     } else {
         if (quant(QR_NORM, p.X, nullptr, E, e->out_norm)) return -1;
         if (gemm(e->embd, EPI_STORE, nullptr, p.LG, c.n_vocab)) return -1;
@@ -1939,7 +1961,20 @@ static int enqueue_prefill_kq(gemma_engine *e, int T) {
     const int64_t E = c.n_embd, F = c.n_ff;
     const int64_t ldk = p.ldq / 256 * 292;  // Q8_K column stride in XQ
     uint8_t *img = (uint8_t *)p.XQ;
+    // T >= kq_gemm_min() (default 8): the lane-tiled matrices go through the MFMA GEMM
+    // (prefill_kq.hip) against the f16 image each Q8_K INIT is expanded to; below, or with
+    // GHIP_KQ_MFMA=0, the dot4 T-column kernel.  Same bytes either way (tests/test_gpu_engine_gguf.py).
+    const bool mfma = kq_prefill_mfma(T);
+    auto mfma_ok = [&](const kq_mat &W) { return mfma && W.tiled && (W.type == T_Q4_K || W.K % 2048 == 0); };
+    auto expand = [&](int64_t K) { return mfma ? kq_expand(e, img, ldk, K, T) : 0; };
     auto mv = [&](const kq_mat &W, float *y, int64_t ldy, const float *resid, const float *gate_in, const kq_mat *up) {
+        if (!up && mfma_ok(W)) {
+            kqg_args g;
+            g.w = W.w; g.row_bytes = W.rb; g.rows = W.rows; g.nsb = (int)(W.K / 256); g.T = T;
+            g.xh = p.XH; g.ldh = p.ldq; g.xd = p.DA; g.ldd = p.ldd; g.xm = p.XM; g.ldm = p.ldq / 256;
+            g.y = y; g.ldy = ldy; g.resid = resid; g.gate_in = gate_in; g.gelu_tab = e->gelu_tab; g.gelu_clamp = c.gelu_clamp;
+            return launch_gemm_kq(W.type, g, s);
+        }
         kq_args k;
         k.w = W.w; k.row_bytes = W.rb; k.rows = W.rows; k.nsb = (int)(W.K / 256);
         k.x = img; k.x_col_stride = ldk; k.y = y; k.y_col_stride = ldy; k.ncols = T;
@@ -1954,7 +1989,7 @@ static int enqueue_prefill_kq(gemma_engine *e, int T) {
     for (int il = 0; il < c.n_layer; ++il) {
         const layer_dev &L = e->layers[il];
         const kq_layer &K = e->kql[il];
-        if (launch_norm_q8K(p.X, E, L.attn_norm, (int)E, c.eps, T, img, ldk, s)) return -1;
+        if (launch_norm_q8K(p.X, E, L.attn_norm, (int)E, c.eps, T, img, ldk, s) || expand(E)) return -1;
         const int64_t ldqkv = e->qkv_rows;
         if (K.qk_fused) {
             kq_mat qk = K.q;
@@ -1975,15 +2010,16 @@ static int enqueue_prefill_kq(gemma_engine *e, int T) {
         at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
         at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
         if (launch_attn_rows(at, s)) return -1;
-        if (launch_quant_q8_K(p.ATT, e->qw, e->qw, T, img, ldk, s)) return -1;
+        if (launch_quant_q8_K(p.ATT, e->qw, e->qw, T, img, ldk, s) || expand(e->qw)) return -1;
         if (mv(K.o, p.SA, E, p.X, nullptr, nullptr)) return -1;  // + inpL
-        if (launch_norm_q8K(p.SA, E, L.ffn_norm, (int)E, c.eps, T, img, ldk, s)) return -1;
-        if (K.gate.type == K.up.type && K.gate.rows == K.up.rows && K.gate.K == K.up.K && e->kq_dual) {
+        if (launch_norm_q8K(p.SA, E, L.ffn_norm, (int)E, c.eps, T, img, ldk, s) || expand(E)) return -1;
+        if (K.gate.type == K.up.type && K.gate.rows == K.up.rows && K.gate.K == K.up.K && e->kq_dual &&
+            !(mfma_ok(K.gate) && mfma_ok(K.up))) {
             if (mv(K.gate, p.U, F, nullptr, nullptr, &K.up)) return -1;  // gelu(gate)*up
         } else if (mv(K.gate, p.G, F, nullptr, nullptr, nullptr) || mv(K.up, p.U, F, nullptr, p.G, nullptr)) {
             return -1;
         }
-        if (launch_quant_q8_K(p.U, F, F, T, img, ldk, s)) return -1;
+        if (launch_quant_q8_K(p.U, F, F, T, img, ldk, s) || expand(F)) return -1;
         if (mv(K.down, p.X, E, p.SA, nullptr, nullptr)) return -1;  // + sa
     }
     return 0;

@@ -326,8 +326,25 @@ int run_mul_mat(run_state &rs, ggml_tensor *node) {
         const int64_t nsb = K / 256;
         uint8_t *xq = (uint8_t *)scratch_take(rs, (size_t)(cols * nsb * 292));
         if (launch_quant_q8_K((const float *)dev_addr(rs, b), K, K, (int)cols, xq, nsb * 292, e.stream)) return -1;
+        // >= kq_gemm_min() (default 8) columns: the MFMA GEMM (prefill_kq.hip), as the C-ABI mul_mat
+        const uint8_t *wdev = (const uint8_t *)dev_addr(rs, a);
+        const int64_t rb_want = nsb * (a->type == GGML_TYPE_Q4_K ? 144 : 210);
+        if (cols >= kq_gemm_min() && (int64_t)a->nb[1] == rb_want &&
+            ((uintptr_t)wdev & (a->type == GGML_TYPE_Q4_K ? 15 : 3)) == 0) {
+            q8kx_args x;
+            x.x = xq; x.x_col_stride = nsb * 292; x.nsb = (int)nsb; x.T = (int)cols;
+            x.xh = (uint16_t *)scratch_take(rs, (size_t)(cols * K * 2)); x.ldh = K;
+            x.xd = (float *)scratch_take(rs, (size_t)(cols * nsb * 4)); x.ldd = nsb;
+            x.xm = (uint16_t *)scratch_take(rs, (size_t)(cols * nsb * 32)); x.ldm = nsb;
+            if (launch_q8k_expand(x, e.stream)) return -1;
+            kqg_args g;
+            g.w = wdev; g.row_bytes = rb_want; g.rows = a->ne[1]; g.nsb = (int)nsb; g.T = (int)cols; g.tiled = 0;
+            g.xh = x.xh; g.ldh = x.ldh; g.xd = x.xd; g.ldd = x.ldd; g.xm = x.xm; g.ldm = x.ldm;
+            g.y = (float *)dev_addr(rs, node); g.ldy = a->ne[1];
+            return launch_gemm_kq(a->type, g, e.stream);
+        }
         kq_args k;
-        k.w = (const uint8_t *)dev_addr(rs, a);
+        k.w = wdev;
         k.row_bytes = (int64_t)a->nb[1];
         k.rows = a->ne[1];
         k.nsb = (int)nsb;

@@ -146,6 +146,49 @@ int launch_embed_q6K(const uint8_t *embd, int64_t row_bytes, const int *tokens, 
 // synthetic Q4_K / Q6_K rows: oracle orc_synth_kquant(seed) with d (and dmin) rescaled by f
 int launch_synth_kquant(int wtype, uint8_t *out, int64_t rows, int64_t K, uint64_t seed, float f, hipStream_t s);
 
+// ---- K-quant prefill GEMM (prefill_kq.hip) -------------------------------------------------------
+// T Q8_K columns -> the operand image of k_gemm_kq: xh f16 [T][ldh] with each super-block's 256
+// values in AVX2-lane-major order (position 32l + 4c + k holds value 32c + 4l + k), xd f32 [T][ldd]
+// (the super-block's d), xm [T][ldm][16] f16 (Q4_K mins operand: per k = 0..3 the pair sums
+// S0 = bs[4k]+bs[4k+1], S1 = bs[4k+2]+bs[4k+3] as S & 63, S1 & 63, S0 >> 6, S1 >> 6)
+struct q8kx_args {
+    const uint8_t *x = nullptr;
+    int64_t x_col_stride = 0;
+    int nsb = 0, T = 0;
+    uint16_t *xh = nullptr;
+    int64_t ldh = 0;
+    float *xd = nullptr;
+    int64_t ldd = 0;
+    uint16_t *xm = nullptr;
+    int64_t ldm = 0;
+};
+int launch_q8k_expand(const q8kx_args &a, hipStream_t s);
+// y[t][r] = vec_dot_{q4_K,q6_K}_q8_K(row r, column t) for all T columns, ggml AVX2 lane order, on
+// v_mfma_f32_32x32x16_f16
+struct kqg_args {
+    const uint8_t *w = nullptr;
+    int64_t row_bytes = 0, rows = 0;
+    int nsb = 0, T = 0;
+    int tiled = 1;  // w in launch_kq_retile's layout (Q6_K: K % 2048 == 0), else ggml's row-major blocks
+    const uint16_t *xh = nullptr;
+    int64_t ldh = 0;
+    const float *xd = nullptr;
+    int64_t ldd = 0;
+    const uint16_t *xm = nullptr;
+    int64_t ldm = 0;
+    float *y = nullptr;
+    int64_t ldy = 0;
+    // epilogue as kq_args: y = v + resid, or y = gelu(gate_in) * v
+    const float *resid = nullptr, *gate_in = nullptr;
+    const uint16_t *gelu_tab = nullptr;
+    int gelu_clamp = 0;
+};
+int launch_gemm_kq(int wtype, const kqg_args &a, hipStream_t s);
+// the column count from which K-quant mul_mats (C-ABI, graph executor, engine prefill) take
+// launch_gemm_kq: GHIP_KQ_MFMA_MIN (default 8; GHIP_KQ_MFMA=0 disables), or hpc_set_kq_gemm_min
+int kq_gemm_min();
+void set_kq_gemm_min(int v);
+
 // ---- prefill (prefill.hip) ----------------------------------------------------------------------
 enum qrow_mode { QR_F32 = 0, QR_NORM = 1, QR_EMBED_NORM = 2, QR_GELU = 3 };
 struct qrow_args {  // T rows of K floats -> Q8_0 image q [T][ldq] int8 + da [T][ldd] (f32 of fp16 d)

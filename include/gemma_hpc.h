@@ -47,6 +47,9 @@ int hpc_weight_cache_entries(void);
 int hpc_unregister_weight(const void *host); /* drop the cached device copies of `host`; returns the count */
 void hpc_flush_weights(void);                /* drop every cached device weight                          */
 void hpc_set_matvec_ks(int ks);          /* K-split of the quantized matvec (1/2/4/8; tests) */
+/* columns from which K-quant mul_mats (and the K-quant engine prefill) run the MFMA GEMM
+ * (prefill_kq.hip) instead of the dot4 kernels; -1 = GHIP_KQ_MFMA_MIN or 8 (tests: same bytes) */
+void hpc_set_kq_gemm_min(int min_cols);
 
 /* ---- graph executor (SURVEY §8(b) `hpc_graph_compute(ggml_cgraph*)`): runs a graph built with the
  * ggml surface of include/ggml.h on the GPU; 0 = ok, else hpc_last_error() tells */

@@ -141,7 +141,7 @@ def _prefill_compare(e, m, shape, n_prompt, n_decode):
 
 
 @gpu
-@pytest.mark.parametrize("n_prompt", [1, 7, 33, 64])
+@pytest.mark.parametrize("n_prompt", [1, 7, 33, 64, 100])
 def test_kquant_engine_batched_prefill_matches_oracle(n_prompt):
     # every prompt row's logits of the batched K-quant prefill (all T columns per launch) equal the
     # CPU path's, and decode continues bit-exactly from its KV cache
@@ -153,11 +153,18 @@ def test_kquant_engine_batched_prefill_matches_oracle(n_prompt):
 
 
 @gpu
-def test_kquant_engine_batched_prefill_gemma2b_layer_shapes():
+@pytest.mark.parametrize("mfma", [1, 0])
+def test_kquant_engine_batched_prefill_gemma2b_layer_shapes(mfma):
+    # mfma = 1: the lane-tiled Q4_K / Q6_K matrices through the MFMA GEMM (prefill_kq.hip), = 0: the
+    # dot4 T-column kernel
     shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
     m = O.Model(O.make_config(shape, n_ctx=256, kmix=1))
     e = G.Engine(shape, n_ctx=256, wtype=G.GGML_TYPE_Q4_K)
-    _prefill_compare(e, m, shape, 40, 2)
+    G.lib().hpc_set_kq_gemm_min(-1 if mfma else 1 << 30)
+    try:
+        _prefill_compare(e, m, shape, 40, 2)
+    finally:
+        G.lib().hpc_set_kq_gemm_min(-1)
     e.close()
     m.close()
 

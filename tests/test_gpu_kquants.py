@@ -15,7 +15,10 @@ gpu = pytest.mark.gpu
                                           (1000, 4096, 1),
                                           # >= 4 columns: the T-column kernel (4 columns share each
                                           # weight load), ragged column tails, > 64 KiB of LDS
-                                          (72, 2048, 4), (300, 4096, 7), (64, 16384, 9)])
+                                          (72, 2048, 4), (300, 4096, 7), (64, 16384, 9),
+                                          # >= 8 columns: the MFMA GEMM (prefill_kq.hip) on ggml's
+                                          # row-major blocks; ragged row / column tiles
+                                          (100, 2048, 8), (130, 4096, 65), (64, 16384, 33), (257, 256, 70)])
 def test_kquant_mul_mat_bit_exact(wtype, rows, K, ncols):
     import gemma_hip as G
     G.lib().hpc_set_error_mode(0)
@@ -40,3 +43,55 @@ def test_kquant_rejects_bad_k():
     wdata, rs = O.mul_mat_init(O.Q4_K, X)
     G.mul_mat(W, O.Q4_K, 8, W.shape[1], 200, wdata, rs, 1)
     assert "K-quant" in G.last_error()
+
+
+def _extreme_blocks(wtype, W, K):
+    """Overwrite rows of W (ggml row-major blocks) with the extreme super-blocks of the exactness
+    argument in prefill_kq.hip: Q6_K (q6 - 32) * scale = 4096 (the 2^24 lane-sum bound with
+    activations of -128), odd products just below it, and mixed signs; Q4_K all nibbles 15 with
+    six-bit scales and mins 63."""
+    W = W.copy()
+    nsb = K // 256
+    for r in range(W.shape[0]):
+        for sb in range(nsb):
+            if wtype == O.Q6_K:
+                b = W[r, sb * 210:(sb + 1) * 210]
+                kind = (r + sb) % 4
+                if kind == 0:    # q6 = 0 -> -32, scale -128: every product 4096
+                    b[:192] = 0
+                    b[192:208] = np.uint8(0x80)
+                elif kind == 1:  # q6 = 1 -> -31, scale -127: odd products 3937
+                    b[:128] = 0x11
+                    b[128:192] = 0
+                    b[192:208] = np.uint8(0x81)
+                elif kind == 2:  # q6 = 63 -> 31, scale 127
+                    b[:192] = 0xFF
+                    b[192:208] = 127
+                # kind 3: the random block stays
+            else:
+                b = W[r, sb * 144:(sb + 1) * 144]
+                if (r + sb) % 3 != 2:
+                    b[4:] = 0xFF  # scales, mins 63; nibbles 15
+    return W
+
+
+@gpu
+@pytest.mark.parametrize("wtype", [O.Q4_K, O.Q6_K], ids=["q4_K", "q6_K"])
+def test_kquant_mul_mat_extreme_blocks(wtype):
+    # lane sums at the f16/fp32 exactness bounds the MFMA GEMM relies on (and the dot4 matvec for
+    # fewer columns): columns of all-equal activations quantize to -128 everywhere
+    import gemma_hip as G
+    G.lib().hpc_set_error_mode(0)
+    rows, K = 96, 4096
+    W = _extreme_blocks(wtype, O.synth_kquant(wtype, 7, rows, K), K)
+    rng = np.random.default_rng(5)
+    for ncols in (3, 12):
+        X = rng.standard_normal((ncols, K)).astype(np.float32)
+        X[0] = 1.0
+        X[1] = -1.0
+        X[2, ::2] = 1.0
+        wdata, rs = O.mul_mat_init(wtype, X)
+        ref = O.mul_mat(W, wtype, rows, W.shape[1], K, wdata, rs, ncols)
+        got = G.mul_mat(W, wtype, rows, W.shape[1], K, wdata, rs, ncols)
+        bad = np.nonzero(got.view(np.uint32) != ref.view(np.uint32))
+        assert bad[0].size == 0, (ncols, bad[0][:5], bad[1][:5], np.abs(got - ref).max())
