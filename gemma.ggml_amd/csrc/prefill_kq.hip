@@ -99,8 +99,15 @@ __device__ __forceinline__ uint32_t gq_u32_a2(const uint8_t *p) {
 }
 
 // TL: the engine's lane-contiguous layout (launch_kq_retile); otherwise ggml's row-major blocks
+#ifndef GHIP_GQ_WPE
+#define GHIP_GQ_WPE 0  // > 0: amdgpu_waves_per_eu (VGPR cap) for the GEMM
+#endif
 template <int WT, int EPI, bool TL>
-__global__ void __launch_bounds__(GQ_NT) k_gemm_kq(kqg_args a) {
+__global__ void __launch_bounds__(GQ_NT)
+#if GHIP_GQ_WPE
+__attribute__((amdgpu_waves_per_eu(GHIP_GQ_WPE, GHIP_GQ_WPE)))
+#endif
+k_gemm_kq(kqg_args a) {
     constexpr bool Q4 = WT == T_Q4_K;
     constexpr int M = gq_tile<WT>::M, N = gq_tile<WT>::N, NT = GQ_NT, WR = M / 16;
     constexpr int WREC = M * 8 / NT;         // (row, lane) weight records per thread

@@ -10,22 +10,33 @@ import json
 import sys
 
 root, out = sys.argv[1], sys.argv[2]
-agg = collections.defaultdict(float)
+KERNELS = {
+    "k_gemm_x": "exact Q4_0 prefill GEMMs (all 18 layers + logits, one T=2048 pass); MFMA util counts ISSUED "
+                "MFMA cycles: the lane-masked f16 MFMAs carry 4x the useful products (DESIGN.md §5b)",
+    "k_attn_rows": "exact prefill attention (per row, v_fma_mix chains; no MFMA by construction)",
+    "k_gemm_kq": "exact K-quant prefill GEMMs (Q4_K_M layout, dense lane-major MFMA; Q6_K issues 2 MFMAs per "
+                 "product, the even part and the low bit; DESIGN.md §5c)",
+}
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(root + "/pmc*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "k_gemm_x" in r["Kernel_Name"]:
-            agg[r["Counter_Name"]] += float(r["Counter_Value"])
-cyc = agg["GRBM_GUI_ACTIVE"] / 8.0
-res = {
-    "kernel": "k_gemm_x (exact prefill GEMMs, all 18 layers + logits, one T=2048 pass)",
-    "mfma_util": round(agg["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024), 4),
-    "lds_busy": round(agg["SQ_LDS_IDX_ACTIVE"] / (cyc * 256), 4),
-    "lds_bank_conflict_frac": round(agg["SQ_LDS_BANK_CONFLICT"] / agg["SQ_LDS_IDX_ACTIVE"], 4),
-    "valu_inst_per_wave_cycle": round(agg["SQ_ACTIVE_INST_VALU"] / agg["SQ_WAVE_CYCLES"], 4),
-    "wait_any_frac": round(agg["SQ_WAIT_ANY"] / agg["SQ_WAVE_CYCLES"], 4),
-    "raw": {k: v for k, v in sorted(agg.items())},
-    "note": "MFMA util counts ISSUED MFMA cycles: the exact path's lane-masked f16 MFMAs carry 4x the useful "
-            "products (3/4 of each A row is zero, DESIGN.md §5b)",
-}
+        for k in KERNELS:
+            if k in r["Kernel_Name"]:
+                agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+res = {}
+for k, a in agg.items():
+    cyc = a["GRBM_GUI_ACTIVE"] / 8.0
+    e = {"kernel": k, "what": KERNELS[k]}
+    if cyc > 0:
+        e["mfma_util"] = round(a["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024), 4)
+        e["lds_busy"] = round(a["SQ_LDS_IDX_ACTIVE"] / (cyc * 256), 4)
+    if a["SQ_LDS_IDX_ACTIVE"] > 0:
+        e["lds_bank_conflict_frac"] = round(a["SQ_LDS_BANK_CONFLICT"] / a["SQ_LDS_IDX_ACTIVE"], 4)
+    if a["SQ_WAVE_CYCLES"] > 0:
+        e["valu_inst_per_wave_cycle"] = round(a["SQ_ACTIVE_INST_VALU"] / a["SQ_WAVE_CYCLES"], 4)
+        e["wait_any_frac"] = round(a["SQ_WAIT_ANY"] / a["SQ_WAVE_CYCLES"], 4)
+        e["wait_inst_lds_frac"] = round(a["SQ_WAIT_INST_LDS"] / a["SQ_WAVE_CYCLES"], 4)
+    e["raw"] = {c: v for c, v in sorted(a.items())}
+    res[k] = e
 json.dump(res, open(out, "w"), indent=1)
-print(json.dumps({k: v for k, v in res.items() if k != "raw"}))
+print(json.dumps({k: {x: y for x, y in v.items() if x != "raw"} for k, v in res.items()}, indent=1))
