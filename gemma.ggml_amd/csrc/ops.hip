@@ -527,7 +527,13 @@ __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
 // for all G heads, so every K / V row is loaded once per row and 8 steps share one round trip
 // (the head-major mapping of round 1 paid a round trip per 256/G positions).  Rows are issued
 // longest first.  q16 / caches come from k_rope_kv_prefill (same RoPE/f16 arithmetic).
-constexpr int AR_THREADS = 1024;
+#ifndef GHIP_AR_THREADS
+#define GHIP_AR_THREADS 512
+#endif
+// 512 threads and P16 written over S in place (LDS G*n_kv*4 + G*hd*2 B): two row workgroups per CU,
+// so one's loads overlap the other's fma chains (1024 threads, separate P16: one per CU)
+constexpr int AR_THREADS = GHIP_AR_THREADS;
+constexpr bool AR_ALIAS = AR_THREADS <= 512;
 
 __global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -535,8 +541,11 @@ __global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
     const int G = a.H / a.Hkv, hd = a.hd, kvw = a.Hkv * hd, nkp = a.n_kv;
     const int kvh = blockIdx.x % a.Hkv, i = a.T - 1 - (int)(blockIdx.x / a.Hkv);
     float *S = (float *)smem;                      // [G][nkp]
-    uint16_t *P16 = (uint16_t *)(S + (size_t)G * nkp);  // [G][nkp]
-    uint16_t *Q16 = P16 + (size_t)G * nkp;              // [G][hd]: this row's q of the G heads
+    // P16 row gg: over S row gg (in place: the softmax's last pass reads S[j] before any lane of the
+    // wave writes P16[j], which lies inside S[j/2], already read) or after S
+    uint16_t *P16 = AR_ALIAS ? (uint16_t *)S : (uint16_t *)(S + (size_t)G * nkp);
+    const int p16s = AR_ALIAS ? 2 * nkp : nkp;     // P16 row stride (halfs)
+    uint16_t *Q16 = (uint16_t *)(S + (size_t)G * nkp) + (AR_ALIAS ? 0 : (size_t)G * nkp);  // [G][hd]
     int n_kv = 32 * ((i + 1) / 32 + 1);
     if (n_kv > nkp) n_kv = nkp;
     for (int k = tid; k < G * hd / 8; k += AR_THREADS) {
@@ -586,7 +595,7 @@ __global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
         for (int j = lane; j < n_kv; j += 64) {
             const float w = Sr[j];
             const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
-            P16[gg * nkp + j] = (uint16_t)f2h(e * inv);
+            P16[gg * p16s + j] = (uint16_t)f2h(e * inv);
         }
     }
     __syncthreads();
@@ -610,7 +619,7 @@ __global__ void __launch_bounds__(AR_THREADS) k_attn_rows(attnp_args a) {
 #pragma unroll
                 for (int gg = 0; gg < 8; ++gg) {
                     if (gg >= G) break;
-                    f16_step8(acc[gg], vv[u], *(const uint4 *)(P16 + gg * nkp + st0 + 32 * u + t4 * 8));
+                    f16_step8(acc[gg], vv[u], *(const uint4 *)(P16 + gg * p16s + st0 + 32 * u + t4 * 8));
                 }
             }
         }
@@ -840,7 +849,7 @@ attn_geom attn_geometry(int H, int Hkv, int hd, int ctx) {
 
 int launch_attn_rows(const attnp_args &a, hipStream_t s) {
     const int G = a.Hkv > 0 ? a.H / a.Hkv : 0;
-    const size_t lds = (size_t)G * a.n_kv * 6 + (size_t)G * a.hd * 2;
+    const size_t lds = (size_t)G * a.n_kv * (AR_ALIAS ? 4 : 6) + (size_t)G * a.hd * 2;
     if (G <= 0 || G > 8 || a.H % a.Hkv || (AR_THREADS / 4) % G || a.hd % 32 || a.hd > 256 || a.ctx % 32 || a.n_kv % 32 ||
         a.n_kv > a.ctx || a.T <= 0 || a.T > a.n_kv || lds > 160 * 1024) {
         set_error("attn_rows: unsupported shape (head_dim <= 256, G <= 8, 256 % G == 0, G*(n_kv*6 + hd*2) B of LDS <= 160 KiB)");

@@ -8,7 +8,8 @@
 // chunk c, times the chunk's integer scale), converts it to fp32 and chains
 // acc_l = fmaf(y.d*f16(x.d), (float)isum_l, acc_l) over super-blocks; Q4_K adds the mins lanes
 // accm_k = fmaf(-y.d*f16(x.dmin), (float)(mn·S)_k, accm_k).  isum_l is an integer dot product of
-// length 32 whose terms are exact in f16 (Q4_K: nibble*scale <= 945; Q6_K: (q6-32)*scale split into
+// length 32 whose terms are exact in f16 (Q4_K: nibble*scale <= 945, whose integer bits are the f16
+// denormal (nibble*scale) * 2^-24, the 2^24 folded into the row's d; Q6_K: (q6-32)*scale split into
 // an even part |.| <= 4096 and its low bit), and every partial sum stays below 2^24 — so an f16
 // MFMA with fp32 accumulation returns isum_l EXACTLY, as the float ggml converts it to.  Ordering K
 // lane-major (the 32 values of lane l are K = 0..31) makes that a DENSE GEMM per lane: for each
@@ -99,6 +100,9 @@ __device__ __forceinline__ uint32_t gq_u32_a2(const uint8_t *p) {
 }
 
 // TL: the engine's lane-contiguous layout (launch_kq_retile); otherwise ggml's row-major blocks
+#ifndef GHIP_GQ_DEN
+#define GHIP_GQ_DEN 1  // Q4_K A operand as f16 denormals (T = 2048 Q4_K_M prefill 57.25 -> 55.8 ms; 0: biased normals)
+#endif
 #ifndef GHIP_GQ_WPE
 #define GHIP_GQ_WPE 0  // > 0: amdgpu_waves_per_eu (VGPR cap) for the GEMM
 #endif
@@ -210,10 +214,19 @@ k_gemm_kq(kqg_args a) {
                     const uint32_t sl = (scw >> (16 * (j & 1))) & 0xFFu, sh = (scw >> (16 * (j & 1) + 8)) & 0xFFu;
                     const uint32_t qd = wraw[k].q[j];
                     const uint32_t lo = qd & 0x0F0F0F0Fu, hi = (qd >> 4) & 0x0F0F0F0Fu;
+#if GHIP_GQ_DEN
+                    // the products' integer bits ARE f16 denormals v * 2^-24 (v < 1024): no conversion;
+                    // the 2^24 goes into the row's d (exact power-of-two scaling)
+                    const uint4 f = make_uint4(__umul24(__builtin_amdgcn_perm(0u, lo, 0x0c010c00u), sl),
+                                               __umul24(__builtin_amdgcn_perm(0u, lo, 0x0c030c02u), sl),
+                                               __umul24(__builtin_amdgcn_perm(0u, hi, 0x0c010c00u), sh),
+                                               __umul24(__builtin_amdgcn_perm(0u, hi, 0x0c030c02u), sh));
+#else
                     const uint4 f = make_uint4(pair_f16(__umul24(__builtin_amdgcn_perm(0u, lo, 0x0c010c00u), sl), 0x64006400u),
                                                pair_f16(__umul24(__builtin_amdgcn_perm(0u, lo, 0x0c030c02u), sl), 0x64006400u),
                                                pair_f16(__umul24(__builtin_amdgcn_perm(0u, hi, 0x0c010c00u), sh), 0x64006400u),
                                                pair_f16(__umul24(__builtin_amdgcn_perm(0u, hi, 0x0c030c02u), sh), 0x64006400u));
+#endif
                     *(uint4 *)(WA + ((4 * l + j) * M + (row ^ l)) * 16) = f;
                 }
                 if (l < 4) {  // mins A fragment (row, k = l): [mn_2k, mn_2k+1, 64 mn_2k, 64 mn_2k+1] at K 4k..
@@ -223,7 +236,7 @@ k_gemm_kq(kqg_args a) {
                     const uint32_t v1 = i2h(64 * (int)mn0) | (i2h(64 * (int)mn1) << 16);
                     MA[row * 4 + l] = make_uint2(v0, v1);
                 } else if (l == 4) {
-                    DW[row] = h2f(wraw[k].h.x);
+                    DW[row] = GHIP_GQ_DEN ? h2f(wraw[k].h.x) * 16777216.0f : h2f(wraw[k].h.x);
                     DM[row] = h2f(wraw[k].h.x >> 16);
                 }
             } else {
