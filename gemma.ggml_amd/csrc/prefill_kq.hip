@@ -37,6 +37,8 @@ namespace {
 
 typedef _Float16 gh8 __attribute__((ext_vector_type(8)));
 typedef _Float16 gh4 __attribute__((ext_vector_type(4)));
+typedef _Float16 gh2 __attribute__((ext_vector_type(2)));
+typedef short gs2 __attribute__((ext_vector_type(2)));
 typedef float gf4 __attribute__((ext_vector_type(4)));
 typedef uint32_t gu4 __attribute__((ext_vector_type(4)));
 
@@ -258,15 +260,14 @@ k_gemm_kq(kqg_args a) {
 #pragma unroll
                         for (int cc = 0; cc < 2; ++cc) {
                             const int ip = 2 * gg + cc, bi = 8 * u + 2 * ip + (l >> 2);
-                            const int sc = (int)(int8_t)(uint8_t)(scd[bi >> 2] >> (8 * (bi & 3)));
-                            int A[4];
+                            const short sc = (short)(int8_t)(uint8_t)(scd[bi >> 2] >> (8 * (bi & 3)));
 #pragma unroll
-                            for (int kk = 0; kk < 4; ++kk) A[kk] = ((int)((q6[ip] >> (8 * kk)) & 0xFFu) - 32) * sc;
-#pragma unroll
-                            for (int p = 0; p < 2; ++p) {
-                                const int x0 = A[2 * p], x1 = A[2 * p + 1];
-                                fe[2 * cc + p] = i2h(x0 & ~1) | (i2h(x1 & ~1) << 16);
-                                fo[2 * cc + p] = __umul24((uint32_t)(x0 & 1) | ((uint32_t)(x1 & 1) << 16), 0x3C00u);
+                            for (int p = 0; p < 2; ++p) {  // values 2p, 2p+1 as an int16 pair: (q6 - 32) * scale
+                                const gs2 q = __builtin_bit_cast(gs2, __builtin_amdgcn_perm(0u, q6[ip], p ? 0x0c030c02u : 0x0c010c00u));
+                                const gs2 A = (q - (gs2){32, 32}) * (gs2){sc, sc};  // |A| <= 4096: exact in int16
+                                const gs2 ev = A & (gs2){(short)0xFFFE, (short)0xFFFE};
+                                fe[2 * cc + p] = __builtin_bit_cast(uint32_t, __builtin_convertvector(ev, gh2));
+                                fo[2 * cc + p] = __umul24(__builtin_bit_cast(uint32_t, A) & 0x00010001u, 0x3C00u);
                             }
                         }
                         const int off = ((4 * l + 2 * u + gg) * M + (row ^ l)) * 16;
