@@ -703,6 +703,9 @@ __device__ __forceinline__ float carry_chain(const void *st_s, const float *st_d
 #ifndef GHIP_UPRE
 #define GHIP_UPRE 4
 #endif
+#ifndef GHIP_SCL
+#define GHIP_SCL 1  // gate/up scales as one 1 KiB run per row tile and matrix (k_matvec SCL)
+#endif
 // ONE_SHOT: every wave's items fit the register ring (n_items <= U): no refills in the stream loop
 template <int WT, int KS, int PRO, int EPI, int U, int R, bool NSA, bool ONE_SHOT>
 __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
@@ -738,9 +741,22 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
                                          : rt0 < a.n_rt ? (a.n_rt - rt0 + rstride - 1) / rstride : 0;
     const int64_t n_items = n_my_rt * NM * nbt;
 
+    // SCL (gate/up, every wave at most one row tile whose scale planes are 1 KiB each): the wave's
+    // gate and up scales come in with ONE 16-B load per lane per matrix (lane L: bytes 16L.. of the
+    // row tile's contiguous scale run) and are read per block tile from a per-wave LDS copy,
+    // instead of one 16-B load per (item, lane) that 8 lanes of a row issue redundantly
+    constexpr bool SCL = KS == 1 && NM == 2 && ONE_SHOT;
+    static_assert(!SCL || 8 * SB * (WT == T_Q4_0 ? 8 : 16) == 1024, "SCL: one 1 KiB scale run per row tile");
+
     // 0) this thread's activation values (older than the weight loads -> waited for by count)
     act_regs<R> ar;
     prefetch_activation<WT, PRO, R, NTH>(a, col, ar);
+    uint4 scl_g = make_uint4(0, 0, 0, 0), scl_u = scl_g;
+    if constexpr (SCL) {
+        const int64_t rts = n_items ? rt0 : 0;
+        scl_g = ld_nt16(a.sc + rts * 1024 + lane * 16);
+        scl_u = ld_nt16(a.sc2 + rts * 1024 + lane * 16);
+    }
 
     // 1) fill the register ring: the HBM round trip overlaps the prologue below.  Loads are
     //    never inside a runtime branch (hipcc would wait vmcnt(0) around them): past the last item
@@ -758,6 +774,9 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
         // weights are read once per token by one CU: non-temporal loads (MI355X_MICROARCH nt-weights:
         // issued -> landed -18 %, decode layer -5..10 %)
         qd = ld_nt16(qt + q_off);
+        if constexpr (SCL) {
+            (void)st; (void)sd;
+        } else {
 #if GHIP_NOSCALE  // timing only: no scale loads (wrong results)
         sd = make_uint4(0x3c003c00u, 0x3c003c00u, 0x3c003c00u, 0x3c003c00u);
         (void)st;
@@ -769,6 +788,7 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
             sd = make_uint4(v.x, v.y, 0, 0);
         }
 #endif
+        }
         ++issued;
         if (issued < n_items) {
             if (NM == 2) {  // gate and up of one block tile back to back (shared act operands)
@@ -800,6 +820,11 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
 #pragma unroll
     for (int u = UP; u < U; ++u) issue(qb[u], sb[u]);
     if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 2] = __builtin_amdgcn_s_memrealtime();
+    uint8_t *scl_w = smem + m.total + (size_t)wave * 2048;  // SCL: this wave's [gate | up] scale runs
+    if constexpr (SCL) {
+        *(uint4 *)(scl_w + lane * 16) = scl_g;
+        *(uint4 *)(scl_w + 1024 + lane * 16) = scl_u;
+    }
     __syncthreads();
     if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 3] = __builtin_amdgcn_s_memrealtime();
 
@@ -814,7 +839,7 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     int y_it = 0;  // row tiles this wave has finished (EPI_GELU_MUL image buffer slot)
     cursor cc{rt0, 0, 0};
     float acc = 0.0f, va = 0.0f;
-    const int64_t n_pad = ONE_SHOT ? U : (n_items + U - 1) / U * U;
+    const int64_t n_pad = ONE_SHOT && !SCL ? U : (n_items + U - 1) / U * U;
     if constexpr (NM == 2) {
         // (gate, up) item pairs of the same block tile; two ordered chains (acc: gate, acc2: up)
         static_assert(KS == 1 && U % 2 == 0, "gate/up pairing");
@@ -822,7 +847,19 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
         for (int64_t k = 0; k < n_pad; k += U) {
 #pragma unroll
             for (int u = 0; u < U; u += 2) {
-                const uint4 q0 = qb[u], s0 = sb[u], q1 = qb[u + 1], s1 = sb[u + 1];
+                const uint4 q0 = qb[u], q1 = qb[u + 1];
+                uint4 s0 = sb[u], s1 = sb[u + 1];
+                if constexpr (SCL) {  // block tile cc.bt, row rr: bytes (bt*8 + rr)*SB of each run
+                    const uint8_t *sp = scl_w + (cc.bt * 8 + rr) * SB;
+                    if constexpr (WT == T_Q4_0) {
+                        s0 = *(const uint4 *)sp;
+                        s1 = *(const uint4 *)(sp + 1024);
+                    } else {
+                        const uint2 g2 = *(const uint2 *)sp, u2 = *(const uint2 *)(sp + 1024);
+                        s0 = make_uint4(g2.x, g2.y, 0, 0);
+                        s1 = make_uint4(u2.x, u2.y, 0, 0);
+                    }
+                }
                 issue(qb[u], sb[u]);
                 issue(qb[u + 1], sb[u + 1]);
                 if (k + u < n_items) {
@@ -1115,13 +1152,25 @@ int launch_t(const mv_args &a, int grid_x, hipStream_t s) {
     la.rt_q = a.n_rt / rstride;
     la.rt_r = a.n_rt % rstride;
     la.ygroups = ygroups;
-    const void *fn = one_shot ? (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1>
-                              : (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>;
-    if (m.total > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m.total));
-    if (one_shot)
-        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, la);
+    // gate/up (KS 1): ONE_SHOT selects the SCL scale-run form (k_matvec) when every wave has at most
+    // one row tile and a row tile's scales are one 1 KiB run per matrix; + 2 KiB of LDS per wave
+    static const int scl_env = getenv("GHIP_SCL") ? atoi(getenv("GHIP_SCL")) : GHIP_SCL;  // A/B switch
+    const bool scl = KS == 1 && EPI == EPI_GELU_MUL && scl_env && a.n_bt * 8 * wfmt<WT>::SCALE_BYTES == 1024 &&
+                     waves_x >= a.n_rt;
+    const bool os = one_shot || scl;
+    const size_t lds = m.total + (scl ? (size_t)(threads / 64) * 2048 : 0);
+    if (lds > 160 * 1024) {
+        set_error("matvec: LDS image too large");
+        return -1;
+    }
+    const void *fn = os ? (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1 || EPI == EPI_GELU_MUL>
+                        : (const void *)k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>;
+    if (lds > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (os)
+        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, KS != 1 || EPI == EPI_GELU_MUL>), dim3(grid_x, a.ncols),
+                           dim3(threads), lds, s, la);
     else
-        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>), dim3(grid_x, a.ncols), dim3(threads), m.total, s, la);
+        hipLaunchKernelGGL((k_matvec<WT, KS, PRO, EPI, U, R, NSA, false>), dim3(grid_x, a.ncols), dim3(threads), lds, s, la);
     GHIP_CHECK(hipGetLastError());
     return 0;
 }
