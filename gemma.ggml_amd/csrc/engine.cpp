@@ -2341,11 +2341,17 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
     const double t1 = prof ? us() : 0.0;
     // logits through a pinned staging row (a pageable device-to-host copy stages through the driver)
     const size_t lb = (size_t)c.n_vocab * 4;
-    if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, lb, hipHostMallocDefault));
-    GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
-    GHIP_CHECK(hipStreamSynchronize(e->stream));
+    static const int direct = getenv("GHIP_EXT_DIRECT") ? atoi(getenv("GHIP_EXT_DIRECT")) : 0;
+    if (direct) {  // A/B: straight into the (pageable) graph tensor
+        GHIP_CHECK(hipMemcpyAsync(logits, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
+        GHIP_CHECK(hipStreamSynchronize(e->stream));
+    } else {
+        if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, lb, hipHostMallocDefault));
+        GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
+        GHIP_CHECK(hipStreamSynchronize(e->stream));
+    }
     const double t2 = prof ? us() : 0.0;
-    memcpy(logits, e->ext_stage, lb);
+    if (!direct) memcpy(logits, e->ext_stage, lb);
     if (prof) fprintf(stderr, "[gemma_hip] ext_decode: launch+run %.1f us, copy %.1f us, host copy %.1f us\n", t1 - t0, t2 - t1, us() - t2);
     e->host_pos = pos + 1;
     return 0;

@@ -74,9 +74,40 @@ int64_t blck_size(int t) {
     }
 }
 
+// tensor objects come from slabs of kSlab, kept in a process pool when their context is freed (the
+// reference re-creates its ~1,000-tensor compute context every token: one heap allocation per tensor
+// was a measurable part of the host's per-token time)
+constexpr size_t kSlab = 512;
+std::mutex slab_mu;
+std::vector<ggml_tensor *> slab_pool;
+ggml_tensor *slab_take(ggml_context *ctx) {
+    if (ctx->slabs.empty() || ctx->slab_used == kSlab) {
+        ggml_tensor *s = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(slab_mu);
+            if (!slab_pool.empty()) {
+                s = slab_pool.back();
+                slab_pool.pop_back();
+            }
+        }
+        if (!s) s = new ggml_tensor[kSlab];
+        ctx->slabs.push_back(s);
+        ctx->slab_used = 0;
+    }
+    return &ctx->slabs.back()[ctx->slab_used++];
+}
+void slab_put(std::vector<ggml_tensor *> &slabs) {
+    std::lock_guard<std::mutex> lk(slab_mu);
+    for (ggml_tensor *s : slabs) {
+        if (slab_pool.size() < 64) slab_pool.push_back(s);
+        else delete[] s;
+    }
+    slabs.clear();
+}
+
 ggml_tensor *new_tensor_impl(ggml_context *ctx, ggml_type type, int n_dims, const int64_t *ne, ggml_tensor *view_src,
                              size_t view_offs) {
-    ggml_tensor *t = new ggml_tensor();
+    ggml_tensor *t = slab_take(ctx);
     memset(t, 0, sizeof(*t));
     t->type = type;
     for (int i = 0; i < GGML_MAX_DIMS; ++i) t->ne[i] = i < n_dims ? ne[i] : 1;
@@ -473,6 +504,102 @@ bool match_norm(const ggml_tensor *t, const ggml_tensor **x, const float **w, fl
     return true;
 }
 
+// pointer set for match_gemma's ancestor walk: linear probing over a power-of-two table, cleared
+// by bumping a generation stamp (no per-insert allocation, no per-call clear of the table)
+struct ptr_set {
+    std::vector<const void *> key;
+    std::vector<uint32_t> gen;
+    uint32_t cur = 0;
+    size_t mask = 0, count = 0;
+    std::vector<const ggml_tensor *> stack;
+    void grow() {  // keep the load factor <= 1/2 (a table never fills, so probes always end)
+        std::vector<const void *> live;
+        for (size_t i = 0; i < key.size(); ++i)
+            if (gen[i] == cur) live.push_back(key[i]);
+        key.assign(key.size() * 2, nullptr);
+        gen.assign(key.size(), 0);
+        cur = 1;
+        mask = key.size() - 1;
+        count = 0;
+        for (const void *p : live) insert(p);
+    }
+    void reset(size_t n) {
+        count = 0;
+        size_t cap = 64;
+        while (cap < 2 * n) cap <<= 1;
+        if (cap > key.size()) {
+            key.assign(cap, nullptr);
+            gen.assign(cap, 0);
+            cur = 0;
+        }
+        mask = key.size() - 1;
+        if (++cur == 0) {  // wrapped: clear once
+            std::fill(gen.begin(), gen.end(), 0u);
+            cur = 1;
+        }
+    }
+    static size_t hash(const void *p) {
+        uint64_t x = (uint64_t)(uintptr_t)p;
+        x ^= x >> 29;
+        x *= 0xbf58476d1ce4e5b9ull;
+        return (size_t)(x ^ (x >> 32));
+    }
+    bool insert(const void *p) {  // true if newly inserted
+        for (size_t i = hash(p) & mask;; i = (i + 1) & mask) {
+            if (gen[i] != cur) {
+                gen[i] = cur;
+                key[i] = p;
+                if (++count * 2 > key.size()) grow();
+                return true;
+            }
+            if (key[i] == p) return false;
+        }
+    }
+    bool has(const void *p) const {
+        for (size_t i = hash(p) & mask;; i = (i + 1) & mask) {
+            if (gen[i] != cur) return false;
+            if (key[i] == p) return true;
+        }
+    }
+};
+ptr_set &anc_set() {
+    static thread_local ptr_set s;
+    return s;
+}
+
+// graphs (node / leaf arrays + the visited set) pooled across contexts, like the tensor slabs
+std::mutex graph_mu;
+std::vector<ggml_cgraph *> graph_pool;
+ggml_cgraph *graph_take() {
+    ggml_cgraph *g = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(graph_mu);
+        if (!graph_pool.empty()) {
+            g = graph_pool.back();
+            graph_pool.pop_back();
+        }
+    }
+    if (!g) {
+        g = new ggml_cgraph();
+        g->nodes = new ggml_tensor *[kGraphSize];
+        g->leafs = new ggml_tensor *[kGraphSize];
+        g->visited = new ptr_set();
+    }
+    ((ptr_set *)g->visited)->reset(1024);
+    return g;
+}
+void graph_put(ggml_cgraph *g) {
+    std::lock_guard<std::mutex> lk(graph_mu);
+    if (graph_pool.size() < 8) {
+        graph_pool.push_back(g);
+        return;
+    }
+    delete (ptr_set *)g->visited;
+    delete[] g->nodes;
+    delete[] g->leafs;
+    delete g;
+}
+
 bool match_gemma(ggml_cgraph *g, gemma_match &m, std::string &why) {
     auto fail = [&](const char *w) {
         why = w;
@@ -627,18 +754,22 @@ bool match_gemma(ggml_cgraph *g, gemma_match &m, std::string &why) {
     if (last->ne[1] != m.T || !last->data || !is_contiguous(last)) return fail("output rows");
     // exactly that graph: every node is an ancestor of the logits or one of the matched cache
     // stores (an extra side node, e.g. a second output or another CPY, would be skipped otherwise)
-    std::unordered_set<const ggml_tensor *> seen(m.stores.begin(), m.stores.end());
-    std::vector<const ggml_tensor *> stack{last};
+    // (a flat open-addressing pointer set reused across calls: the per-token check allocates nothing)
+    ptr_set &anc = anc_set();
+    anc.reset(4 * (size_t)(g->n_nodes + g->n_leafs) + 64);
+    std::vector<const ggml_tensor *> &stack = anc.stack;
+    stack.clear();
+    stack.push_back(last);
     for (const ggml_tensor *st : m.stores) stack.push_back(st);
-    std::unordered_set<const ggml_tensor *> anc;
     while (!stack.empty()) {
         const ggml_tensor *t = stack.back();
         stack.pop_back();
-        if (!t || !anc.insert(t).second) continue;
-        for (int k = 0; k < GGML_MAX_SRC; ++k) stack.push_back(t->src[k]);
+        if (!t || !anc.insert(t)) continue;
+        for (int k = 0; k < GGML_MAX_SRC; ++k)
+            if (t->src[k]) stack.push_back(t->src[k]);
     }
     for (int i = 0; i < g->n_nodes; ++i)
-        if (!anc.count(g->nodes[i])) return fail("extra node");
+        if (!anc.has(g->nodes[i])) return fail("extra node");
     return true;
 }
 
@@ -801,9 +932,23 @@ struct ggml_context *ggml_init(struct ggml_init_params params) {
 
 void ggml_free(struct ggml_context *ctx) {
     if (!ctx) return;
+    // the address span of this context's data: the executor caches and the fast path's weights are
+    // checked tensor by tensor only when one of their keys falls inside it (the per-token compute
+    // context of the reference's loop never holds one, and hundreds of lookups per token are host time)
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    for (const ggml_tensor *t : ctx->tensors)
+        if (!t->view_src && t->data) {
+            lo = std::min(lo, (uintptr_t)t->data);
+            hi = std::max(hi, (uintptr_t)t->data + 1);
+        }
+    auto inside = [&](const void *p) { return (uintptr_t)p >= lo && (uintptr_t)p < hi; };
     {
         std::lock_guard<std::recursive_mutex> lk(ex().mu);
+        bool any = false;
+        for (const auto &kv : ex().leaves) any = any || inside(kv.first);
+        for (const auto &kv : ex().tiled) any = any || inside(kv.first.first);
         // a freed compute context's tensors leave the executor's caches keyed by their data
+        if (any)
         for (ggml_tensor *t : ctx->tensors) {
             if (t->view_src || !t->data) continue;
             auto it = ex().leaves.find(t->data);
@@ -820,7 +965,7 @@ void ggml_free(struct ggml_context *ctx) {
     }
     {  // a freed weight context takes the fast path's device copy of its weights with it
         fast_engine &f = fast();
-        if (f.e) {
+        if (f.e && std::any_of(f.weights.begin(), f.weights.end(), inside)) {
             const std::unordered_set<const void *> ws(f.weights.begin(), f.weights.end());
             for (ggml_tensor *t : ctx->tensors)
                 if (t->data && ws.count(t->data)) {
@@ -829,13 +974,8 @@ void ggml_free(struct ggml_context *ctx) {
                 }
         }
     }
-    for (ggml_tensor *t : ctx->tensors) delete t;
-    for (ggml_cgraph *g : ctx->graphs) {
-        delete (std::unordered_set<ggml_tensor *> *)g->visited;
-        delete[] g->nodes;
-        delete[] g->leafs;
-        delete g;
-    }
+    slab_put(ctx->slabs);
+    for (ggml_cgraph *g : ctx->graphs) graph_put(g);
     if (ctx->owns_mem) arena_put((ctx->mem_size + 63) & ~(size_t)63, ctx->mem);
     delete ctx;
 }
@@ -1041,20 +1181,16 @@ struct ggml_tensor *ggml_cpy(struct ggml_context *ctx, struct ggml_tensor *a, st
 
 // ---- graphs ------------------------------------------------------------------------------------
 struct ggml_cgraph *ggml_new_graph(struct ggml_context *ctx) {
-    ggml_cgraph *g = new ggml_cgraph();
+    ggml_cgraph *g = graph_take();
     g->size = kGraphSize;
-    g->nodes = new ggml_tensor *[kGraphSize];
-    g->leafs = new ggml_tensor *[kGraphSize];
     g->grads = nullptr;
     g->n_nodes = g->n_leafs = 0;
-    g->visited = new std::unordered_set<ggml_tensor *>();
     ctx->graphs.push_back(g);
     return g;
 }
 
-static void visit(ggml_cgraph *g, std::unordered_set<ggml_tensor *> &seen, ggml_tensor *t) {
-    if (!t || seen.count(t)) return;
-    seen.insert(t);
+static void visit(ggml_cgraph *g, ptr_set &seen, ggml_tensor *t) {
+    if (!t || !seen.insert(t)) return;
     for (int i = 0; i < GGML_MAX_SRC; ++i) visit(g, seen, t->src[i]);
     if (t->op == GGML_OP_NONE) {
         if (g->n_leafs < g->size) g->leafs[g->n_leafs++] = t;
@@ -1070,7 +1206,7 @@ static void visit(ggml_cgraph *g, std::unordered_set<ggml_tensor *> &seen, ggml_
 void ggml_build_forward_expand(struct ggml_cgraph *g, struct ggml_tensor *t) {
     // the graph keeps its visited set: rebuilding it from nodes + leafs on every call made the
     // reference's per-layer expands quadratic (~2.5 ms of host time per Gemma-2B decode graph)
-    visit(g, *(std::unordered_set<ggml_tensor *> *)g->visited, t);
+    visit(g, *(ptr_set *)g->visited, t);
 }
 
 enum ggml_status ggml_graph_compute_with_ctx(struct ggml_context *ctx, struct ggml_cgraph *g, int n_threads) {

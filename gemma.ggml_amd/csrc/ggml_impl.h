@@ -14,6 +14,8 @@ struct ggml_context {
     bool owns_mem = false, no_alloc = false;
     std::vector<ggml_tensor *> tensors;
     std::vector<ggml_cgraph *> graphs;
+    std::vector<ggml_tensor *> slabs;  // tensor objects (ggml_api.cpp slab_take), pooled on free
+    size_t slab_used = 0;
 };
 
 struct ggml_backend_buffer_type {
