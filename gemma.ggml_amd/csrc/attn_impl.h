@@ -330,6 +330,9 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     for (int s = 0; s < 8; ++s) qr[s] = *(const uint4 *)(q16 + (s * 32 < hd ? s * 32 : 0) + t4 * 8);
     for (int j0 = 0; j0 < n_kv; j0 += NTH / 4) {
         const int j = j0 + quad;
+        // a wave whose 16 positions all lie past n_kv has nothing to store: skip its dots (wave-
+        // uniform; its lmax stays -inf, below every stored score)
+        if (j0 + wave * 16 >= n_kv) continue;
         float acc[8];
 #pragma unroll
         for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
