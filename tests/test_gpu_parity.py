@@ -312,6 +312,18 @@ def test_gate_up_split_waves_bitexact(wtype, rpw, img):
 
 
 @gpu
+@pytest.mark.parametrize("wtype", [O.Q4_0, O.Q8_0])
+@pytest.mark.parametrize("rpw,img", [(1, 0), (1, 1), (2, 1)])
+def test_gate_up_scale_runs_bitexact(wtype, rpw, img):
+    """gate/up in one wave per row tile (plan k_split 1): at rows_per_wg 1 every wave owns one row
+    tile and its scales come as one 1 KiB run per matrix (k_matvec SCL form, Q4_0 8 and Q8_0 16
+    block tiles); at rows_per_wg 2 waves own two row tiles and the per-item scale loads run."""
+    shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
+    _check_decode_plan(shape, 9, 6, 128, wtype,
+                       lambda p: {"gate_up": (1, rpw, 0), "down": (p["down"][0], p["down"][1], img)})
+
+
+@gpu
 def test_gate_up_split_waves_tiny_multi_round():
     """several row tiles per wave pair (rounds > 1: the refill path)."""
     _check_decode_plan(O.TINY, 7, 10, 128, O.Q4_0, lambda p: {"gate_up": (2, 16, 0)})
