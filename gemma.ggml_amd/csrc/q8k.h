@@ -9,7 +9,43 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef GHIP_Q8K_DPP
+#define GHIP_Q8K_DPP 1
+#endif
+
 namespace ghip {
+
+// the (|x| max, first index) reduction's partner value at lane distance `off`: DPP within a row of
+// 16 lanes (xor 1, xor 2 by quad permutes; the 4- and 8-lane steps by the half-row / row mirrors,
+// which pair each group with its neighbour), ds_bpermute across rows.  The reduction (max, ties to
+// the smaller index) is order-independent, so any pairing gives the same result in every lane.
+template <int OFF>
+__device__ __forceinline__ uint32_t q8k_partner(uint32_t v) {
+    if constexpr (OFF == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+    else if constexpr (OFF == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    else if constexpr (OFF == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
+    else if constexpr (OFF == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false); // row_mirror
+    else return (uint32_t)__shfl_xor((int)v, OFF);
+}
+template <int OFF>
+__device__ __forceinline__ void q8k_amax_level(float &amax, float &mx, int &idx) {
+    const float oa = __builtin_bit_cast(float, q8k_partner<OFF>(__builtin_bit_cast(uint32_t, amax)));
+    const float om = __builtin_bit_cast(float, q8k_partner<OFF>(__builtin_bit_cast(uint32_t, mx)));
+    const int oi = (int)q8k_partner<OFF>((uint32_t)idx);
+    if (oa > amax || (oa == amax && oi < idx)) {
+        amax = oa;
+        mx = om;
+        idx = oi;
+    }
+}
+__device__ __forceinline__ void q8k_amax_reduce(float &amax, float &mx, int &idx) {
+    q8k_amax_level<1>(amax, mx, idx);
+    q8k_amax_level<2>(amax, mx, idx);
+    q8k_amax_level<4>(amax, mx, idx);
+    q8k_amax_level<8>(amax, mx, idx);
+    q8k_amax_level<16>(amax, mx, idx);
+    q8k_amax_level<32>(amax, mx, idx);
+}
 
 __device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *blk) {
     float amax = 0.0f, mx = 0.0f;
@@ -23,6 +59,9 @@ __device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *
             idx = lane * 4 + j;
         }
     }
+#if GHIP_Q8K_DPP
+    q8k_amax_reduce(amax, mx, idx);
+#else
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         const float oa = __shfl_xor(amax, off), om = __shfl_xor(mx, off);
@@ -33,6 +72,7 @@ __device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *
             idx = oi;
         }
     }
+#endif
     int q[4] = {0, 0, 0, 0};
     float d = 0.0f;
     if (amax != 0.0f) {
@@ -70,6 +110,10 @@ __device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, u
             }
         }
     }
+#if GHIP_Q8K_DPP
+#pragma unroll
+    for (int k = 0; k < N; ++k) q8k_amax_reduce(amax[k], mx[k], idx[k]);
+#else
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         float oa[N], om[N];
@@ -89,6 +133,7 @@ __device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, u
             }
         }
     }
+#endif
     int bs[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
