@@ -82,8 +82,8 @@ __device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *
         d = (float)(1.0 / (double)iscale);
     }
     int bs = q[0] + q[1] + q[2] + q[3];
-    bs += __shfl_xor(bs, 1);
-    bs += __shfl_xor(bs, 2);
+    bs += (int)q8k_partner<1>((uint32_t)bs);  // sums of 16 (4 lanes): exact integer adds
+    bs += (int)q8k_partner<2>((uint32_t)bs);
     *(uint32_t *)(blk + 4 + lane * 4) =
         (uint32_t)(q[0] & 255) | ((uint32_t)(q[1] & 255) << 8) | ((uint32_t)(q[2] & 255) << 16) | ((uint32_t)q[3] << 24);
     if ((lane & 3) == 0) *(int16_t *)(blk + 260 + (lane >> 2) * 2) = (int16_t)bs;
@@ -152,9 +152,9 @@ __device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, u
         if (lane == 0) *(float *)b = d;
     }
 #pragma unroll
-    for (int k = 0; k < N; ++k) bs[k] += __shfl_xor(bs[k], 1);
+    for (int k = 0; k < N; ++k) bs[k] += (int)q8k_partner<1>((uint32_t)bs[k]);
 #pragma unroll
-    for (int k = 0; k < N; ++k) bs[k] += __shfl_xor(bs[k], 2);
+    for (int k = 0; k < N; ++k) bs[k] += (int)q8k_partner<2>((uint32_t)bs[k]);
 #pragma unroll
     for (int k = 0; k < N; ++k)
         if ((lane & 3) == 0) *(int16_t *)(blk + k * stride + 260 + (lane >> 2) * 2) = (int16_t)bs[k];

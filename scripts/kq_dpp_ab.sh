@@ -4,9 +4,9 @@
 set -o pipefail
 mkdir -p gpurun_out/dpp
 export TMPDIR=/tmp
-GHIP_LIB=$PWD/ab_libs/libdpp.so timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_engine_gguf.py tests/test_gpu_kquants.py tests/test_gpu_ggml_kquant_ops.py tests/test_gpu_ops.py > gpurun_out/dpp/test.log 2>&1 || { tail -30 gpurun_out/dpp/test.log; exit 1; }
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_engine_gguf.py tests/test_gpu_kquants.py tests/test_gpu_ggml_kquant_ops.py tests/test_gpu_ops.py > gpurun_out/dpp/test.log 2>&1 || { tail -30 gpurun_out/dpp/test.log; exit 1; }
 tail -1 gpurun_out/dpp/test.log
 for rep in 1 2 3; do
-  echo -n "base "; timeout -k 10 120 python -u scripts/run_kqm.py 64 2>&1 | tail -1 || exit 1
-  echo -n "dpp  "; GHIP_LIB=$PWD/ab_libs/libdpp.so timeout -k 10 120 python -u scripts/run_kqm.py 64 2>&1 | tail -1 || exit 1
+  echo -n "base "; GHIP_LIB=$PWD/ab_libs/libbase.so timeout -k 10 120 python -u scripts/run_kqm.py 64 2>&1 | tail -1 || exit 1
+  echo -n "new  "; timeout -k 10 120 python -u scripts/run_kqm.py 64 2>&1 | tail -1 || exit 1
 done
