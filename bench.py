@@ -58,22 +58,53 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(n_prompt=128, n_decode=48, threads=4, q8_decode=24):
+def _pick_cpus(n):
+    """n CPUs of this process's affinity set, one per physical core (SMT siblings skipped), lowest
+    ids first: the CPU legs run pinned so that repeated runs see the same cores."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return None
+    picked, seen = [], set()
+    for c in allowed:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                sib = f.read().strip()
+        except OSError:
+            sib = str(c)
+        if sib in seen:
+            continue
+        seen.add(sib)
+        picked.append(c)
+        if len(picked) == n:
+            return picked
+    for c in allowed:  # fewer physical cores than n: SMT siblings too (never fewer CPUs than threads)
+        if len(picked) == n:
+            break
+        if c not in picked:
+            picked.append(c)
+    return sorted(picked)
+
+
+def cpu_baseline(n_prompt=128, n_decode=32, threads=4, q8_decode=16, reps=3):
     """Oracle (CPU restatement of the reference CPU + thread_pool path) on the host cores, BASELINE.md §2.
 
     Config 1: Gemma-2B Q4_0 synthetic weights, the 128-token synthetic prompt (seed 1) as ONE prefill
     graph (logits for every row, as src/gemma_model.cpp:740 computes them), then n_decode greedy
     DECODE steps (bounded sample of the 128 of config 1: each step's cost is flat in this range).
-    Timed with std::chrono like src/gemma_model.cpp:552-572.  Runs (other ops always on one thread,
-    src/macro.h:20):
-      ref_pool x4   mul_mat on the reference's 4-worker task pool (src/macro.h:21)  -> "value"
+    Timed with std::chrono like src/gemma_model.cpp:552-572.  Every leg runs pinned
+    (os.sched_setaffinity before its pool's threads start) to one CPU per physical core.  Runs (other
+    ops always on one thread, src/macro.h:20):
+      ref_pool x4   mul_mat on the reference's 4-worker task pool (src/macro.h:21), `reps` times:
+                    "value" is the MEDIAN, "spread" = (max - min) / median
       ref_pool xN   the same pool with every core this process may use (nproc, capped by the box's share)
       spin_pool xN  the same row split on a spin fork-join pool (oracle/hpc_cpu.cpp spin_pool; NOT the
                     reference's pool, the "fixed" figure)
     and the Q8_0 weights (config 5) on ref_pool x4 and spin_pool xN.  Each run carries the decode
     steps' mul_mat profile: wall time, the slowest share's compute time, and the rest ("pool_s": the
     wake/hand-off latency of the pool; 415 mul_mat calls per token, 288 of them tiny per-head
-    attention products)."""
+    attention products).  Configs 3 and 4 on the CPU are bounded samples (cpu_prefill_2048 and
+    cpu_decode_7b below), extrapolated from a 1- or 2-layer model with a 16,000-row output."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes as C
     import numpy as np
@@ -81,22 +112,32 @@ def cpu_baseline(n_prompt=128, n_decode=48, threads=4, q8_decode=24):
     nproc = os.cpu_count() or 1
     try:
         allowed = len(os.sched_getaffinity(0))
+        saved_aff = os.sched_getaffinity(0)
     except AttributeError:
-        allowed = nproc
+        allowed, saved_aff = nproc, None
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or allowed
     all_threads = max(1, min(allowed, share))
     L = O.lib()
     prompt = np.array(make_prompt(n_prompt, GEMMA_2B["n_vocab"]), dtype=np.int32)
 
-    def run(m, pool, th, nd):
-        toks = np.zeros(n_prompt + nd + 2, dtype=np.int32)
+    def pin(th):
+        cpus = _pick_cpus(th)
+        if cpus and saved_aff is not None:
+            os.sched_setaffinity(0, cpus)  # the pool's threads start after this and inherit it
+        return cpus
+
+    def run(m, pool, th, nd, prm=prompt, n_pr=n_prompt):
+        cpus = pin(th)
+        toks = np.zeros(n_pr + nd + 2, dtype=np.int32)
         pre = C.c_double()
         prof = np.zeros(6)
         L.orc_set_pool(pool)
-        dec_s = L.orc_bench_run(m.h, O.ptr(prompt), n_prompt, nd, th, O.ptr(toks), C.byref(pre), O.ptr(prof))
+        dec_s = L.orc_bench_run(m.h, O.ptr(prm), n_pr, nd, th, O.ptr(toks), C.byref(pre), O.ptr(prof))
         L.orc_set_pool(0)
-        return {"pool": ("ref_pool", "spin_pool")[pool], "threads": th, "decode_tok_s": round(nd / dec_s, 3),
-                "prefill_tok_s": round(n_prompt / pre.value, 3), "first_tokens": toks[n_prompt:n_prompt + 4].tolist(),
+        L.orc_set_threads(1)  # the next leg's pool is created afresh under its own affinity
+        return {"pool": ("ref_pool", "spin_pool")[pool], "threads": th, "pinned_cpus": cpus,
+                "decode_tok_s": round(nd / dec_s, 3) if nd else None, "decode_s": dec_s, "prefill_s": pre.value,
+                "prefill_tok_s": round(n_pr / pre.value, 3), "first_tokens": toks[n_pr:n_pr + 4].tolist(),
                 "decode_profile_ms_per_token": {
                     "total": round(dec_s / nd * 1e3, 3),
                     "mul_mat_wall": round(prof[1] / nd * 1e3, 3),
@@ -104,29 +145,101 @@ def cpu_baseline(n_prompt=128, n_decode=48, threads=4, q8_decode=24):
                     "pool_s": round((prof[1] - prof[2]) / nd * 1e3, 3),
                     "attention_mul_mat_wall": round(prof[4] / nd * 1e3, 3),
                     "serial_ops": round((dec_s - prof[1]) / nd * 1e3, 3),
-                    "mul_mat_calls": int(round((prof[0] + prof[3]) / nd))}}
+                    "mul_mat_calls": int(round((prof[0] + prof[3]) / nd))} if nd else None}
 
-    m = O.Model(O.make_config(GEMMA_2B, n_ctx=512))
-    runs = [run(m, 0, threads, n_decode)]
-    if all_threads != threads:
-        runs.append(run(m, 0, all_threads, n_decode))
-    runs.append(run(m, 1, all_threads, n_decode))
-    m.close()
-    q8 = []
-    if q8_decode > 0:
-        m = O.Model(O.make_config(GEMMA_2B, n_ctx=512, wtype=O.Q8_0))
-        q8 = [run(m, 0, threads, q8_decode), run(m, 1, all_threads, q8_decode)]
+    def logits_mm_s(E, V, T, th):
+        """one orc_mul_mat of a V x E Q4_0 output matrix over T columns on the reference pool (s)."""
+        pin(th)
+        rng = np.random.default_rng(3)
+        W = O.quantize((rng.standard_normal((V, E)) * 0.02).astype(np.float32), "q4_0_ref")
+        X = rng.standard_normal((T, E)).astype(np.float32)
+        wdata, rs = O.mul_mat_init(O.Q4_0, X)
+        dst = np.zeros((T, V), dtype=np.float32)
+        L.orc_set_threads(th)
+        t0 = time.perf_counter()
+        L.orc_mul_mat(V, T, 1, W.shape[1], T, V * 4, V * 4 * T, rs, E, O.ptr(W), O.ptr(dst), O.Q4_0, O.ptr(wdata), 1)
+        dt = time.perf_counter() - t0
+        L.orc_set_threads(1)
+        return dt
+
+    try:
+        m = O.Model(O.make_config(GEMMA_2B, n_ctx=512))
+        heads = [run(m, 0, threads, n_decode) for _ in range(reps)]
+        vals = sorted(r["decode_tok_s"] for r in heads)
+        med = vals[len(vals) // 2]
+        pvals = sorted(r["prefill_tok_s"] for r in heads)
+        runs = list(heads)
+        if all_threads != threads:
+            runs.append(run(m, 0, all_threads, n_decode))
+        runs.append(run(m, 1, all_threads, n_decode))
         m.close()
-    r0 = runs[0]
-    return {"value": r0["decode_tok_s"], "unit": "tok/s", "cores": threads, "kind": "port",
+        q8 = []
+        if q8_decode > 0:
+            m = O.Model(O.make_config(GEMMA_2B, n_ctx=512, wtype=O.Q8_0))
+            q8 = [run(m, 0, threads, q8_decode), run(m, 1, all_threads, q8_decode)]
+            m.close()
+
+        # config 3 on the CPU: T = 2048 prefill, bounded sample = ONE layer + a 16,000-row output at
+        # T = 2048 on the reference pool; full = 18 x layer + (256,000 / 16,000) x output GEMM
+        V_S, T3 = 16000, 2048
+        c3 = None
+        try:
+            one = dict(GEMMA_2B, n_layer=1, n_vocab=V_S)
+            m = O.Model(O.make_config(one, n_ctx=T3 + 64))
+            pr3 = np.array(make_prompt(T3, V_S, seed=2), dtype=np.int32)
+            r3 = run(m, 0, threads, 0, prm=pr3, n_pr=T3)
+            m.close()
+            lg = logits_mm_s(GEMMA_2B["n_embd"], V_S, T3, threads)
+            layer = max(r3["prefill_s"] - lg, 1e-9)
+            full = GEMMA_2B["n_layer"] * layer + (GEMMA_2B["n_vocab"] / V_S) * lg
+            c3 = {"value": round(T3 / full, 3), "unit": "tok/s", "est_s": round(full, 2), "cores": threads,
+                  "sample_layer_s": round(layer, 3), "sample_output_gemm_s": round(lg, 3),
+                  "sample": f"BASELINE config 3 on the CPU, extrapolated: one Gemma-2B Q4_0 layer + a {V_S}-row tied "
+                            f"output at T = {T3} through the oracle's prefill graph on the reference's {threads}-worker "
+                            f"pool ({r3['prefill_s']:.2f} s), minus that output GEMM timed alone; full = 18 x layer + "
+                            f"{GEMMA_2B['n_vocab'] // V_S} x output GEMM"}
+        except Exception as ex:
+            c3 = {"error": str(ex)[:200]}
+
+        # config 4 on the CPU: Gemma-7B Q4_0 batch-1 decode (one process, the reference pool; the
+        # reference has no multi-device path), bounded sample = 2 of 28 layers + a 16,000-row output
+        c4 = None
+        try:
+            nl, nd7, np7 = 2, 16, 16
+            two = dict(GEMMA_7B, n_layer=nl, n_vocab=V_S)
+            m = O.Model(O.make_config(two, n_ctx=128))
+            pr7 = np.array(make_prompt(np7, V_S), dtype=np.int32)
+            r7 = run(m, 0, threads, nd7, prm=pr7, n_pr=np7)
+            m.close()
+            lg7 = logits_mm_s(GEMMA_7B["n_embd"], V_S, 1, threads)
+            step = r7["decode_s"] / nd7
+            layer7 = max(step - lg7, 1e-9) / nl
+            full7 = GEMMA_7B["n_layer"] * layer7 + (GEMMA_7B["n_vocab"] / V_S) * lg7
+            c4 = {"value": round(1.0 / full7, 3), "unit": "tok/s", "est_ms_per_token": round(full7 * 1e3, 2),
+                  "cores": threads, "sample_layer_ms": round(layer7 * 1e3, 3), "sample_output_ms": round(lg7 * 1e3, 3),
+                  "sample": f"BASELINE config 4 on the CPU (one host, reference pool x{threads}), extrapolated: "
+                            f"{nl} Gemma-7B Q4_0 layers + a {V_S}-row output, {nd7} greedy decode steps after a "
+                            f"{np7}-token prompt, minus that output matvec timed alone; full = 28 x layer + "
+                            f"{GEMMA_7B['n_vocab'] // V_S} x output"}
+        except Exception as ex:
+            c4 = {"error": str(ex)[:200]}
+    finally:
+        if saved_aff is not None:
+            os.sched_setaffinity(0, saved_aff)
+    for r in runs + q8:
+        r.pop("decode_s", None), r.pop("prefill_s", None)
+    return {"value": med, "unit": "tok/s", "cores": threads, "kind": "port",
+            "reps": reps, "reps_decode_tok_s": [r["decode_tok_s"] for r in heads],
+            "spread": round((vals[-1] - vals[0]) / med, 4) if med else None,
             "sample": f"BASELINE config 1: Gemma-2B Q4_0 synthetic weights, {n_prompt}-token prompt prefilled as one graph, "
                       f"then {n_decode} greedy decode steps (of config 1's 128; per-step cost is flat), mul_mat on "
                       f"the reference's {threads}-worker task pool (oracle/ restatement of src/hpc.cpp + src/thread_pool.cpp, "
-                      f"AVX2 vec_dot), other ops on 1 thread",
-            "prefill_tok_s": r0["prefill_tok_s"], "cpu_model": _cpu_model(), "nproc": nproc,
+                      f"AVX2 vec_dot), other ops on 1 thread; median of {reps} runs pinned to {threads} physical cores",
+            "prefill_tok_s": pvals[len(pvals) // 2], "cpu_model": _cpu_model(), "nproc": nproc,
             "affinity_cpus": allowed, "runs": runs,
             "q8_0": {"value": q8[0]["decode_tok_s"] if q8 else None, "unit": "tok/s",
                      "sample": f"BASELINE config 5: Gemma-2B Q8_0, same prompt, {q8_decode} decode steps", "runs": q8},
+            "prefill_2048": c3, "decode_7b": c4,
             "thread_scaling_note": ("decode does not scale past ~4 reference-pool workers because each of the 415 "
                                     "mul_mat calls per token pays a packaged_task + mutex + condvar wake per worker "
                                     "(pool_s grows with the worker count, and the 288 per-head attention products are "
@@ -156,18 +269,39 @@ def prefill_roofline(T, prefill):
     out["achieved"] = out["exact"]["achieved"]
     out["peak"] = MFMA_PEAK_TOPS["i8"]
     out["frac"] = out["exact"]["frac_i8"]
+    out["pmc_exact_gemm"] = None
+    out["pmc_exact_attention"] = None
+    path = latest_profile("pmc_prefill_q4_0.json")
     try:
-        with open(os.path.join(ROOT, "profiles", "r02", "pmc_prefill.json")) as f:
+        with open(path) as f:
             pmc = json.load(f)
-        out["pmc_exact_gemm"] = {k: pmc[k] for k in ("mfma_util", "lds_busy", "lds_bank_conflict_frac", "note")}
+        keys = ("mfma_util", "lds_busy", "lds_bank_conflict_frac", "valu_inst_per_wave_cycle", "wait_any_frac", "what")
+        src = os.path.relpath(path, ROOT)
+        for k_name, field in (("k_gemm_x", "pmc_exact_gemm"), ("k_attn_rows", "pmc_exact_attention")):
+            if k_name in pmc:
+                out[field] = dict({k: pmc[k_name][k] for k in keys if k in pmc[k_name]}, source=src)
     except Exception:
-        out["pmc_exact_gemm"] = None
+        pass
     return out
+
+
+def latest_profile(name):
+    """profiles/rNN/<name> of the newest round that has it (committed and shipped with the tree)."""
+    pdir = os.path.join(ROOT, "profiles")
+    try:
+        rounds = sorted((d for d in os.listdir(pdir) if d.startswith("r") and d[1:].isdigit()), reverse=True)
+    except OSError:
+        rounds = []
+    for d in rounds:
+        path = os.path.join(pdir, d, name)
+        if os.path.exists(path):
+            return path
+    return os.path.join(pdir, name)
 
 
 def load_traffic(kernel_id):
     """HBM bytes per launch of the roofline kernel from the committed PMC summary (or None)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    path = latest_profile("pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)

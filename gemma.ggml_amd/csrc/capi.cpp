@@ -217,15 +217,24 @@ namespace ghip {
 // the tiled device copy of a registered (or already mul_mat'ed) Q4_0 / Q8_0 host weight with rows
 // of K values, any row count: the ggml fast path's engine copies its weights from here, device to
 // device, instead of uploading them from the host a second time
+// Only dense registrations qualify (nb01 = the row size of (type, K): upload_rows copies rows as
+// if they were contiguous; a strided view sharing the base pointer would hand it the wrong rows),
+// and of those the one with the most rows.
 bool registered_tiled(const void *host, int type, int64_t K, tiled_mat *out) {
     hpc_state &s = st();
     std::lock_guard<std::recursive_mutex> lk(s.mu);
+    const size_t dense = (size_t)(K / 32) * (type == T_Q4_0 ? 18 : 34);
+    const tiled_mat *best = nullptr;
+    int64_t best_rows = -1;
     for (const auto &kv : s.weights)
-        if (kv.first.host == host && kv.first.type == type && kv.first.ne00 == K) {
-            *out = kv.second;
-            return true;
+        if (kv.first.host == host && kv.first.type == type && kv.first.ne00 == K && (size_t)kv.first.nb01 == dense &&
+            kv.first.ne01 > best_rows) {
+            best = &kv.second;
+            best_rows = kv.first.ne01;
         }
-    return false;
+    if (!best) return false;
+    *out = *best;
+    return true;
 }
 }  // namespace ghip
 

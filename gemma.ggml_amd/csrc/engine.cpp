@@ -214,6 +214,7 @@ struct gemma_engine {
     // RCCL all-gather completes them
     int tp_n = 1, tp_rank = 0;
     int n_virtual = 1;  // > 1: all tp_n ranks' shards in this one engine (single-GPU parity mode, no RCCL)
+    bool tp_n_keys = false;  // logits through per-rank argmax keys (row split: virtual ranks or an RCCL comm)
     ncclComm_t comm = nullptr;
     int64_t sh_qkv = 0, sh_e = 0, sh_ff = 0, sh_v = 0;  // rows per rank (qkv, n_embd, n_ff, n_vocab)
     unsigned long long *rank_keys = nullptr;           // [tp_n] one argmax key per rank
@@ -247,6 +248,7 @@ struct gemma_engine {
     unsigned long long *tok_gran = nullptr;  // hand-off granules (zeroed once; tags carry the epoch)
     unsigned *epoch = nullptr;         // bumped by k_advance / k_set_position once per token
     int *tok_err = nullptr;            // sticky hand-off timeout [flag, site, layer]
+    unsigned persist_timeout = 2000000u;  // per-wait bound of the launch (100 MHz ticks; tests shorten it)
     int fuse_front = 0;  // measured: 727 vs 672 us/token (the in-launch hand-offs cost as much as the
                          // launch boundaries they replace; DESIGN.md perf log) — kept as an option
     unsigned *front_cnt = nullptr;
@@ -310,7 +312,7 @@ static int pick_ks(int wtype, int64_t n_bt, int target) {
 
 // in-place all-gather of a full vector whose rank-r shard [r*cnt, (r+1)*cnt) was just written
 static int tp_gather(gemma_engine *e, float *full, int64_t cnt) {
-    if (e->tp_n == 1 || !e->comm) return 0;  // one rank, or virtual ranks (shards already in place)
+    if (!e->comm) return 0;  // one unsplit engine, or virtual ranks (shards already in place)
     const ncclResult_t r = ncclAllGather(full + (size_t)e->tp_rank * cnt, full, (size_t)cnt, ncclFloat, e->comm, e->stream);
     if (r != ncclSuccess) {
         set_error(std::string("ncclAllGather: ") + ncclGetErrorString(r));
@@ -321,7 +323,7 @@ static int tp_gather(gemma_engine *e, float *full, int64_t cnt) {
 
 // in-place all-gather of the h image: per rank `act_bytes` of act (u32 groups) and `nda` scales
 static int tp_gather_bytes(gemma_engine *e, uint32_t *act, int64_t act_bytes, float *da, int64_t nda) {
-    if (e->tp_n == 1 || !e->comm) return 0;
+    if (!e->comm) return 0;
     ncclGroupStart();
     ncclResult_t r = ncclAllGather((uint8_t *)act + (size_t)e->tp_rank * act_bytes, act, (size_t)act_bytes, ncclUint8,
                                    e->comm, e->stream);
@@ -383,7 +385,7 @@ static int tok_prepare(gemma_engine *e) {
     e->persist_why.clear();
     if (e->kq) e->persist_why = "K-quant layers";
     else if (e->out_type == T_Q6_K) e->persist_why = "Q6_K token_embd (the launch dequantizes the layer type)";
-    else if (e->tp_n != 1 || e->n_virtual != 1) e->persist_why = "row-split TP";
+    else if (e->tp_n != 1 || e->n_virtual != 1 || e->comm) e->persist_why = "row-split TP";
     if (!e->persist_why.empty() || !e->tok_gran) {
         if (e->persist_why.empty()) e->persist_why = "no buffers";
         return 0;
@@ -419,6 +421,7 @@ static int tok_prepare(gemma_engine *e) {
     a.gh = p; p += g.gh;
     a.gh_da = p;
     a.epoch = e->epoch; a.x_out = e->x; a.att_out = e->attn; a.err = e->tok_err;
+    a.timeout = e->persist_timeout;
     e->persist_why = token_unsupported(c.wtype, a);
     GHIP_CHECK(hipMemcpy(e->tok_dev, &a, sizeof(tok_args), hipMemcpyHostToDevice));
     return 0;
@@ -426,6 +429,25 @@ static int tok_prepare(gemma_engine *e) {
 static bool persist_on(const gemma_engine *e) {
     return e->persist && e->persist_why.empty() && !e->dbg && !e->stamp && e->att_mode == ATTN_PER_HEAD && !e->warm &&
            !e->fuse_front;
+}
+
+// After a stream sync that covers persistent-launch steps: a hand-off that timed out (a workgroup
+// not co-resident, the CUs shared with another stream or process) leaves the sticky word set and the
+// step's numbers wrong.  Report it, clear it and fall back to the per-layer launches for later steps
+// (ADVICE r3); returns 1 when a timeout was seen.
+static void drop_graph(gemma_engine *e);
+static int persist_check(gemma_engine *e) {
+    if (!persist_on(e) || !e->tok_err) return 0;
+    int w[3] = {0, 0, 0};
+    if (hipMemcpy(w, e->tok_err, 12, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    if (!w[0]) return 0;
+    (void)hipMemset(e->tok_err, 0, 64);
+    e->persist = 0;
+    drop_graph(e);
+    set_error("persistent token launch: hand-off timeout (site " + std::to_string(w[1]) + ", layer " +
+              std::to_string(w[2]) + "): the step's logits and KV rows are invalid; the engine now runs the "
+              "per-layer launches");
+    return 1;
 }
 
 static int enqueue_step(gemma_engine *e) {
@@ -447,7 +469,7 @@ static int enqueue_step(gemma_engine *e) {
         goto logits;
     }
     {
-    const bool front_ok = e->front_cnt && e->fuse_front && e->tp_n == 1 && e->n_virtual == 1 && !e->warm &&
+    const bool front_ok = e->front_cnt && e->fuse_front && e->tp_n == 1 && !e->comm && e->n_virtual == 1 && !e->warm &&
                           e->att_mode == ATTN_PER_HEAD && e->att_act && e->plan[MC_QKV].ks == KS_RR &&
                           e->plan[MC_O].ks == KS_RR && e->plan[MC_O].img;
     if (front_ok) GHIP_CHECK(hipMemsetAsync(e->front_cnt, 0, (size_t)c.n_layer * 16 * 32 * 4, s));
@@ -624,9 +646,9 @@ logits:
         o.dbg_t = e->stamp ? e->stamp + 5 * kStampRegion : nullptr;
         if (launch_matvec(wt, 1, PRO_NORM, EPI_ARGMAX, o, lg_grid, s)) return -1;
         // TP: one key per rank, its index made global
-        if (e->tp_n > 1 && launch_reduce_keys(e->key, lg_grid, (int64_t)rk * e->sh_v, e->rank_keys + rk, s)) return -1;
+        if (e->tp_n_keys && launch_reduce_keys(e->key, lg_grid, (int64_t)rk * e->sh_v, e->rank_keys + rk, s)) return -1;
     }
-    if (e->tp_n == 1) {
+    if (!e->tp_n_keys) {
         if (launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s)) return -1;
         return warm_join(e);
     }
@@ -829,11 +851,12 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         set_error("gemma_engine_create: unsupported config");
         return nullptr;
     }
-    if (kq_layers && (c.n_embd % 256 || c.n_ff % 256 || (c.n_head * c.head_dim) % 256 || c.n_embd > 4096 || tp_n > 1)) {
+    if (kq_layers && (c.n_embd % 256 || c.n_ff % 256 || (c.n_head * c.head_dim) % 256 || c.n_embd > 4096 || tp_n > 1 ||
+                      nccl_id)) {
         set_error("gemma_engine_create: K-quant layers need n_embd, n_ff, n_head*head_dim % 256 == 0, n_embd <= 4096, one rank");
         return nullptr;
     }
-    if ((c.out_type == T_Q6_K || kq_layers) && (c.n_embd % 256 || c.n_embd > 4096 || tp_n > 1)) {
+    if ((c.out_type == T_Q6_K || kq_layers) && (c.n_embd % 256 || c.n_embd > 4096 || tp_n > 1 || nccl_id)) {
         set_error("gemma_engine_create: a Q6_K output needs n_embd % 256 == 0, n_embd <= 4096 and one rank");
         return nullptr;
     }
@@ -869,7 +892,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     if (const char *v = getenv("GHIP_GRID_BIG")) e->grid_big = atoi(v);
     if (const char *v = getenv("GHIP_WARM")) e->warm = atoi(v);
     if (const char *v = getenv("GHIP_WARM_GRID")) e->warm_grid = atoi(v);
-    if (tp_n > 1) e->warm = 0;  // single-GPU decode only
+    if (tp_n > 1 || nccl_id) e->warm = 0;  // single-GPU decode only
     if (e->warm) {
         GHIP_FATAL(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
         e->ev_fork.resize(c.n_layer);
@@ -1119,12 +1142,15 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     GHIP_FATAL(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
     GHIP_FATAL(hipMalloc(&e->rank_keys, (size_t)tp_n * 8));
     GHIP_FATAL(hipStreamSynchronize(s));
-    if (tp_n > 1 && nccl_id) {
+    // a communicator whenever an id is given, also for ONE rank: every gather, the key gather and
+    // RCCL inside the captured hipGraph then run exactly as on N GPUs (a 1-rank all-gather in place)
+    if (nccl_id) {
         ncclUniqueId id;
         memcpy(&id, nccl_id, sizeof(id));
         const ncclResult_t nr = ncclCommInitRank(&e->comm, tp_n, id, tp_rank);
         if (nr != ncclSuccess) set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
     }
+    e->tp_n_keys = tp_n > 1 || e->comm;
     {
         // default launch plan (the shapes of every rank's shards are equal)
         const layer_dev &L0 = e->layers[0];
@@ -1134,7 +1160,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         e->plan[MC_DOWN] = {pick_ks(wt, L0.down.n_bt, e->ks_down), 1, 0};
         e->plan[MC_LOGITS] = {1, 1, 0};
     }
-    if (last_error().empty() && !kq_layers) (void)tok_prepare(e);
+    if (last_error().empty()) (void)tok_prepare(e);  // K-quant engines: persist_why = "K-quant layers"
     if (!last_error().empty()) {
         gemma_engine_free(e);
         return nullptr;
@@ -1261,6 +1287,16 @@ extern "C" gemma_engine *gemma_engine_create_from_gguf(const char *path, int n_c
 extern "C" int gemma_engine_config(const gemma_engine *e, gemma_hip_config *out) {
     if (!e || !out) return -1;
     *out = e->cfg;
+    return 0;
+}
+
+// the engine's row split: [ranks, this rank, RCCL communicator present, shard slots in this engine]
+extern "C" int gemma_engine_tp_info(const gemma_engine *e, int *out4) {
+    if (!e || !out4) return -1;
+    out4[0] = e->tp_n;
+    out4[1] = e->tp_rank;
+    out4[2] = e->comm ? 1 : 0;
+    out4[3] = e->n_virtual;
     return 0;
 }
 
@@ -1408,6 +1444,7 @@ extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_
         e->host_pos += 1;
     }
     GHIP_CHECK(hipStreamSynchronize(e->stream));
+    if (persist_check(e)) return -1;  // the sequence must be restarted (gemma_engine_begin)
     return 0;
 }
 
@@ -1745,9 +1782,19 @@ extern "C" int gemma_engine_set_persist(gemma_engine *e, int on) {
         e->persist = on;
         drop_graph(e);
     }
-    if (!e->kq && tok_prepare(e)) return -1;
+    if (tok_prepare(e)) return -1;
     if (e->persist && !e->persist_why.empty()) set_error("persistent token launch: " + e->persist_why);
     return persist_on(e) ? 1 : 0;
+}
+
+// tests: the persistent launch's per-wait bound in 100 MHz ticks (0 = the default 20 ms); a tiny
+// bound forces hand-off timeouts so that their reporting can be checked
+extern "C" int gemma_engine_set_persist_timeout(gemma_engine *e, unsigned ticks) {
+    set_error("");
+    (void)hipSetDevice(e->device);
+    e->persist_timeout = ticks ? ticks : 2000000u;
+    drop_graph(e);
+    return tok_prepare(e);
 }
 
 // the persistent launch's sticky hand-off timeout words [flag, site, layer] (0 = none seen);
@@ -2039,7 +2086,7 @@ static int prefill_run(gemma_engine *e, bool exact, float *logits_last, float *l
         set_error("gemma_engine_prefill: call right after gemma_engine_begin");
         return -1;
     }
-    if (e->tp_n > 1) {
+    if (e->tp_n > 1 || e->comm) {
         set_error("gemma_engine_prefill: the MFMA prefill is single-GPU (row-split engines prefill token by token)");
         return -1;
     }
@@ -2336,6 +2383,14 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
         if (ensure_graph(e)) return -1;
     } else {
         GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
+    }
+    if (persist_on(e)) {  // a hand-off timeout: redo this token on the per-layer launches (same bits)
+        GHIP_CHECK(hipStreamSynchronize(e->stream));
+        if (persist_check(e)) {
+            fprintf(stderr, "[gemma_hip] %s; token at position %d redone\n", last_error().c_str(), pos);
+            set_error("");
+            if (ext_set_position(e, token, pos) || enqueue_step(e)) return -1;
+        }
     }
     if (prof) GHIP_CHECK(hipStreamSynchronize(e->stream));
     const double t1 = prof ? us() : 0.0;

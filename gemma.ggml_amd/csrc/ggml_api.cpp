@@ -962,8 +962,8 @@ void ggml_free(struct ggml_context *ctx) {
                 ex().tiled.erase(tt);
             }
         }
-    }
-    {  // a freed weight context takes the fast path's device copy of its weights with it
+        // a freed weight context takes the fast path's device copy of its weights with it; under the
+        // executor's lock, which try_fast holds while it runs that engine
         fast_engine &f = fast();
         if (f.e && std::any_of(f.weights.begin(), f.weights.end(), inside)) {
             const std::unordered_set<const void *> ws(f.weights.begin(), f.weights.end());
@@ -999,6 +999,31 @@ size_t ggml_nbytes(const struct ggml_tensor *t) {
     return nbytes;
 }
 
+// ---- ggml's naming of derived tensors (ggml.c of the reference's era): a view / reshape / permute /
+// transpose / cont is named "<src> (view)" etc., a cpy "<dst> (copy of <src>)" (or "<src> (copy)" when
+// the destination is unnamed), and ggml_build_forward_expand names the still unnamed nodes
+// "node_<index>" and leaves "leaf_<index>".  These are the names the reference's graph listings hold
+// (tensor_dump/tensor_in_target_cgraph; the source-side dump at src/gemma_model.cpp:240-248).  Plain
+// concatenation instead of snprintf: ~600 tensors per decode graph on the host path.
+static void name_cat(ggml_tensor *t, const char *a, const char *b, const char *c = nullptr, const char *d = nullptr) {
+    char *o = t->name, *const end = t->name + GGML_MAX_NAME - 1;
+    for (const char *p : {a, b, c, d})
+        for (; p && *p && o < end; ++p) *o++ = *p;
+    *o = 0;
+}
+static void name_index(char *name, const char *prefix, int i) {
+    char digits[12];
+    int n = 0;
+    do {
+        digits[n++] = (char)('0' + i % 10);
+        i /= 10;
+    } while (i > 0 && n < 11);
+    char *o = name;
+    for (const char *p = prefix; *p; ++p) *o++ = *p;
+    while (n > 0) *o++ = digits[--n];
+    *o = 0;
+}
+
 // ---- tensors and views -------------------------------------------------------------------------
 struct ggml_tensor *ggml_new_tensor(struct ggml_context *ctx, enum ggml_type type, int n_dims, const int64_t *ne) {
     return new_tensor_impl(ctx, type, n_dims, ne, nullptr, 0);
@@ -1019,6 +1044,7 @@ struct ggml_tensor *ggml_view_1d(struct ggml_context *ctx, struct ggml_tensor *a
     ggml_tensor *t = view_of(ctx, a, 1, &ne0, offset);
     t->op = GGML_OP_VIEW;
     t->src[0] = a;
+    name_cat(t, a->name, " (view)");
     return t;
 }
 struct ggml_tensor *ggml_view_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1, size_t nb1,
@@ -1030,6 +1056,7 @@ struct ggml_tensor *ggml_view_2d(struct ggml_context *ctx, struct ggml_tensor *a
     t->nb[3] = t->nb[2];
     t->op = GGML_OP_VIEW;
     t->src[0] = a;
+    name_cat(t, a->name, " (view)");
     return t;
 }
 struct ggml_tensor *ggml_view_3d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1, int64_t ne2,
@@ -1041,6 +1068,7 @@ struct ggml_tensor *ggml_view_3d(struct ggml_context *ctx, struct ggml_tensor *a
     t->nb[3] = t->nb[2] * ne2;
     t->op = GGML_OP_VIEW;
     t->src[0] = a;
+    name_cat(t, a->name, " (view)");
     return t;
 }
 struct ggml_tensor *ggml_reshape_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1) {
@@ -1048,6 +1076,7 @@ struct ggml_tensor *ggml_reshape_2d(struct ggml_context *ctx, struct ggml_tensor
     ggml_tensor *t = view_of(ctx, a, 2, ne, 0);
     t->op = GGML_OP_RESHAPE;
     t->src[0] = a;
+    name_cat(t, a->name, " (reshaped)");
     return t;
 }
 struct ggml_tensor *ggml_reshape_3d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1,
@@ -1056,6 +1085,7 @@ struct ggml_tensor *ggml_reshape_3d(struct ggml_context *ctx, struct ggml_tensor
     ggml_tensor *t = view_of(ctx, a, 3, ne, 0);
     t->op = GGML_OP_RESHAPE;
     t->src[0] = a;
+    name_cat(t, a->name, " (reshaped)");
     return t;
 }
 struct ggml_tensor *ggml_permute(struct ggml_context *ctx, struct ggml_tensor *a, int axis0, int axis1, int axis2,
@@ -1068,6 +1098,7 @@ struct ggml_tensor *ggml_permute(struct ggml_context *ctx, struct ggml_tensor *a
     }
     t->op = GGML_OP_PERMUTE;
     t->src[0] = a;
+    name_cat(t, a->name, " (permuted)");
     return t;
 }
 struct ggml_tensor *ggml_transpose(struct ggml_context *ctx, struct ggml_tensor *a) {
@@ -1079,6 +1110,7 @@ struct ggml_tensor *ggml_transpose(struct ggml_context *ctx, struct ggml_tensor 
     t->nb[1] = a->nb[0];
     t->op = GGML_OP_TRANSPOSE;
     t->src[0] = a;
+    name_cat(t, a->name, " (transposed)");
     return t;
 }
 struct ggml_tensor *ggml_cont_2d(struct ggml_context *ctx, struct ggml_tensor *a, int64_t ne0, int64_t ne1) {
@@ -1086,6 +1118,7 @@ struct ggml_tensor *ggml_cont_2d(struct ggml_context *ctx, struct ggml_tensor *a
     ggml_tensor *t = new_tensor_impl(ctx, a->type, 2, ne, nullptr, 0);
     t->op = GGML_OP_CONT;
     t->src[0] = a;
+    name_cat(t, a->name, " (cont)");
     return t;
 }
 struct ggml_tensor *ggml_set_name(struct ggml_tensor *t, const char *name) {
@@ -1100,6 +1133,12 @@ struct ggml_tensor *ggml_format_name(struct ggml_tensor *t, const char *fmt, ...
     return t;
 }
 const char *ggml_get_name(const struct ggml_tensor *t) { return t->name; }
+const char *ggml_op_name(enum ggml_op op) {
+    static const char *const names[GGML_OP_COUNT] = {"NONE", "GET_ROWS", "SCALE", "RMS_NORM", "MUL", "ADD", "MUL_MAT",
+                                                     "ROPE", "SOFT_MAX", "GELU", "CPY", "CONT", "VIEW", "RESHAPE",
+                                                     "PERMUTE", "TRANSPOSE"};
+    return (int)op >= 0 && op < GGML_OP_COUNT ? names[op] : "?";
+}
 struct ggml_tensor *ggml_get_tensor(struct ggml_context *ctx, const char *name) {
     for (ggml_tensor *t : ctx->tensors)
         if (strcmp(t->name, name) == 0) return t;
@@ -1176,6 +1215,8 @@ struct ggml_tensor *ggml_cpy(struct ggml_context *ctx, struct ggml_tensor *a, st
     t->op = GGML_OP_CPY;
     t->src[0] = a;
     t->src[1] = b;
+    if (b->name[0]) name_cat(t, b->name, " (copy of ", a->name, ")");
+    else name_cat(t, a->name, " (copy)");
     return t;
 }
 
@@ -1193,12 +1234,16 @@ static void visit(ggml_cgraph *g, ptr_set &seen, ggml_tensor *t) {
     if (!t || !seen.insert(t)) return;
     for (int i = 0; i < GGML_MAX_SRC; ++i) visit(g, seen, t->src[i]);
     if (t->op == GGML_OP_NONE) {
-        if (g->n_leafs < g->size) g->leafs[g->n_leafs++] = t;
+        if (g->n_leafs < g->size) {
+            if (!t->name[0]) name_index(t->name, "leaf_", g->n_leafs);
+            g->leafs[g->n_leafs++] = t;
+        }
     } else {
         if (g->n_nodes >= g->size) {
             fprintf(stderr, "[gemma_hip] ggml: graph full\n");
             abort();
         }
+        if (!t->name[0]) name_index(t->name, "node_", g->n_nodes);
         g->nodes[g->n_nodes++] = t;
     }
 }

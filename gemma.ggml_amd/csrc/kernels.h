@@ -331,6 +331,7 @@ struct tok_args {
     float *x_out = nullptr;           // the last layer's output x (the logits launch's input)
     float *att_out = nullptr;         // attention output scratch (written, unused)
     int *err = nullptr;               // [0] sticky hand-off timeout, [1] site, [2] layer
+    unsigned timeout = 2000000u;      // per-wait bound in s_memrealtime ticks (100 MHz): 20 ms
     unsigned long long *dbg_t = nullptr;  // stamps build: [grid][n_layer][16] s_memrealtime
 };
 // granules each buffer holds for shapes (E, F, qkv_rows)

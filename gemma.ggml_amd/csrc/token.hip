@@ -49,7 +49,6 @@ constexpr int TK_AUX = 4;                    // aux waves: wave 8 = the carrier;
 constexpr int TK_NTH = 64 * (TK_TW + TK_AUX);
 constexpr int TK_ATH = 64 * TK_AUX;          // aux threads
 constexpr int TK_SLOT = 1152;                // ring slot: 1 KiB quants + up to 128 B scales
-constexpr unsigned TK_TIMEOUT = 2000000u;    // s_memrealtime ticks (100 MHz): 20 ms per wait
 constexpr int TK_MAXL = 32;                  // layers the LDS pointer table holds
 constexpr int TK_TABB = (int)sizeof(tok_layer);  // bytes per layer in that table (14 pointers)
 // the launch's arguments live in device memory and are read through the constant address space:
@@ -171,7 +170,7 @@ __device__ void gather(int atid, bool *fail, ctok &a, const unsigned long long *
 #pragma unroll
         for (int k = 0; k < MAXP; ++k) ok &= (v[k][1] == tag) & (v[k][3] == tag);
         if (ok || failed) break;
-        if ((unsigned)__builtin_amdgcn_s_memrealtime() - t0 > TK_TIMEOUT) {
+        if ((unsigned)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
             *fail = true;
             note_timeout(a, site, layer);
             break;
@@ -207,7 +206,7 @@ __device__ void probe(int atid, bool *fail, ctok &a, const unsigned long long *g
     for (;;) {
         const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, p * 16, 0, 16 /* sc1 */);
         if (r[1] == tag && r[3] == tag) break;
-        if ((unsigned)__builtin_amdgcn_s_memrealtime() - t0 > TK_TIMEOUT) {
+        if ((unsigned)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
             *fail = true;
             note_timeout(a, site, layer);
             break;

@@ -24,7 +24,7 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
            "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs",
-           "gemma_tp_unique_id", "gemma_engine_create_tp",
+           "gemma_tp_unique_id", "gemma_engine_create_tp", "gemma_engine_tp_info", "gemma_engine_set_persist_timeout",
            "gguf_init_from_file", "gguf_free", "gguf_get_n_kv", "gguf_get_key", "gguf_get_kv_type",
            "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
            "gguf_get_val_data", "gguf_get_n_tensors", "gguf_get_tensor_name", "gguf_get_tensor_type",
@@ -113,6 +113,8 @@ def lib():
     L.gemma_engine_set_fuse.argtypes = [vp, C.c_int]
     L.gemma_engine_set_persist.argtypes = [vp, C.c_int]
     L.gemma_engine_persist_err.argtypes = [vp, vp, C.c_int]
+    L.gemma_engine_set_persist_timeout.argtypes = [vp, C.c_uint]
+    L.gemma_engine_tp_info.argtypes = [vp, vp]
     L.gemma_engine_graph_kernels.argtypes = [vp]
     L.gemma_engine_time.restype = C.c_double
     L.gemma_engine_time.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_double)]
@@ -200,7 +202,7 @@ class Engine:
         self.cfg = GemmaConfig(n_ctx=n_ctx, wtype=wtype, eps=eps, rope_base=rope_base, seed=seed,
                                gelu_clamp=gelu_clamp, out_type=out_type, out_gain=out_gain, **shape)
         self.L = lib()
-        if tp is not None and tp[0] > 1:
+        if tp is not None and (tp[0] > 1 or tp[2] is not None):  # n_ranks 1 + id: a 1-rank RCCL comm
             idbuf = C.create_string_buffer(bytes(tp[2]), len(tp[2])) if tp[2] is not None else None
             self.h = self.L.gemma_engine_create_tp(C.byref(self.cfg), device, tp[0], tp[1], idbuf)
         else:
@@ -310,6 +312,16 @@ class Engine:
         """The decode step's layers as one persistent launch (token.hip): on 1/0, -1 keep; returns
         True when it runs this engine's steps."""
         return self.L.gemma_engine_set_persist(self.h, on) == 1
+
+    def set_persist_timeout(self, ticks):
+        """the persistent launch's per-wait bound in 100 MHz ticks (0 = default; tests force timeouts)"""
+        return self.L.gemma_engine_set_persist_timeout(self.h, ticks)
+
+    def tp_info(self):
+        """[ranks, rank, RCCL communicator present, shard slots in this engine]"""
+        out = (C.c_int * 4)()
+        self.L.gemma_engine_tp_info(self.h, out)
+        return list(out)
 
     def persist_err(self, reset=False):
         """Sticky hand-off timeout words [flag, site, layer] of the persistent launch."""

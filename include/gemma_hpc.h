@@ -84,6 +84,10 @@ int gemma_engine_config(const gemma_engine *e, gemma_hip_config *out);
 int gemma_tp_unique_id(void *out, int cap);
 gemma_engine *gemma_engine_create_tp(const gemma_hip_config *cfg, int device, int n_ranks, int rank,
                                      const void *nccl_id);
+/* n_ranks == 1 with an id: a 1-rank RCCL communicator; every all-gather and the key gather then run
+ * through RCCL (captured in the decode hipGraph) exactly as on N GPUs.  tp_info: [ranks, rank,
+ * communicator present, shard slots in this engine] */
+int gemma_engine_tp_info(const gemma_engine *e, int *out4);
 void gemma_engine_free(gemma_engine *e);
 /* start a sequence: KV cache cleared, prompt stored on the device */
 int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_prompt);
@@ -116,11 +120,16 @@ int gemma_engine_plan(gemma_engine *e, int *out, int cap);
 int gemma_engine_set_plan(gemma_engine *e, const int *in, int n);
 int gemma_engine_set_fuse(gemma_engine *e, int fuse_front); /* fused layer front on/off (-1 = keep); returns the hand-off timeout word */
 int gemma_engine_graph_kernels(gemma_engine *e);            /* kernel launches per decode token (captured graph) */
-/* the decode step's layers as ONE persistent launch (default where the shapes allow it; -1 = keep):
- * returns 1 when it runs this engine's steps, 0 when not (hpc_last_error says why) */
+/* the decode step's layers as ONE persistent launch (opt-in: off by default, GHIP_PERSIST=1 or this
+ * call; -1 = keep): returns 1 when it runs this engine's steps, 0 when not (hpc_last_error says why:
+ * K-quant layers, row-split TP, shapes).  A hand-off timeout inside the launch (a workgroup not
+ * co-resident) is reported: gemma_engine_step returns -1 (restart the sequence), the ggml executor's
+ * decode redoes the token on the per-layer launches; either way the engine leaves the launch off. */
 int gemma_engine_set_persist(gemma_engine *e, int on);
 /* its sticky hand-off timeout words [flag, site, layer]; returns the flag (0 = none); reset clears */
 int gemma_engine_persist_err(gemma_engine *e, int *out3, int reset);
+/* tests: the launch's per-wait bound in 100 MHz ticks (0 = default 20 ms) */
+int gemma_engine_set_persist_timeout(gemma_engine *e, unsigned ticks);
 /* debugging: one eager step with per-layer taps [n_layer][qkv | attn_out | layer_out] */
 int gemma_engine_debug_step(gemma_engine *e, float *host_taps, float *logits);
 /* diagnostics: prefill (exact != 0: the exact path) with the residual stream after each layer

@@ -164,6 +164,7 @@ struct ggml_tensor *ggml_cont_2d(struct ggml_context *ctx, struct ggml_tensor *a
 struct ggml_tensor *ggml_set_name(struct ggml_tensor *tensor, const char *name);
 struct ggml_tensor *ggml_format_name(struct ggml_tensor *tensor, const char *fmt, ...);
 const char *ggml_get_name(const struct ggml_tensor *tensor);
+const char *ggml_op_name(enum ggml_op op); /* "MUL_MAT", "VIEW", ... */
 struct ggml_tensor *ggml_get_tensor(struct ggml_context *ctx, const char *name);
 
 /* ops (src/gemma_model.cpp:438-518, 665-747) */

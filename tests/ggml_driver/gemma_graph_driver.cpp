@@ -54,6 +54,7 @@ struct model {
     std::vector<ggml_tensor *> k_layer, v_layer;
     int kv_n = 0, kv_head = 0;
     std::vector<char> compute_mem;
+    bool no_alloc = false;  // --graph-listing: node metadata only
     // GGUF-loaded models: kv index, tensors by name, tokenizer tables (src/gemma_model.cpp:200-214)
     std::map<std::string, int> kv_index;
     std::map<std::string, ggml_tensor *> tensors;
@@ -251,7 +252,7 @@ void build_kv_store(model &m, ggml_context *ctx, ggml_cgraph *g, ggml_tensor *k_
 
 void reset_compute_context(model &m) {  // :650-663
     if (m.compute_ctx) ggml_free(m.compute_ctx);
-    ggml_init_params p = {m.compute_mem.size(), m.compute_mem.data(), false};
+    ggml_init_params p = {m.compute_mem.size(), m.compute_mem.data(), m.no_alloc};
     m.compute_ctx = ggml_init(p);
 }
 
@@ -266,7 +267,9 @@ ggml_cgraph *build_compute_graph(model &m, const std::vector<int32_t> &input, st
     ggml_tensor *inpL = ggml_get_rows(ctx, m.token_embd, tok);
     inpL = ggml_scale(ctx, inpL, sqrtf((float)h.n_embd));
     ggml_tensor *pos = ggml_view_1d(ctx, m.inp_pos, T, 0);
+    ggml_set_name(pos, "inp_pos (view)");
     ggml_tensor *mask = ggml_view_2d(ctx, m.inp_KQ_mask, m.kv_n, T, m.kv_n * ggml_type_size(m.inp_KQ_mask->type), 0);
+    ggml_set_name(mask, "inp_KQ_mask (view)");
     for (int il = 0; il < h.n_layer; ++il) {
         const layer_w &L = m.layers[il];
         ggml_tensor *cur = build_norm(m, ctx, inpL, L.attn_norm);
@@ -440,7 +443,60 @@ int run_one(int argc, char **argv, const char *wpath, const char *opath) {
     return 0;
 }
 
+// --graph-listing: build_compute_graph on weight / input / cache tensors without data (no device,
+// no weights) and print the graph as src/gemma_model.cpp:240-248 dumps it, "node[i]: name", plus
+// each node's op — the form of the reference's tensor_dump/tensor_in_target_cgraph listing
+int graph_listing(int argc, char **argv) {
+    if (argc < 12) return 2;
+    model m;
+    m.hp = {atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8]),
+            atoi(argv[9]), atoi(argv[10])};
+    const int T = atoi(argv[11]);
+    const stage st = argc > 12 && atoi(argv[12]) ? DECODE : PREFILL;
+    const hparams &h = m.hp;
+    const ggml_type wt = (ggml_type)h.wtype;
+    const int64_t qw = (int64_t)h.n_head * h.head_dim, kvw = (int64_t)h.n_head_kv * h.head_dim;
+    ggml_init_params p = {(size_t)(h.n_layer * 9 + 2) * ggml_tensor_overhead(), nullptr, true};
+    m.weight_ctx = ggml_init(p);
+    m.token_embd = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, h.n_vocab);
+    ggml_set_name(m.token_embd, "token_embd.weight");
+    m.output_norm = ggml_new_tensor_1d(m.weight_ctx, GGML_TYPE_F32, h.n_embd);
+    ggml_set_name(m.output_norm, "output_norm.weight");
+    for (int il = 0; il < h.n_layer; ++il) {
+        layer_w L;
+        L.attn_norm = ggml_new_tensor_1d(m.weight_ctx, GGML_TYPE_F32, h.n_embd);
+        L.q = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, qw);
+        L.k = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, kvw);
+        L.v = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, kvw);
+        L.o = ggml_new_tensor_2d(m.weight_ctx, wt, qw, h.n_embd);
+        L.ffn_norm = ggml_new_tensor_1d(m.weight_ctx, GGML_TYPE_F32, h.n_embd);
+        L.gate = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, h.n_ff);
+        L.up = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_embd, h.n_ff);
+        L.down = ggml_new_tensor_2d(m.weight_ctx, wt, h.n_ff, h.n_embd);
+        const char *names[9] = {"attn_norm", "attn_q", "attn_k", "attn_v", "attn_output", "ffn_norm", "ffn_gate", "ffn_up", "ffn_down"};
+        ggml_tensor *ts[9] = {L.attn_norm, L.q, L.k, L.v, L.o, L.ffn_norm, L.gate, L.up, L.down};
+        for (int k = 0; k < 9; ++k) ggml_format_name(ts[k], "blk.%d.%s.weight", il, names[k]);
+        m.layers.push_back(L);
+    }
+    init_input_tensor(m);
+    init_kv_cache(m);
+    std::vector<int32_t> input(T, 2);
+    update_kv_cache(m, input, st);
+    m.compute_mem.resize(ggml_tensor_overhead() * 4096 + ggml_graph_overhead() + (1u << 20));
+    m.no_alloc = true;  // metadata only: the listing needs no node data
+    ggml_cgraph *g = build_compute_graph(m, input, st);
+    for (int i = 0; i < g->n_nodes; ++i) printf("node[%d]: %s\t%s\n", i, g->nodes[i]->name, ggml_op_name((enum ggml_op)g->nodes[i]->op));
+    ggml_free(m.compute_ctx);
+    ggml_backend_buffer_free(m.input_buf);
+    ggml_backend_buffer_free(m.kv_buf);
+    ggml_free(m.input_ctx);
+    ggml_free(m.kv_ctx);
+    ggml_free(m.weight_ctx);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && strcmp(argv[1], "--graph-listing") == 0) return graph_listing(argc, argv);
     const size_t alen = argc > 1 ? strlen(argv[1]) : 0;
     const bool gguf = alen > 5 && strcmp(argv[1] + alen - 5, ".gguf") == 0;
     if ((gguf && argc < 6) || (!gguf && argc < 14)) {

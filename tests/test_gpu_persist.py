@@ -92,3 +92,38 @@ def test_persist_declines_unsupported_shapes():
     e = _engine(O.TINY, n_ctx=64)
     assert not e.set_persist(1)
     e.close()
+
+
+@gpu
+def test_persist_declines_kquant():
+    """K-quant layers never take the launch: set_persist reports 0 and steps run the K-quant path"""
+    import gemma_hip as G
+    e = _engine(dict(GEMMA_2B_LAYERS, n_layer=1), n_ctx=64, wtype=G.GGML_TYPE_Q4_K)
+    assert not e.set_persist(1)
+    assert "K-quant" in G.last_error()
+    e.close()
+
+
+@gpu
+def test_persist_timeout_reported():
+    """a hand-off timeout inside the launch (forced with a 10 ns per-wait bound) must
+    fail the step, leave the launch off, and the restarted sequence must be the oracle's again"""
+    import gemma_hip as G
+    O.lib().orc_set_threads(16)
+    shape = GEMMA_2B_LAYERS
+    m = O.Model(O.make_config(shape, n_ctx=64))
+    prompt = O.make_prompt(4, shape["n_vocab"])
+    seq_ref, lg_ref = m.generate(prompt, 3)
+    e = _engine(shape, n_ctx=64)
+    assert e.set_persist(1)
+    assert e.set_persist_timeout(1) == 0
+    e.persist_err(reset=True)
+    e.begin(prompt)
+    with pytest.raises(RuntimeError, match="hand-off timeout"):
+        e.step(len(prompt) + 3, want_logits=False, use_graph=True)
+    assert not e.set_persist(-1), "the launch must be off after a timeout"
+    assert e.persist_err()[0] == 0, "the sticky word is cleared once reported"
+    lg, toks = _decode(e, prompt, 3)
+    e.close()
+    assert toks[: len(seq_ref)] == list(seq_ref)
+    assert np.array_equal(lg[len(prompt) - 1:].view(np.uint32), lg_ref.view(np.uint32))

@@ -1,0 +1,78 @@
+"""The RCCL transport of the row-split engine (BASELINE config 4) on ONE GPU.
+
+The box has one GPU and RCCL refuses two ranks per device, so N > 1 runs only on the driver's
+8-GPU node.  A 1-rank communicator (gemma_tp_unique_id + ncclCommInitRank(nranks = 1)) sends the
+engine down exactly the code the N-GPU ranks run: every activation vector and the h image through
+in-place ncclAllGather (grouped for the image), the per-rank argmax key through ncclAllGather +
+the key merge, RCCL inside the captured decode hipGraph.  Bar: tokens and every logit bit-identical
+to the CPU oracle (the reference's per-token graph, src/gemma_model.cpp:231-286 with the row
+partition of src/hpc.cpp:245-269 restated in oracle/), as the virtual-rank tests require.
+"""
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+
+gpu = pytest.mark.gpu
+
+GEMMA_7B_LAYERS = dict(n_layer=3, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, n_ff=24576, n_vocab=8192)
+
+
+def _rccl_engine(shape, n_ctx, **kw):
+    import gemma_hip as G
+    uid = G.tp_unique_id()
+    e = G.Engine(shape, n_ctx=n_ctx, device=0, tp=(1, 0, uid), **kw)
+    info = e.tp_info()
+    assert info == [1, 0, 1, 1], f"expected a 1-rank RCCL communicator, got tp_info {info}"
+    return e
+
+
+def _check(shape, n_prompt, n_decode, n_ctx=64, graph=True):
+    O.lib().orc_set_threads(16)
+    prompt = O.make_prompt(n_prompt, shape["n_vocab"])
+    m = O.Model(O.make_config(shape, n_ctx=n_ctx))
+    seq_ref, lg_ref = m.generate(prompt, n_decode)
+    m.close()
+    e = _rccl_engine(shape, n_ctx)
+    e.begin(prompt)
+    lg = e.step(len(prompt) + n_decode, want_logits=True, use_graph=graph)
+    toks = list(e.tokens()[: len(seq_ref)])
+    # without logits: graph replays back to back, tokens fed back on the device through the key gather
+    e.begin(prompt)
+    e.step(len(prompt) + n_decode, want_logits=False, use_graph=graph)
+    toks2 = list(e.tokens()[: len(seq_ref)])
+    e.close()
+    assert toks == list(seq_ref)
+    assert toks2 == list(seq_ref)
+    got = lg[len(prompt) - 1:]
+    bad = np.argwhere(got.view(np.uint32) != lg_ref.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} logits differ, first {bad[:5]}"
+
+
+@gpu
+def test_rccl_one_rank_tiny_eager_and_graph():
+    for graph in (False, True):
+        _check(dict(O.TINY), 6, 6, n_ctx=128, graph=graph)
+
+
+@gpu
+def test_rccl_one_rank_gemma2b():
+    _check(dict(O.GEMMA_2B), 5, 3)
+
+
+@gpu
+def test_rccl_one_rank_gemma7b_layers():
+    _check(dict(GEMMA_7B_LAYERS), 5, 3)
+
+
+@gpu
+def test_rccl_one_rank_declines_prefill_and_kquant():
+    import gemma_hip as G
+    e = _rccl_engine(dict(O.TINY), 64)
+    e.begin(O.make_prompt(4, O.TINY["n_vocab"]))
+    with pytest.raises(RuntimeError):
+        e.prefill(4)
+    assert not e.set_persist(1)  # the persistent launch is single-engine only
+    e.close()
+    with pytest.raises(RuntimeError):
+        G.Engine(dict(O.GEMMA_2B, n_layer=1), n_ctx=64, wtype=G.GGML_TYPE_Q4_K, tp=(1, 0, G.tp_unique_id()))
