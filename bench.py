@@ -32,6 +32,11 @@ KERNEL_NAMES = {0: "ffn gate/up matvec (+norm, +gelu*mul)", 1: "ffn down matvec 
 KERNEL_CALLS_PER_TOKEN = {0: 18, 1: 18, 2: 18, 3: 18, 4: 1}
 
 
+def log(msg):
+    """progress on stderr (the JSON line stays the only stdout line)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def make_prompt(n, n_vocab, seed=1):
     """Synthetic prompt: BOS=2 then uniform ids in [3, n_vocab) (DESIGN.md §Synthetic inputs)."""
     M = (1 << 64) - 1
@@ -371,6 +376,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    log('engine: Gemma-2B decode')
     eng = G.Engine(GEMMA_2B, n_ctx=args.ctx, wtype=wtype, device=local_rank)
     plan = eng.tune(8) if not args.no_tune else eng.plan()  # engine setup (untimed): launch shapes
     prompt = make_prompt(args.prompt, GEMMA_2B["n_vocab"])
@@ -399,11 +405,13 @@ def main():
 
     # row-split TP leg (BASELINE config 4): Gemma-7B Q4_0 batch-1 decode, weights row-split across
     # the job's GPUs with RCCL all-gathers (one rank per GPU; at N = 1 the same engine unsplit)
+    log('tp leg')
     tp = None
     if args.tp_steps > 0:
         tp = run_tp_leg(args, world, rank)
 
     # second quant format (BASELINE config 5): the same decode with Q8_0 weights (2.66 GB/token)
+    log('q8_0 leg')
     q8 = None
     if args.wtype == "q4_0" and args.q8_steps > 0:
         try:
@@ -428,6 +436,7 @@ def main():
 
     # llama.cpp's Q4_0 file layout: the same decode with a Q6_K token_embd / tied output
     # (1,544,847,360 weight bytes per token; logits through Q8_K INIT + the K-quant matvec)
+    log('q6_K output leg')
     q6o = None
     if args.wtype == "q4_0" and args.q8_steps > 0:
         try:
@@ -450,6 +459,7 @@ def main():
 
     # the reference's shipped format (src/app.cpp:36, gemma-2b-it-q4_k_m): K-quant layers (Q4_K q/k/o/
     # gate/up, Q6_K v/down) and a Q6_K token_embd / output, token by token through the K-quant matvecs
+    log('q4_k_m leg')
     kqm = None
     if args.wtype == "q4_0" and args.q8_steps > 0:
         try:
@@ -506,6 +516,7 @@ def main():
     # prefill leg (BASELINE config 3): batched prefill of a 2048-token synthetic prompt, logits for
     # every row as the reference computes them.  "exact": bit-identical to the CPU path (the
     # headline prefill_tok_s); "fast": int8/f16 MFMA, fp32 summation order differs
+    log('prefill leg')
     prefill = None
     if args.prefill > 0:
         pe = G.Engine(GEMMA_2B, n_ctx=args.prefill + 64, wtype=wtype, device=local_rank)
@@ -533,6 +544,7 @@ def main():
     # ggml-API drop-in leg: the reference's graph code (tests/ggml_driver, restating
     # src/gemma_model.cpp) driving ggml_graph_compute_with_ctx on a Gemma-2B Q4_0 GGUF of the same
     # synthetic weights; timed like src/gemma_model.cpp:552-572 (graph build + compute + greedy sample)
+    log('ggml path leg')
     ggml_leg = None
     if args.ggml_steps > 0 and rank == 0 and world == 1:
         import re
@@ -567,6 +579,7 @@ def main():
                 ggml_leg = {"error": str(ex)[:300]}
 
     # K-quant leg: Q4_K / Q6_K x Q8_K matvec alone at Gemma-2B shapes, cold weights
+    log('kquant matvec leg')
     kquant = {}
     for t, name in ((G.GGML_TYPE_Q4_K, "q4_K"), (G.GGML_TYPE_Q6_K, "q6_K")):
         for rows, K, nm in ((16384, 2048, "gate"), (2048, 16384, "down"), (256000, 2048, "output")):
@@ -576,6 +589,7 @@ def main():
                 kquant[f"{name}_{nm}"] = {"us": round(us, 3), "GB/s": round(ab.value / us / 1e3, 1)}
 
     # roofline leg: each hot matvec timed alone with hipEvents on the engine stream
+    log('roofline leg')
     kern = {}
     for k in (0, 1, 2, 3, 4):
         us, algo = eng.time_kernel(k, args.kernel_iters)
@@ -587,6 +601,7 @@ def main():
     # measured HBM read roofline on this box: streaming read of 4 GiB (defeats the Infinity Cache)
     hbm_measured = eng.L.gemma_hbm_read_gbs(local_rank, 4 << 30, 5)
 
+    log('cpu baseline')
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

@@ -95,3 +95,26 @@ def test_kquant_mul_mat_extreme_blocks(wtype):
         got = G.mul_mat(W, wtype, rows, W.shape[1], K, wdata, rs, ncols)
         bad = np.nonzero(got.view(np.uint32) != ref.view(np.uint32))
         assert bad[0].size == 0, (ncols, bad[0][:5], bad[1][:5], np.abs(got - ref).max())
+
+
+@gpu
+@pytest.mark.parametrize("wtype", [O.Q4_K, O.Q6_K], ids=["q4_K", "q6_K"])
+def test_kquant_gemm_extreme_activation_scales(wtype):
+    """the Q4_K MFMA GEMM folds 2^24 into x.d (its A operand is f16 denormals), which is
+    ggml's rounding of y.d * x.d only while that product is a normal fp32 below 2^104; columns whose
+    Q8_K scales make it subnormal or overflow the scaled form must still give ggml's bits (the kernel
+    takes the unscaled d for such super-blocks).  >= 8 columns: the GEMM path."""
+    import gemma_hip as G
+    G.lib().hpc_set_error_mode(0)
+    rows, K = 64, 2048
+    W = O.synth_kquant(wtype, 11, rows, K)
+    rng = np.random.default_rng(9)
+    scales = np.array([1e-36, 3e-38, 1e-33, 1e-30, 1e-20, 1.0, 1e20, 1e30, 1e33, 2e34, 1e35, 1.0], np.float32)
+    X = (rng.standard_normal((len(scales), K)) * scales[:, None]).astype(np.float32)
+    X[5, 256:512] *= np.float32(1e-37)  # one super-block tiny inside an ordinary column
+    wdata, rs = O.mul_mat_init(wtype, X)
+    ref = O.mul_mat(W, wtype, rows, W.shape[1], K, wdata, rs, len(scales))
+    got = G.mul_mat(W, wtype, rows, W.shape[1], K, wdata, rs, len(scales))
+    assert np.isfinite(ref).all()
+    bad = np.nonzero(got.view(np.uint32) != ref.view(np.uint32))
+    assert bad[0].size == 0, (bad[0][:5], bad[1][:5])
