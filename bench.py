@@ -132,6 +132,7 @@ def cpu_baseline(n_prompt=128, n_decode=32, threads=4, q8_decode=16, reps=3):
         return cpus
 
     def run(m, pool, th, nd, prm=prompt, n_pr=n_prompt):
+        log(f"cpu run: {('ref_pool', 'spin_pool')[pool]} x{th}, prompt {n_pr}, {nd} decode steps")
         cpus = pin(th)
         toks = np.zeros(n_pr + nd + 2, dtype=np.int32)
         pre = C.c_double()
@@ -168,6 +169,7 @@ def cpu_baseline(n_prompt=128, n_decode=32, threads=4, q8_decode=16, reps=3):
         return dt
 
     try:
+        log("cpu: oracle model (Gemma-2B Q4_0)")
         m = O.Model(O.make_config(GEMMA_2B, n_ctx=512))
         heads = [run(m, 0, threads, n_decode) for _ in range(reps)]
         vals = sorted(r["decode_tok_s"] for r in heads)
@@ -189,6 +191,7 @@ def cpu_baseline(n_prompt=128, n_decode=32, threads=4, q8_decode=16, reps=3):
         V_S, T3 = 16000, 2048
         c3 = None
         try:
+            log('cpu: config 3 sample (1 layer at T = 2048)')
             one = dict(GEMMA_2B, n_layer=1, n_vocab=V_S)
             m = O.Model(O.make_config(one, n_ctx=T3 + 64))
             pr3 = np.array(make_prompt(T3, V_S, seed=2), dtype=np.int32)
@@ -211,6 +214,7 @@ def cpu_baseline(n_prompt=128, n_decode=32, threads=4, q8_decode=16, reps=3):
         c4 = None
         try:
             nl, nd7, np7 = 2, 16, 16
+            log('cpu: config 4 sample (2 Gemma-7B layers)')
             two = dict(GEMMA_7B, n_layer=nl, n_vocab=V_S)
             m = O.Model(O.make_config(two, n_ctx=128))
             pr7 = np.array(make_prompt(np7, V_S), dtype=np.int32)
