@@ -126,8 +126,16 @@ def cpu_baseline(n_prompt=128, n_decode=32, threads=4, q8_decode=16, reps=3):
     prompt = np.array(make_prompt(n_prompt, GEMMA_2B["n_vocab"]), dtype=np.int32)
 
     def pin(th):
+        """the reference-pool x4 legs run pinned (reproducible medians); the all-core diagnostics run on
+        the process's whole affinity set: a spin pool pinned to as many CPUs as it has threads shares
+        them with the runtime's own threads and measured 0.28 tok/s on the box (2 min)"""
+        if saved_aff is None:
+            return None
+        if th != threads:
+            os.sched_setaffinity(0, saved_aff)
+            return None
         cpus = _pick_cpus(th)
-        if cpus and saved_aff is not None:
+        if cpus:
             os.sched_setaffinity(0, cpus)  # the pool's threads start after this and inherit it
         return cpus
 

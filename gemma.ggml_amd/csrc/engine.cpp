@@ -1902,6 +1902,16 @@ static int kq_expand(gemma_engine *e, const uint8_t *x, int64_t ld, int64_t K, i
     return launch_q8k_expand(a, e->stream);
 }
 
+// The exact prefill attention: on the f32 matrix cores where the shapes allow it (attn_mx.hip:
+// v_mfma_f32_16x16x4_f32 is an fmaf chain over K, so vec_dot_f16's chains ride it bit for bit),
+// else per row with v_fma_mix (k_attn_rows).  GHIP_ATT_MX=0 forces the row form (tests, A/B).
+static int launch_attn_exact(const attnp_args &at, hipStream_t s) {
+    const char *env = getenv("GHIP_ATT_MX");
+    const bool mx = !env || atoi(env) != 0;
+    if (mx && attn_mx_unsupported(at).empty()) return launch_attn_mx(at, s);
+    return launch_attn_rows(at, s);
+}
+
 static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nullptr) {
     const gemma_hip_config &c = e->cfg;
     hipStream_t s = e->stream;
@@ -1950,7 +1960,7 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
         attnp_args at;
         at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
         at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
-        if (exact ? launch_attn_rows(at, s) : launch_attn_prefill(at, s)) return -1;
+        if (exact ? launch_attn_exact(at, s) : launch_attn_prefill(at, s)) return -1;
         if (quant(QR_F32, p.ATT, nullptr, e->qw, nullptr)) return -1;
         if (gemm(L.o, EPI_ADD, p.X, p.SA, E)) return -1;
         if (quant(QR_NORM, p.SA, nullptr, E, L.ffn_norm)) return -1;
@@ -2056,7 +2066,7 @@ static int enqueue_prefill_kq(gemma_engine *e, int T) {
         attnp_args at;
         at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
         at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
-        if (launch_attn_rows(at, s)) return -1;
+        if (launch_attn_exact(at, s)) return -1;
         if (launch_quant_q8_K(p.ATT, e->qw, e->qw, T, img, ldk, s) || expand(e->qw)) return -1;
         if (mv(K.o, p.SA, E, p.X, nullptr, nullptr)) return -1;  // + inpL
         if (launch_norm_q8K(p.SA, E, L.ffn_norm, (int)E, c.eps, T, img, ldk, s) || expand(E)) return -1;

@@ -248,6 +248,10 @@ struct attnp_args {  // causal attention of T prompt tokens against the layer ca
 int launch_attn_prefill(const attnp_args &a, hipStream_t s);
 // exact rows: each prompt row with the decode attention's arithmetic (ops.hip)
 int launch_attn_rows(const attnp_args &a, hipStream_t s);
+// the same rows on the f32 matrix cores (attn_mx.hip): v_mfma_f32_16x16x4_f32 is an fmaf chain over K,
+// so vec_dot_f16's 32 chains ride K four steps at a time; "" when it runs the shapes
+std::string attn_mx_unsupported(const attnp_args &a);
+int launch_attn_mx(const attnp_args &a, hipStream_t s);
 int launch_row_argmax(const float *row, int64_t n, unsigned long long *keys, int parts, hipStream_t s);
 
 // ---- weights (ops.hip) ------------------------------------------------------------------------

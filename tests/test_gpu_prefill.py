@@ -229,3 +229,31 @@ def test_prefill_exact_gemma7b_layers():
     """Gemma-7B layer shapes (E 3072, 16 q / 16 kv heads, F 24576), 3 layers, Q4_0: every row."""
     _prefill_exact_case(dict(n_layer=3, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, n_ff=24576,
                              n_vocab=8192), 37, 128, n_decode=2)
+
+
+@gpu
+@pytest.mark.parametrize("shape,T", [(dict(n_layer=2, n_embd=2048, n_head=8, n_head_kv=1, head_dim=256, n_ff=2048,
+                                          n_vocab=4096), 700),
+                                     (dict(n_layer=2, n_embd=1024, n_head=4, n_head_kv=2, head_dim=256, n_ff=2048,
+                                           n_vocab=4096), 333),
+                                     (dict(n_layer=1, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, n_ff=2048,
+                                           n_vocab=4096), 129)])
+def test_prefill_attention_mfma_equals_rows(shape, T, monkeypatch):
+    """The exact prefill attention on the f32 matrix cores (attn_mx.hip) against the v_fma_mix row
+    form (k_attn_rows): every prompt row's logits and the decode that continues from the cache
+    bit-identical (G = 8 / 2 / 1 query heads per kv head; T not a multiple of 16 or 32)."""
+    import gemma_hip as G
+    prompt = O.make_prompt(T, shape["n_vocab"], seed=3)
+    out = {}
+    for mx in ("1", "0"):
+        monkeypatch.setenv("GHIP_ATT_MX", mx)
+        e = G.Engine(shape, n_ctx=T + 64, device=0)
+        e.begin(prompt)
+        tok, last, allv = e.prefill(T, want_all=True, exact=True)
+        lg = e.step(3, want_logits=True, use_graph=True)
+        out[mx] = (tok, allv, lg)
+        e.close()
+    assert out["1"][0] == out["0"][0]
+    bad = np.nonzero((out["1"][1].view(np.uint32) != out["0"][1].view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, (bad[:8], np.abs(out["1"][1] - out["0"][1]).max())
+    assert np.array_equal(out["1"][2].view(np.uint32), out["0"][2].view(np.uint32))
