@@ -73,7 +73,9 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
     const int i_last = min(i0 + P - 1, a.T - 1);
     int L = 32 * ((i_last + 1) / 32 + 1);
     if (L > a.n_kv) L = a.n_kv;
-    float *S = (float *)smem;  // [16][L]; P16 row m over S row m (in place)
+    // S [16][LS], LS = L + 4: the 16 rows of an MFMA operand read sit 16 B apart in the banks
+    const int LS = L + 4;
+    float *S = (float *)smem;  // P16 row m over S row m (in place)
     const int m_l = lane & 15, kk = lane >> 4;  // MFMA A row / B column, K index of this lane
 
     // ---- q operands: row m_l = (position, head), elements 32(4t + kk) + c, t = 0, 1 ----------
@@ -93,14 +95,25 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
     // ---- KQ: 16-position key tiles; wave w takes tiles w, w + 8, ... ----------------------------
     const int n_keys = i_last + 1;  // positions past the block's last row are all masked
     const int n_kt = (n_keys + 15) / 16;
-    for (int kt = wave; kt < n_kt; kt += MX_WAVES) {
-        const int j = kt * 16 + m_l;  // this lane's key row (B column n = lane & 15)
+    // this lane's 128 B of key row kt*16 + (lane & 15); the next tile's loads are issued before
+    // the current tile's MFMAs
+    auto kload = [&](int kt, uint4 kv[2][4]) {
+        const int j = kt * 16 + m_l;
         const uint16_t *kr = a.kc + (int64_t)(j < n_keys ? j : 0) * kvw + (int64_t)kvh * MX_HD;
-        uint4 kv[2][4];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int q = 0; q < 4; ++q) kv[t][q] = *(const uint4 *)(kr + 32 * (4 * t + kk) + 8 * q);
+    };
+    uint4 kn[2][4];
+    if (wave < n_kt) kload(wave, kn);
+    for (int kt = wave; kt < n_kt; kt += MX_WAVES) {
+        uint4 kv[2][4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) kv[t][q] = kn[t][q];
+        if (kt + MX_WAVES < n_kt) kload(kt + MX_WAVES, kn);
         mx4 acc[32];
         const mx4 z = {0.0f, 0.0f, 0.0f, 0.0f};
         {
@@ -118,14 +131,14 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
         for (int r = 0; r < 4; ++r) {
             const float kq = fold32(acc, r);
             const int m = 4 * kk + r;
-            if (jn < L) S[m * L + jn] = kq * 1.0f + 0.0f;  // ggml: kq * scale + mask (0 where unmasked)
+            if (jn < L) S[m * LS + jn] = kq * 1.0f + 0.0f;  // ggml: kq * scale + mask (0 where unmasked)
         }
     }
     __syncthreads();
     // ---- soft_max_ext per row (k_attn_rows' arithmetic): wave w takes rows 2w, 2w + 1 ---------
     for (int m = wave; m < 16; m += MX_WAVES) {
         const int ip = i0 + m / G;
-        float *Sr = S + m * L;
+        float *Sr = S + m * LS;
         uint16_t *Pr = (uint16_t *)Sr;
         if (ip >= a.T) {  // padding row of the last block: zeros (its outputs are not stored)
             for (int j = lane; j < L; j += 64) Pr[j] = 0;
@@ -161,23 +174,26 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
     for (int dt = wave; dt < MX_HD / 16; dt += MX_WAVES) {
         const int d = dt * 16 + m_l;  // this lane's V row (B column)
         const uint16_t *vr = a.vc + ((int64_t)kvh * MX_HD + d) * a.ctx;
-        const uint16_t *pr = (const uint16_t *)(S + m_l * L);  // A row m_l of P16
+        const uint16_t *pr = (const uint16_t *)(S + m_l * LS);  // A row m_l of P16
         mx4 acc[32];
 #pragma unroll
         for (int c = 0; c < 32; ++c) acc[c] = (mx4){0.0f, 0.0f, 0.0f, 0.0f};
+        // this lane's V step of group u (positions 32(4u + kk) ..), one group ahead of its MFMAs
+        auto vload = [&](int u, uint4 vv[4]) {
+            const int e0 = 32 * (4 * u + kk);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vv[q] = e0 < L ? *(const uint4 *)(vr + e0 + 8 * q) : make_uint4(0u, 0u, 0u, 0u);
+        };
+        uint4 vn[4];
+        vload(0, vn);
         for (int u = 0; u < n_sg; ++u) {
             const int e0 = 32 * (4 * u + kk);  // this lane's step: positions e0 .. e0 + 31
             uint4 pv[4], vv[4];
-            if (e0 < L) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    pv[q] = *(const uint4 *)(pr + e0 + 8 * q);
-                    vv[q] = *(const uint4 *)(vr + e0 + 8 * q);
-                }
-            } else {
+            for (int q = 0; q < 4; ++q) vv[q] = vn[q];
+            if (u + 1 < n_sg) vload(u + 1, vn);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) pv[q] = vv[q] = make_uint4(0u, 0u, 0u, 0u);
-            }
+            for (int q = 0; q < 4; ++q) pv[q] = e0 < L ? *(const uint4 *)(pr + e0 + 8 * q) : make_uint4(0u, 0u, 0u, 0u);
             float pf[32], vf[32];
             widen32(pv, pf);
             widen32(vv, vf);
@@ -206,7 +222,7 @@ std::string attn_mx_unsupported(const attnp_args &a) {
     (void)P;
     int L = 32 * ((i_last + 1) / 32 + 1);
     if (L > a.n_kv) L = a.n_kv;
-    if ((size_t)16 * L * 4 > 160 * 1024) return "scores of 16 rows exceed the LDS (n_kv > 2560)";
+    if ((size_t)16 * (L + 4) * 4 > 160 * 1024) return "scores of 16 rows exceed the LDS (n_kv > 2556)";
     return "";
 }
 
@@ -219,7 +235,7 @@ int launch_attn_mx(const attnp_args &a, hipStream_t s) {
     const int G = a.H / a.Hkv, P = 16 / G;
     int L = 32 * (a.T / 32 + 1);
     if (L > a.n_kv) L = a.n_kv;
-    const size_t lds = (size_t)16 * L * 4;
+    const size_t lds = (size_t)16 * (L + 4) * 4;
     GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_mx, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int nblk = (a.T + P - 1) / P;
     hipLaunchKernelGGL(k_attn_mx, dim3((unsigned)(nblk * a.Hkv)), dim3(MX_THREADS), lds, s, a);

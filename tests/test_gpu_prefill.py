@@ -247,7 +247,7 @@ def test_prefill_attention_mfma_equals_rows(shape, T, monkeypatch):
     out = {}
     for mx in ("1", "0"):
         monkeypatch.setenv("GHIP_ATT_MX", mx)
-        e = G.Engine(shape, n_ctx=T + 64, device=0)
+        e = G.Engine(shape, n_ctx=(T + 64) // 32 * 32 + 32, device=0)
         e.begin(prompt)
         tok, last, allv = e.prefill(T, want_all=True, exact=True)
         lg = e.step(3, want_logits=True, use_graph=True)
