@@ -161,6 +161,9 @@ constexpr int KQ_PF = GHIP_KQ_PF;
 #ifndef GHIP_KQ_EARLY
 #define GHIP_KQ_EARLY 1  // 1: first weight round issued before the Q8_K staging
 #endif
+#ifndef GHIP_KQ_NORM1
+#define GHIP_KQ_NORM1 1  // 1: the norm prologue's tree with one barrier (every wave runs the lane levels)
+#endif
 
 // the column's Q8_K image into LDS: 16-B loads, all of a thread's loads issued before the first
 // store (a plain copy loop waits one memory round trip per iteration, behind the weight loads
@@ -242,7 +245,25 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
             part[j] = pj;
         }
         int n = a.nsb * 64;
-        if (two) {
+        if (two && nw == 4 && GHIP_KQ_NORM1) {
+            // the same pairwise tree (h = (n+1)/2 over nw*64 = 256 partials: i + 128, then i + 64,
+            // then the six lane levels), with ONE barrier: every wave reads its lane's four wave
+            // partials and runs the lane levels itself, so no wave waits for wave 0's tree
+            red[wave * 64 + lane] = part[0] + part[XJ - 1];
+            __syncthreads();
+            const double r0 = red[lane], r1 = red[64 + lane], r2 = red[128 + lane], r3 = red[192 + lane];
+            double v = (r0 + r2) + (r1 + r3);
+            for (int m = 64; m > 1;) {
+                const int h = (m + 1) >> 1;
+                const double o = __shfl_down(v, h);
+                if (lane + h < m) v += o;
+                m = h;
+            }
+            v = __shfl(v, 0);
+            const float mean = (float)(v / (double)(a.nsb * 256));
+            scale = 1.0f / sqrtf(mean + a.eps);
+            n = 0;  // done
+        } else if (two) {
             red[wave * 64 + lane] = part[0] + part[XJ - 1];
             n = nw * 64;
         } else {
@@ -250,6 +271,7 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
             for (int j = 0; j < XJ; ++j)
                 if (wave + nw * j < a.nsb) red[(wave + nw * j) * 64 + lane] = part[j];
         }
+        if (n) {
         __syncthreads();
         while (n > 64) {  // cross-wave levels through LDS
             const int h = (n + 1) >> 1;
@@ -270,6 +292,7 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
         __syncthreads();
         const float mean = (float)(red[0] / (double)(a.nsb * 256));
         scale = 1.0f / sqrtf(mean + a.eps);
+        }
     }
     float y[XJ][4];
 #pragma unroll
