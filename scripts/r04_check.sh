@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-4 GPU pass: the new prefill attention and GEMM change (tests, timing, rocprof, PMC), the
+# K-quant prologue change (tests + A/B against ab_libs/libnorm0.so), decode phase stamps.
+# usage (repo root, GPU box): bash scripts/r04_check.sh <tag> [steps...]   steps: pf kq stamp pmc
+set -o pipefail
+TAG=${1:-r04}; shift
+STEPS=${@:-"pf kq stamp pmc"}
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+for st in $STEPS; do
+  case $st in
+    pf)
+      timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_prefill.py -m gpu -k "exact or mfma" > $O/pf_tests.log 2>&1 || { tail -30 $O/pf_tests.log; exit 1; }
+      tail -1 $O/pf_tests.log
+      for mx in 1 0; do GHIP_ATT_MX=$mx timeout -k 10 120 python scripts/prof_prefill.py 2048 1 3 > $O/pf_t_$mx.txt 2>&1 || exit 1; echo "GHIP_ATT_MX=$mx"; cat $O/pf_t_$mx.txt; done
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_pf -o run -- python3 scripts/prof_prefill.py 2048 1 1 > $O/prof_pf.log 2>&1 || { tail -5 $O/prof_pf.log; exit 1; }
+      f=$(find $O/prof_pf -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp $f $O/kernel_stats_prefill.csv && head -8 $O/kernel_stats_prefill.csv | cut -c1-160 ;;
+    kq)
+      timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_kquants.py tests/test_gpu_engine_gguf.py -m gpu > $O/kq_tests.log 2>&1 || { tail -30 $O/kq_tests.log; exit 1; }
+      tail -1 $O/kq_tests.log
+      for rep in 1 2 3; do
+        GHIP_LIB=$PWD/ab_libs/libnorm0.so timeout -k 10 120 python scripts/run_kqm.py 64 2>&1 | sed "s/^/base /" || exit 1
+        timeout -k 10 120 python scripts/run_kqm.py 64 2>&1 | sed "s/^/new  /" || exit 1
+      done ;;
+    stamp)
+      GHIP_LIB=$PWD/ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 9 > $O/stamp_step.log 2>&1 || { tail -20 $O/stamp_step.log; exit 1; }
+      cat $O/stamp_step.log ;;
+    pmc)
+      bash scripts/pmc_prefill.sh $TAG/pmc 2048 > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
+      tail -24 $O/pmc.log ;;
+  esac
+done
