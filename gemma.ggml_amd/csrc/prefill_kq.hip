@@ -304,15 +304,16 @@ k_gemm_kq(kqg_args a) {
     const uint8_t *ab = WA + (kg * M + wr) * 16;
     const uint8_t *bb0 = XB + (kg * N + wt + (l16 ^ kg)) * 16, *bb1 = XB + (kg * N + wt + (l16 ^ (kg + 4))) * 16;
 
-    // SLOW (Q4_K with GHIP_GQ_DEN only): some y.d * x.d of the tile is outside [2^-126, 2^104) in
-    // magnitude, where rounding (y.d * x.d * 2^24) is not rounding (y.d * x.d) scaled by 2^24 (a
-    // subnormal or overflowing product); those super-blocks take ggml's d = y.d * x.d unscaled and
-    // the MFMA's isum * 2^-24 scaled back to isum (exact), i.e. ggml's fmaf(d, isum, acc)
-    auto compute = [&](auto slow_t) {
-        constexpr bool SLOW = decltype(slow_t)::value;
+    // Q4_K with GHIP_GQ_DEN: DW = x.d * 2^24 and the MFMA returns isum * 2^-24, so ggml's
+    // fmaf(d, isum, acc) with d = y.d * x.d is fmaf(d * 2^24, isum * 2^-24, acc) exactly — provided
+    // d * 2^24 is d scaled, not a fresh rounding.  d is therefore rounded as ggml rounds it (unscaled,
+    // a subnormal when |y.d * x.d| < 2^-126) and then scaled by 2^24 (exact): (y.d * (DW * 2^-24)) *
+    // 2^24.  Assumption kept: |y.d * x.d| < 2^104, i.e. activations below ~3e26 for any
+    // f16 x.d (beyond, d * 2^24 overflows; ggml's d would not)
+    auto compute = [&]() {
         float dd[2][4], dm[2][4];
         float4 w4 = *(const float4 *)&DW[wr + 4 * kg];
-        if constexpr (SLOW) {
+        if constexpr (Q4 && GHIP_GQ_DEN) {
             constexpr float inv = 1.0f / 16777216.0f;  // exact: DW = x.d * 2^24
             w4.x *= inv; w4.y *= inv; w4.z *= inv; w4.w *= inv;
         }
@@ -322,6 +323,10 @@ k_gemm_kq(kqg_args a) {
         for (int ct = 0; ct < 2; ++ct) {
             const float yd = DX[wt + 16 * ct + l16];
             dd[ct][0] = yd * w4.x; dd[ct][1] = yd * w4.y; dd[ct][2] = yd * w4.z; dd[ct][3] = yd * w4.w;
+            if constexpr (Q4 && GHIP_GQ_DEN) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dd[ct][i] = pin(dd[ct][i]) * 16777216.0f;
+            }
             if constexpr (Q4) {
                 const float ny = -yd;
                 dm[ct][0] = ny * m4.x; dm[ct][1] = ny * m4.y; dm[ct][2] = ny * m4.z; dm[ct][3] = ny * m4.w;
@@ -351,8 +356,7 @@ k_gemm_kq(kqg_args a) {
                     if constexpr (!Q4) D = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b, D, 0, 0, 0);
                 }
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    acc[l][ct][i] = __builtin_fmaf(dd[ct][i], SLOW ? D[i] * 16777216.0f : D[i], acc[l][ct][i]);
+                for (int i = 0; i < 4; ++i) acc[l][ct][i] = __builtin_fmaf(dd[ct][i], D[i], acc[l][ct][i]);
             }
         }
         if constexpr (Q4 && !(GQ_ABL & 8)) {
@@ -375,24 +379,7 @@ k_gemm_kq(kqg_args a) {
         lstore();
         __syncthreads();
         if (sb + 1 < a.nsb && !(GQ_ABL & 4)) gload(sb + 1);
-        if (!(GQ_ABL & 2)) {
-            bool slow = false;
-            if constexpr (Q4 && GHIP_GQ_DEN) {  // the tile's scaled d values of this super-block
-                const float4 w4 = *(const float4 *)&DW[wr + 4 * kg];
-                const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-                for (int ct = 0; ct < 2; ++ct) {
-                    const float yd = DX[wt + 16 * ct + l16];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const float d = fabsf(yd * wv[i]);
-                        slow |= (d != 0.0f && d < 0x1p-102f) || d == INFINITY;
-                    }
-                }
-            }
-            if (__any(slow)) compute(std::true_type{});
-            else compute(std::false_type{});
-        }
+        if (!(GQ_ABL & 2)) compute();
         __syncthreads();
     }
 

@@ -100,10 +100,10 @@ def test_kquant_mul_mat_extreme_blocks(wtype):
 @gpu
 @pytest.mark.parametrize("wtype", [O.Q4_K, O.Q6_K], ids=["q4_K", "q6_K"])
 def test_kquant_gemm_extreme_activation_scales(wtype):
-    """the Q4_K MFMA GEMM folds 2^24 into x.d (its A operand is f16 denormals), which is
-    ggml's rounding of y.d * x.d only while that product is a normal fp32 below 2^104; columns whose
-    Q8_K scales make it subnormal or overflow the scaled form must still give ggml's bits (the kernel
-    takes the unscaled d for such super-blocks).  >= 8 columns: the GEMM path."""
+    """the Q4_K MFMA GEMM folds 2^24 into x.d (its A operand is f16 denormals); it rounds
+    d = y.d * x.d unscaled, as ggml does, and scales it by 2^24 afterwards, so columns whose Q8_K scales
+    make d subnormal (column 0 here: |d| ~ 1e-40) still give ggml's bits.  The documented bound is
+    |y.d * x.d| < 2^104 (the largest column here reaches 9.8e30 of 2.0e31).  >= 8 columns: the GEMM."""
     import gemma_hip as G
     G.lib().hpc_set_error_mode(0)
     rows, K = 64, 2048
