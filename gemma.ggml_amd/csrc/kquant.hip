@@ -245,14 +245,29 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
             part[j] = pj;
         }
         int n = a.nsb * 64;
-        if (two && nw == 4 && GHIP_KQ_NORM1) {
-            // the same pairwise tree (h = (n+1)/2 over nw*64 = 256 partials: i + 128, then i + 64,
-            // then the six lane levels), with ONE barrier: every wave reads its lane's four wave
-            // partials and runs the lane levels itself, so no wave waits for wave 0's tree
-            red[wave * 64 + lane] = part[0] + part[XJ - 1];
+        const int R = two ? nw : a.nsb;  // rows of 64 partials in the tree
+        if (GHIP_KQ_NORM1 && (R == 2 || R == 4 || R == 8)) {
+            // the same pairwise tree (h = n/2 per level over R rows of 64 partials, then the six lane
+            // levels) with ONE barrier: every wave reads its lane's R partials and runs the row levels
+            // in registers and the lane levels itself, so no wave waits for wave 0's tree
+            if (two) {
+                red[wave * 64 + lane] = part[0] + part[XJ - 1];
+            } else {
+#pragma unroll
+                for (int j = 0; j < XJ; ++j)
+                    if (wave + nw * j < a.nsb) red[(wave + nw * j) * 64 + lane] = part[j];
+            }
             __syncthreads();
-            const double r0 = red[lane], r1 = red[64 + lane], r2 = red[128 + lane], r3 = red[192 + lane];
-            double v = (r0 + r2) + (r1 + r3);
+            double rv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) rv[k] = k < R ? red[k * 64 + lane] : 0.0;
+#pragma unroll
+            for (int h = 4; h >= 1; h >>= 1)
+                if (h < R)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (k < h) rv[k] += rv[k + h];
+            double v = rv[0];
             for (int m = 64; m > 1;) {
                 const int h = (m + 1) >> 1;
                 const double o = __shfl_down(v, h);
