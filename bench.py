@@ -294,9 +294,10 @@ def prefill_roofline(T, prefill):
             pmc = json.load(f)
         keys = ("mfma_util", "lds_busy", "lds_bank_conflict_frac", "valu_inst_per_wave_cycle", "wait_any_frac", "what")
         src = os.path.relpath(path, ROOT)
-        for k_name, field in (("k_gemm_x", "pmc_exact_gemm"), ("k_attn_rows", "pmc_exact_attention")):
-            if k_name in pmc:
-                out[field] = dict({k: pmc[k_name][k] for k in keys if k in pmc[k_name]}, source=src)
+        for names, field in ((("k_gemm_x",), "pmc_exact_gemm"), (("k_attn_mx", "k_attn_rows"), "pmc_exact_attention")):
+            k_name = next((n for n in names if n in pmc), None)
+            if k_name:
+                out[field] = dict({k: pmc[k_name][k] for k in keys if k in pmc[k_name]}, kernel=k_name, source=src)
     except Exception:
         pass
     return out

@@ -422,16 +422,18 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
         const uint16_t *vr = a.vc + ((int64_t)kvh * hd + d) * a.ctx;
         const float vx = d == d0 ? vx0 : ld1<SC1>(vh + d);
-        auto patch = [&](uint4 &xv, int e0) {  // this token's V: its cache write may not be visible
-            if (pos >= e0 && pos < e0 + 8) {
-                const uint32_t hv = f2h(vx), sh = 16 * ((pos - e0) & 1);
-                const uint32_t msk = ~(0xFFFFu << sh);
-                switch ((pos - e0) >> 1) {
-                    case 0: xv.x = (xv.x & msk) | (hv << sh); break;
-                    case 1: xv.y = (xv.y & msk) | (hv << sh); break;
-                    case 2: xv.z = (xv.z & msk) | (hv << sh); break;
-                    default: xv.w = (xv.w & msk) | (hv << sh); break;
-                }
+        // this token's V: its cache write may not be visible.  Element pos sits in step pos/32, on
+        // quad lane (pos/8)%4, dword (pos%8)/2, half pos%2 — all wave-uniform but the lane test, so
+        // the patch holds no per-step VGPRs (the per-step e0 form was hoisted and spilled)
+        const int p_s = pos >> 5, p_t = (pos >> 3) & 3, p_w = (pos >> 1) & 3;
+        const uint32_t p_sh = 16 * (pos & 1), p_msk = ~(0xFFFFu << p_sh);
+        auto patch = [&](uint4 &xv, int s) {
+            if (s == p_s && t4 == p_t) {
+                const uint32_t hv = f2h(vx) << p_sh;
+                if (p_w == 0) xv.x = (xv.x & p_msk) | hv;
+                else if (p_w == 1) xv.y = (xv.y & p_msk) | hv;
+                else if (p_w == 2) xv.z = (xv.z & p_msk) | hv;
+                else xv.w = (xv.w & p_msk) | hv;
             }
         };
         if (n_kv <= 256) {
@@ -451,9 +453,8 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 if (s * 32 >= n_kv) break;
-                const int e0 = s * 32 + t4 * 8;
                 uint4 xv = xs8[s];
-                patch(xv, e0);
+                patch(xv, s);
                 f16_step8(acc, xv, pr8[s]);
             }
         } else
@@ -468,16 +469,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             } else {
                 xv = *(const uint4 *)(vr + e0);
             }
-            if (pos >= e0 && pos < e0 + 8) {  // this token's V: its cache write may not be visible
-                const uint32_t hv = f2h(vx), sh = 16 * ((pos - e0) & 1);
-                const uint32_t msk = ~(0xFFFFu << sh);
-                switch ((pos - e0) >> 1) {
-                    case 0: xv.x = (xv.x & msk) | (hv << sh); break;
-                    case 1: xv.y = (xv.y & msk) | (hv << sh); break;
-                    case 2: xv.z = (xv.z & msk) | (hv << sh); break;
-                    default: xv.w = (xv.w & msk) | (hv << sh); break;
-                }
-            }
+            patch(xv, s);
             f16_step8(acc, xv, *(const uint4 *)(P16 + e0));
         }
         const float o = quad_reduce_f16(acc);

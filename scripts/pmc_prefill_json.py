@@ -13,7 +13,9 @@ root, out = sys.argv[1], sys.argv[2]
 KERNELS = {
     "k_gemm_x": "exact Q4_0 prefill GEMMs (all 18 layers + logits, one T=2048 pass); MFMA util counts ISSUED "
                 "MFMA cycles: the lane-masked f16 MFMAs carry 4x the useful products (DESIGN.md §5b)",
-    "k_attn_rows": "exact prefill attention (per row, v_fma_mix chains; no MFMA by construction)",
+    "k_attn_rows": "exact prefill attention, row form (per row, v_fma_mix chains; GHIP_ATT_MX=0)",
+    "k_attn_mx": "exact prefill attention on the f32 matrix cores (vec_dot_f16's 32 fmaf chains on "
+                 "v_mfma_f32_16x16x4_f32, four K steps per MFMA; DESIGN.md §5b)",
     "k_gemm_kq": "exact K-quant prefill GEMMs (Q4_K_M layout, dense lane-major MFMA; Q6_K issues 2 MFMAs per "
                  "product, the even part and the low bit; DESIGN.md §5c)",
 }

@@ -26,6 +26,22 @@ for st in $STEPS; do
     stamp)
       GHIP_LIB=$PWD/ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 9 > $O/stamp_step.log 2>&1 || { tail -20 $O/stamp_step.log; exit 1; }
       cat $O/stamp_step.log ;;
+    attn)
+      # decode attention without the KQV-phase spills (new) vs the spilling build (base) and K prefetch 8
+      timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_ops.py -m gpu -k "decode or attn or attention" > $O/attn_tests.log 2>&1 || { tail -30 $O/attn_tests.log; exit 1; }
+      tail -1 $O/attn_tests.log
+      for v in base new akpf8; do
+        L=""; [ $v != new ] && L=$PWD/ab_libs/lib$v.so
+        GHIP_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_$v -o run -- python3 bench.py --no-cpu --prefill 0 --tp-steps 0 --q8-steps 0 --ggml-steps 0 --steps 32 > $O/prof_$v.json 2> $O/prof_$v.err || { tail -5 $O/prof_$v.err; exit 1; }
+        f=$(find $O/prof_$v -name "*kernel_stats.csv" | head -1)
+        echo "== $v $(python3 -c "import json; d=json.load(open('$O/prof_$v.json')); print(d['value'], d['ms_per_step'])")"
+        grep -E "k_attn_head" $f | cut -d, -f1-8 | cut -c1-200
+      done
+      for rep in 1 2; do for v in base new akpf8; do
+        L=""; [ $v != new ] && L=$PWD/ab_libs/lib$v.so
+        GHIP_LIB=$L timeout -k 10 240 python bench.py --no-cpu --prefill 0 --tp-steps 0 --q8-steps 0 --ggml-steps 0 > $O/ab_$v$rep.json 2> $O/ab_$v$rep.err || { tail -20 $O/ab_$v$rep.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/ab_$v$rep.json')); print('$v', d['value'], d['ms_per_step'], (d.get('q4_k_m_decode') or {}).get('tok_s'))"
+      done; done ;;
     pmc)
       bash scripts/pmc_prefill.sh $TAG/pmc 2048 > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
       tail -24 $O/pmc.log ;;
