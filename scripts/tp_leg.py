@@ -32,15 +32,21 @@ def main():
     import gemma_hip as G
     from bench import GEMMA_7B, make_prompt
     wtype = G.GGML_TYPE_Q4_0 if wtype_s == "q4_0" else G.GGML_TYPE_Q8_0
-    rid = None
     if world > 1:
         dist.init_process_group(backend="gloo", init_method="env://")
+
+    def new_id():
+        """A fresh RCCL unique id for ONE communicator (an id serves a single ncclCommInitRank round:
+        its bootstrap root leaves once every rank has joined, so a second init on it fails with
+        "remote process exited").  N > 1: rank 0 makes it and broadcasts it over gloo."""
+        if world == 1:
+            return G.tp_unique_id()
         idt = torch.zeros(256, dtype=torch.uint8)
         if rank == 0:
             raw = G.tp_unique_id()
             idt[: len(raw)] = torch.tensor(list(raw), dtype=torch.uint8)
         dist.broadcast(idt, 0)
-        rid = bytes(idt.numpy())
+        return bytes(idt.numpy())
 
     def sync():
         torch.cuda.synchronize(local_rank)
@@ -82,12 +88,13 @@ def main():
         re_.close()
     if world > 1:
         dist.broadcast(ref, 0)
-    else:
-        rid = G.tp_unique_id()  # N = 1: a 1-rank RCCL communicator, so the timed engine runs the transport
-    # checked: the RCCL ranks (N > 1) or, at N = 1, 8 virtual ranks AND the 1-rank RCCL engine
-    splits = [(world, rank, rid)] if world > 1 else [(8, 0, None), (1, 0, rid)]
+    # checked: the RCCL ranks (N > 1) or, at N = 1, 8 virtual ranks AND a 1-rank RCCL engine (so the
+    # timed engine below runs the transport); every communicator gets its own id
+    splits = [(world, rank, "rccl")] if world > 1 else [(8, 0, None), (1, 0, "rccl")]
     nbad = 0
     for split in splits:
+        if split[2] == "rccl":
+            split = (split[0], split[1], new_id())
         ce = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=split, out_gain=OUT_GAIN)
         ce.begin(prompt)
         got = row_hashes(ce.step(n_check, want_logits=True, use_graph=True))
@@ -101,7 +108,7 @@ def main():
             print(json.dumps({"error": f"row-split logits differ from the unsplit engine: {int(bad.item())} rows over all ranks"}), flush=True)
         sys.exit(3)
 
-    te = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=(world, rank, rid), out_gain=OUT_GAIN)
+    te = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=(world, rank, new_id()), out_gain=OUT_GAIN)
     plan = te.tune(6) if tune else te.plan()
     te.begin(prompt)
     te.step(16 + 4, use_graph=True)

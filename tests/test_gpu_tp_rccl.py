@@ -76,3 +76,39 @@ def test_rccl_one_rank_declines_prefill_and_kquant():
     e.close()
     with pytest.raises(RuntimeError):
         G.Engine(dict(O.GEMMA_2B, n_layer=1), n_ctx=64, wtype=G.GGML_TYPE_Q4_K, tp=(1, 0, G.tp_unique_id()))
+
+
+@gpu
+def test_rccl_unique_id_serves_one_communicator():
+    """Two communicators in one process each need their own id (the bench's TP leg builds a parity
+    engine and then the timed engine): a fresh id per engine works, in sequence and side by side."""
+    import gemma_hip as G
+    shape = dict(O.TINY)
+    a = G.Engine(shape, n_ctx=64, device=0, tp=(1, 0, G.tp_unique_id()))
+    b = G.Engine(shape, n_ctx=64, device=0, tp=(1, 0, G.tp_unique_id()))
+    assert a.tp_info() == [1, 0, 1, 1] and b.tp_info() == [1, 0, 1, 1]
+    prompt = O.make_prompt(4, shape["n_vocab"])
+    outs = []
+    for e in (a, b):
+        e.begin(prompt)
+        outs.append(e.step(len(prompt) + 2, want_logits=True, use_graph=True))
+        e.close()
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+@gpu
+def test_bench_tp_leg_runs_at_one_gpu():
+    """bench.py's config-4 leg (scripts/tp_leg.py) end to end at N = 1: unsplit reference, 8 virtual
+    ranks and a 1-rank RCCL engine checked bit-exact, then the timed 1-rank RCCL engine."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "tp_leg.py"), "4", "q4_0", "0"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "error" not in line, line
+    assert line["parity_check"]["mismatched_rows_all_ranks"] == 0 and line["tok_s"] > 0
