@@ -30,6 +30,10 @@ namespace ghip {
 namespace {
 
 typedef float mx4 __attribute__((ext_vector_type(4)));
+#ifndef GHIP_MX_ABL
+#define GHIP_MX_ABL 0  // timing ablations only (wrong results): 1 K rows all row 0, 2 V rows all row 0, 4 no softmax passes,
+                       // 8 no KQV, 16 no KQ
+#endif
 constexpr int MX_THREADS = 512, MX_WAVES = MX_THREADS / 64, MX_HD = 256;
 
 // ggml_vec_dot_f16's fold of the 32 chain values of one output (reduce_f16_acc, attn_impl.h)
@@ -99,7 +103,7 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
     // the current tile's MFMAs
     auto kload = [&](int kt, uint4 kv[2][4]) {
         const int j = kt * 16 + m_l;
-        const uint16_t *kr = a.kc + (int64_t)(j < n_keys ? j : 0) * kvw + (int64_t)kvh * MX_HD;
+        const uint16_t *kr = a.kc + (int64_t)((GHIP_MX_ABL & 1) ? 0 : j < n_keys ? j : 0) * kvw + (int64_t)kvh * MX_HD;
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -107,7 +111,7 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
     };
     uint4 kn[2][4];
     if (wave < n_kt) kload(wave, kn);
-    for (int kt = wave; kt < n_kt; kt += MX_WAVES) {
+    for (int kt = wave; kt < ((GHIP_MX_ABL & 16) ? 0 : n_kt); kt += MX_WAVES) {
         uint4 kv[2][4];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -136,7 +140,7 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
     }
     __syncthreads();
     // ---- soft_max_ext per row (k_attn_rows' arithmetic): wave w takes rows 2w, 2w + 1 ---------
-    for (int m = wave; m < 16; m += MX_WAVES) {
+    for (int m = wave; m < ((GHIP_MX_ABL & 4) ? 0 : 16); m += MX_WAVES) {
         const int ip = i0 + m / G;
         float *Sr = S + m * LS;
         uint16_t *Pr = (uint16_t *)Sr;
@@ -171,9 +175,9 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
     // ---- KQV: out[m][d] = vec_dot_f16 over the row's n_kv of P16[m] and V[d]; wave w takes the
     // 16-dim tiles w, w + 8; steps 4u .. 4u + 3 of chain c are one MFMA
     const int n_sg = (L / 32 + 3) / 4;  // step groups (steps past L: zero operands)
-    for (int dt = wave; dt < MX_HD / 16; dt += MX_WAVES) {
+    for (int dt = wave; dt < ((GHIP_MX_ABL & 8) ? 0 : MX_HD / 16); dt += MX_WAVES) {
         const int d = dt * 16 + m_l;  // this lane's V row (B column)
-        const uint16_t *vr = a.vc + ((int64_t)kvh * MX_HD + d) * a.ctx;
+        const uint16_t *vr = a.vc + ((int64_t)kvh * MX_HD + ((GHIP_MX_ABL & 2) ? 0 : d)) * a.ctx;
         const uint16_t *pr = (const uint16_t *)(S + m_l * LS);  // A row m_l of P16
         mx4 acc[32];
 #pragma unroll

@@ -336,6 +336,9 @@ static_assert(XN * XKB * 64 / 16 % XNT == 0, "token records");
 #ifndef GHIP_XZS
 #define GHIP_XZS 1  // W32: inactive lanes' zero reads spread over free bank slots (0: one shared slot)
 #endif
+#ifndef GHIP_XWFR
+#define GHIP_XWFR 9  // W32 fragment-row pitch in 16-B slots (9: the active lanes of a b128 group on distinct banks)
+#endif
 #ifndef GHIP_XMASK
 #define GHIP_XMASK 0  // 1: EXEC-masked A reads for the inactive lanes (measured slower: 99.6 vs 88.0 ms)
 #endif
@@ -358,7 +361,7 @@ k_gemm_x(gemm_args g) {
     // + a zero region the inactive lanes read at the same strides (no per-lane select)
     // W32 pads the fragment rows to 9 x 16 B: the 8 active lanes of a ds_read_b128 lane group then
     // hit distinct banks (rows 2 apart would share them at 8 x 16 B)
-    constexpr int WFR = W32 ? 9 : 8;
+    constexpr int WFR = W32 ? GHIP_XWFR : 8;
     // compact W32 image: 8 B per (block, row, lane), rows padded to 10 x 8 B (distinct banks for the
     // 16 active lanes of a ds_read_b64 lane group); the LDS saved fits a third workgroup per CU
     constexpr bool CW = W32 && GHIP_XCOMPACT;
