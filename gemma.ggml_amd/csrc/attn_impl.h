@@ -53,6 +53,7 @@ constexpr int ATT_QUADS = ATT_THREADS / 4;  // one KQ (position, head) or KQV (d
 constexpr int ATT_VW = 256;                 // V positions staged in LDS per dimension row (n_kv <= 256)
 constexpr int ATT_STG = 2;                  // staging uint4 per thread for each of K and V
 constexpr int ATT_MAXWG = 256;              // co-resident workgroups (in-kernel hand-off)
+constexpr int ATT_VDMA_PITCH = 576;         // bytes per V row in the per-head form's LDS copy
 
 // ggml_vec_dot_f16 with accumulator row j = t4 held by lane t4 of a quad: fold the
 // quad exactly as sum0+=sum2, sum1+=sum3, sum0+=sum1 (xor-2 then xor-1), then halves and hadds.
@@ -201,12 +202,18 @@ constexpr int AH_KPF = GHIP_AH_KPF;  // K steps (of 32 elements) prefetched per 
 constexpr int AH_VPF = GHIP_AH_VPF;  // V steps (of 32 positions) prefetched per lane: n_kv <= 256
 
 #ifndef GHIP_AH_ABL
-#define GHIP_AH_ABL 0  // timing ablation only (wrong results): every K load reads row 0
+#define GHIP_AH_ABL 0  // timing ablations only (wrong results): 1 every K load reads row 0, 2 no KQ dots,
+                       // 4 no KQ phase at all, 8 no KQV dots, 16 KQ dots over 4 of 8 steps
 #endif
 #define AH_STAMP(i)                                                                                         \
     do {                                                                                                    \
         if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[(int64_t)h * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+
+// Workgroup barrier on LDS traffic only (s_waitcnt lgkmcnt(0); s_barrier): __syncthreads() would
+// also drain vmcnt, i.e. hold every wave at the RoPE barrier until its K / V prefetch has landed.
+// Register operands of global loads stay guarded by the compiler's counted vmcnt waits at their use.
+__device__ __forceinline__ void attn_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // K/V rows of the first pass (no dependence on this token's q|k|v): KPF K steps of 32 elements for
 // position `quad`, VPF V steps of 32 positions for dimension `quad`, and the published position
@@ -222,15 +229,31 @@ __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, a
     const int G = a.H / a.Hkv, kvh = h / G, kvw = a.Hkv * hd;
     p.pos_v = ((const int *)a.rope_cur)[hd];  // published with the row (k_advance / begin)
     {
-        const int j = GHIP_AH_ABL ? 0 : quad < a.ctx ? quad : 0;  // no dependency on pos: rows >= pos are masked
+        const int j = (GHIP_AH_ABL & 1) ? 0 : quad < a.ctx ? quad : 0;  // no dependency on pos: rows >= pos are masked
         const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
 #pragma unroll
         for (int s = 0; s < KPF; ++s) p.k[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
     }
+    if (a.v_lds) return;  // the V rows come by LDS-DMA (attn_vdma)
     const int d0 = d_lo + quad < (hd < d_hi ? hd : d_hi) ? d_lo + quad : d_lo;
     const uint16_t *vrow0 = a.vc + ((int64_t)kvh * hd + d0) * a.ctx;
 #pragma unroll
     for (int s = 0; s < VPF; ++s) p.v[s] = *(const uint4 *)(vrow0 + (s * 32 < a.ctx ? s * 32 : 0) + t4 * 8);
+}
+
+// The workgroup's V rows [d_lo, d_hi) x positions [0, min(ctx, 256)) into LDS by LDS-DMA (no
+// registers, no round trip at the KQV): row r at smem + a.v_lds + r * ATT_VDMA_PITCH, one wave
+// instruction per row (16 B per lane = 8 positions).  The pitch (512 + 64 B) puts the 16 quads of a
+// KQV read on distinct banks (quad q at dword 16q + 4 t4 mod 64).  Completion: each wave waits for
+// its own DMAs (vmcnt) before the barrier ahead of the KQV.
+__device__ __forceinline__ void attn_vdma(const attn_args &a, int kvh, int d_lo, int dsz, uint8_t *smem, int wave, int nwave,
+                                          int lane) {
+    const int np = a.ctx < 256 ? a.ctx : 256;  // positions copied (n_kv <= np on the KQV's fast branch)
+    for (int r = wave; r < dsz; r += nwave) {
+        const uint16_t *src = a.vc + ((int64_t)kvh * a.hd + d_lo + r) * a.ctx + lane * 8;
+        auto *dst = (__attribute__((address_space(3))) void *)(smem + a.v_lds + (uint32_t)r * ATT_VDMA_PITCH);
+        if (lane * 8 < np) __builtin_amdgcn_global_load_lds((const void *)src, dst, 16, 0, 0);
+    }
 }
 
 // One token's attention for query head h by one NTH-thread workgroup (SURVEY A.4/A.6 order).
@@ -267,6 +290,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     }
     attn_pre<KPF, VPF> own;
     if (!PRE) attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi, tid);
+    if (a.v_lds) attn_vdma(a, kvh, d_lo, dsz, smem, wave, nwave, lane);
     const attn_pre<KPF, VPF> &P = PRE ? *pre : own;
     const int pos_v = P.pos_v;
     const uint4 *kpre = P.k, *vpre = P.v;
@@ -312,7 +336,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         *mx_key = 0u;  // below the key of every float, -inf included
         *e_sum = 0ull;
     }
-    __syncthreads();
+    attn_barrier();  // LDS only: the K / V prefetch stays in flight
     AH_STAMP(1);
     // this token's cache entries (src/gemma_model.cpp:506-517), by the group's first head; readers
     // in this launch use k16 / the v values instead
@@ -332,33 +356,42 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         const int j = j0 + quad;
         // a wave whose 16 positions all lie past n_kv has nothing to store: skip its dots (wave-
         // uniform; its lmax stays -inf, below every stored score)
-        if (j0 + wave * 16 >= n_kv) continue;
+        if (j0 + wave * 16 >= n_kv || (GHIP_AH_ABL & 4)) continue;
         float acc[8];
 #pragma unroll
         for (int y = 0; y < 8; ++y) acc[y] = 0.0f;
-        if (j == pos) {
-#pragma unroll
-            for (int s = 0; s < 8; ++s)
-                if (s * 32 < hd) f16_step8(acc, *(const uint4 *)(k16 + s * 32 + t4 * 8), qr[s]);
-        } else if (j0 == 0) {
+        if (j0 == 0) {
             // the row's remaining K steps (hd <= 256: at most 8 - KPF) issued together before the
             // prefetched steps' arithmetic: one round trip, not one per step
-            const uint16_t *krow = a.kc + (int64_t)(GHIP_AH_ABL ? 0 : j < a.ctx ? j : 0) * kvw + (int64_t)kvh * hd;
+            const uint16_t *krow = a.kc + (int64_t)((GHIP_AH_ABL & 1) ? 0 : j < a.ctx ? j : 0) * kvw + (int64_t)kvh * hd;
             constexpr int KR = 8 - KPF > 0 ? 8 - KPF : 1;
-            uint4 krest[KR];
+            uint4 kx[8];
 #pragma unroll
             for (int r = 0; r < KR; ++r) {
                 const int s = KPF + r;
-                krest[r] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0) + t4 * 8);
+                if (s < 8) kx[s < 8 ? s : 0] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0) + t4 * 8);
             }
 #pragma unroll
             for (int s = 0; s < KPF; ++s)
-                if (s * 32 < hd) f16_step8(acc, kpre[s], qr[s < 8 ? s : 0]);
+                if (s < 8) kx[s] = kpre[s];
+            // this token's own row (its cache store may not be visible): only the quad of j == pos
+            // swaps its operands for k16 from LDS — one divergent LDS read, not a second dot
+            if (j == pos) {
 #pragma unroll
-            for (int r = 0; r < KR; ++r) {
-                const int s = KPF + r;
-                if (KPF < 8 && s * 32 < hd) f16_step8(acc, krest[r], qr[s < 8 ? s : 0]);
+                for (int s = 0; s < 8; ++s)
+                    if (s * 32 < hd) kx[s] = *(const uint4 *)(k16 + s * 32 + t4 * 8);
             }
+            if (GHIP_AH_ABL & 2) {
+#pragma unroll
+                for (int s = 0; s < 8; ++s) acc[s] = __builtin_bit_cast(float, kx[s].x ^ qr[s].y);
+            } else
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s * 32 < hd && (!(GHIP_AH_ABL & 16) || s < 4)) f16_step8(acc, kx[s], qr[s]);
+        } else if (j == pos) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s * 32 < hd) f16_step8(acc, *(const uint4 *)(k16 + s * 32 + t4 * 8), qr[s]);
         } else {
             const int jc = j < pos ? j : 0;  // j > pos is masked below
             const uint16_t *krow = a.kc + (int64_t)jc * kvw + (int64_t)kvh * hd;
@@ -380,7 +413,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         const uint32_t b = __builtin_bit_cast(uint32_t, lmax);
         atomicMax(mx_key, (b & 0x80000000u) ? ~b : (b | 0x80000000u));
     }
-    __syncthreads();
+    attn_barrier();  // LDS only: the K / V prefetch stays in flight
     AH_STAMP(2);
     // ---- soft_max_ext: e = f16(exp(f16(w - max))) per position, its exact integer
     // sum, P16 = f16(e * (float)(1 / sum)).  The position's quad lane 0 (which formed S[j]) forms e;
@@ -389,31 +422,32 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     {
         const uint32_t key = *mx_key;
         const float mx = __builtin_bit_cast(float, (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key);
-        AH_STAMP(5);
+        if (GHIP_STAMPS != 2) AH_STAMP(5);
         unsigned long long isum = 0;
         for (int j = quad; j < n_kv; j += NTH / 4) {
             if (t4 != 0) break;
             const float w = S[j];
             const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
             isum += (unsigned long long)(uint32_t)(e * 16777216.0f);  // e*2^24 <= 2^24: exact
+            P16[j] = (uint16_t)f2h(e);  // e is an f16 value: kept exactly for the second pass
         }
         isum = wave_sum_u64(isum);
         if (lane == 0 && isum) atomicAdd(e_sum, isum);
-        __syncthreads();
-        AH_STAMP(6);
+        attn_barrier();  // LDS only: the K / V prefetch stays in flight
+        if (GHIP_STAMPS != 2) AH_STAMP(6);
         const double sum = (double)*e_sum * (1.0 / 16777216.0);
         const float inv = (float)(1.0 / sum);
-        AH_STAMP(7);
+        if (GHIP_STAMPS != 2) AH_STAMP(7);
         if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
         for (int j = quad; j < n_kv; j += NTH / 4) {
             if (t4 != 0) break;
-            const float w = S[j];
-            const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
+            const float e = h2f(P16[j]);  // this lane's own e from the first pass (no second exp)
             P16[j] = f2h(e * inv);
             if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
         }
     }
-    __syncthreads();
+    if (a.v_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V DMAs have landed
+    attn_barrier();
     AH_STAMP(3);
     // ---- KQV: out[d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16); lane t4 runs accumulator j = t4
     for (int d = d_lo + quad; d < d_hi; d += NTH / 4) {
@@ -442,26 +476,37 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             // for every dimension) read into registers once
             uint4 xs8[8], pr8[8];
             const bool first = d == d0;
+            if (a.v_lds) {
+                const uint8_t *vl = smem + a.v_lds + (uint32_t)(d - d_lo) * ATT_VDMA_PITCH + t4 * 16;
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const int e0 = s * 32 + t4 * 8;
-                if (s < VPF && first) xs8[s] = vpre[s < VPF ? s : 0];
-                else xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
+                for (int s = 0; s < 8; ++s) xs8[s] = *(const uint4 *)(vl + (s * 32 < n_kv ? s * 64 : 0));
+            } else {
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    const int e0 = s * 32 + t4 * 8;
+                    if (s < VPF && first) xs8[s] = vpre[s < VPF ? s : 0];
+                    else xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
+                }
             }
 #pragma unroll
             for (int s = 0; s < 8; ++s) pr8[s] = *(const uint4 *)(P16 + (s * 32 < n_kv ? s * 32 : 0) + t4 * 8);
+            if (GHIP_STAMPS == 2 && d == d_lo + quad) {  // operands in registers (stamps build 2)
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                AH_STAMP(5);
+            }
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 if (s * 32 >= n_kv) break;
                 uint4 xv = xs8[s];
                 patch(xv, s);
-                f16_step8(acc, xv, pr8[s]);
+                if (GHIP_AH_ABL & 8) acc[s] = __builtin_bit_cast(float, xv.x ^ pr8[s].y);
+                else f16_step8(acc, xv, pr8[s]);
             }
         } else
         for (int st = 0, s = 0; st < n_kv; st += 32, ++s) {
             const int e0 = st + t4 * 8;
             uint4 xv;
-            if (d == d0 && s < VPF) {
+            if (!a.v_lds && d == d0 && s < VPF) {  // (with the LDS copy no V was loaded early)
                 xv = vpre[0];  // statically-indexed pick from the early loads
 #pragma unroll
                 for (int k = 1; k < VPF; ++k)
@@ -473,6 +518,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             f16_step8(acc, xv, *(const uint4 *)(P16 + e0));
         }
         const float o = quad_reduce_f16(acc);
+        if (GHIP_STAMPS == 2 && d == d_lo + quad) AH_STAMP(6);  // chains folded
         if (t4 == 0) {
             a.out[(int64_t)h * hd + d] = o;
             if (a.out_act || a.out_q8k || a.out_gran) ((float *)smem)[d] = o;  // q16|k16 (hd floats) are dead after KQ
@@ -493,6 +539,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         // this head's hd/32 blocks of the Q8_0 activation image of `out` (attn-out's PRO_IMG input;
         // the same quantize_row_q8_0 the consumer would run, DESIGN.md §Activation image)
         __syncthreads();
+        if (GHIP_STAMPS == 2) AH_STAMP(7);  // the image's barrier passed
         if (tid < dsz / 8) {  // this workgroup's dims: dsz / 32 whole blocks
             const int b = d_lo / 32 + (tid >> 2);
             const float *o = (const float *)smem + b * 32 + (tid & 3) * 8;

@@ -276,6 +276,9 @@ struct attn_args {
     float *out_da = nullptr;
     uint8_t *out_q8k = nullptr;   // per-head mode, hd == 256: out's Q8_K image (one super-block per head)
     int dsplit = 1;               // per-head mode: workgroups per head, each the KQV of hd/dsplit dims
+    // per-head mode (k_attn_head): byte offset in LDS of the workgroup's V rows, copied there by
+    // LDS-DMA at the start (positions < min(ctx, 256), row pitch ATT_VDMA_PITCH); 0 = no copy
+    uint32_t v_lds = 0;
     int H, Hkv, hd, ctx;
     float q_scale;
     float *dbg_w = nullptr;      // optional debug taps: [H][ctx] scores, [H][ctx] fp16 P, [H] inv

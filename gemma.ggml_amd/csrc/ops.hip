@@ -869,14 +869,23 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
             set_error("attn_decode: unsupported shape for the per-head form");
             return -1;
         }
-        const size_t lds = ((2 * (size_t)a.hd * 2 + 15) & ~(size_t)15) + (size_t)a.ctx * 4 + (size_t)a.ctx * 2 + 16;
+        size_t lds = ((2 * (size_t)a.hd * 2 + 15) & ~(size_t)15) + (size_t)a.ctx * 4 + (size_t)a.ctx * 2 + 16;
         if (lds > 160 * 1024) {
             set_error("attn_decode: context too long for the LDS image");
             return -1;
         }
+        // the workgroup's V rows by LDS-DMA when they fit beside the scores (GHIP_ATT_VDMA=1; off by
+        // default: measured neutral to -0.5 % per decode step)
+        static const bool vdma_env = getenv("GHIP_ATT_VDMA") && atoi(getenv("GHIP_ATT_VDMA")) != 0;
+        attn_args la = a;
+        const size_t v_off = (lds + 15) & ~(size_t)15, v_bytes = (size_t)(a.hd / a.dsplit) * ATT_VDMA_PITCH;
+        if (vdma_env && v_off + v_bytes <= 160 * 1024) {
+            la.v_lds = (uint32_t)v_off;
+            lds = v_off + v_bytes;
+        }
         if (lds > 64 * 1024)
             GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_head, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k_attn_head, dim3(8 * a.H * a.dsplit), dim3(AH_THREADS), lds, s, a);
+        hipLaunchKernelGGL(k_attn_head, dim3(8 * a.H * a.dsplit), dim3(AH_THREADS), lds, s, la);
         GHIP_CHECK(hipGetLastError());
         return 0;
     }

@@ -42,6 +42,26 @@ for st in $STEPS; do
         GHIP_LIB=$L timeout -k 10 240 python bench.py --no-cpu --prefill 0 --tp-steps 0 --q8-steps 0 --ggml-steps 0 > $O/ab_$v$rep.json 2> $O/ab_$v$rep.err || { tail -20 $O/ab_$v$rep.err; exit 1; }
         python3 -c "import json; d=json.load(open('$O/ab_$v$rep.json')); print('$v', d['value'], d['ms_per_step'], (d.get('q4_k_m_decode') or {}).get('tok_s'))"
       done; done ;;
+    vdma)
+      # decode attention V rows by LDS-DMA (GHIP_ATT_VDMA=1) vs register/global loads (the default)
+      timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_ops.py tests/test_gpu_persist.py -m gpu > $O/vdma_tests.log 2>&1 || { tail -30 $O/vdma_tests.log; exit 1; }
+      tail -1 $O/vdma_tests.log
+      for v in 1 0; do GHIP_ATT_VDMA=$v GHIP_LIB=$PWD/ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 9 > $O/vdma_stamp_$v.log 2>&1 || { tail -20 $O/vdma_stamp_$v.log; exit 1; }; echo "== VDMA=$v"; grep -A2 "^attention" $O/vdma_stamp_$v.log; done
+      for rep in 1 2; do for v in 1 0; do
+        GHIP_ATT_VDMA=$v timeout -k 10 240 python bench.py --no-cpu --prefill 0 --tp-steps 0 --q8-steps 0 --ggml-steps 0 > $O/vdma_$v$rep.json 2> $O/vdma_$v$rep.err || { tail -20 $O/vdma_$v$rep.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/vdma_$v$rep.json')); print('VDMA=$v', d['value'], d['ms_per_step'])"
+      done; done ;;
+    attn2)
+      # decode attention round-4 changes (V by LDS-DMA, own-row operand swap, single-exp softmax)
+      # against the previous build (ab_libs/libbase.so), and the new build with the DMA off
+      timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_ops.py tests/test_gpu_persist.py tests/test_gpu_ggml_graph.py -m gpu > $O/attn2_tests.log 2>&1 || { tail -30 $O/attn2_tests.log; exit 1; }
+      tail -1 $O/attn2_tests.log
+      GHIP_LIB=$PWD/ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 9 > $O/attn2_stamp.log 2>&1 || { tail -20 $O/attn2_stamp.log; exit 1; }; grep -A2 "^attention" $O/attn2_stamp.log
+      for rep in 1 2 3; do for v in base new nodma; do
+        L=""; E=1; [ $v = base ] && L=$PWD/ab_libs/libbase.so; [ $v = nodma ] && E=0  # new = DMA on
+        GHIP_ATT_VDMA=$E GHIP_LIB=$L timeout -k 10 240 python bench.py --no-cpu --prefill 0 --tp-steps 0 --q8-steps 0 --ggml-steps 0 > $O/a2_$v$rep.json 2> $O/a2_$v$rep.err || { tail -20 $O/a2_$v$rep.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/a2_$v$rep.json')); print('$v', d['value'], d['ms_per_step'])"
+      done; done ;;
     pmc)
       bash scripts/pmc_prefill.sh $TAG/pmc 2048 > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
       tail -24 $O/pmc.log ;;
