@@ -34,7 +34,10 @@ typedef float mx4 __attribute__((ext_vector_type(4)));
 #define GHIP_MX_ABL 0  // timing ablations only (wrong results): 1 K rows all row 0, 2 V rows all row 0, 4 no softmax passes,
                        // 8 no KQV, 16 no KQ
 #endif
-constexpr int MX_THREADS = 512, MX_WAVES = MX_THREADS / 64, MX_HD = 256;
+#ifndef GHIP_MX_THREADS
+#define GHIP_MX_THREADS 512  // 256: 4-wave workgroups, two per CU where the scores fit 80 KB
+#endif
+constexpr int MX_THREADS = GHIP_MX_THREADS, MX_WAVES = MX_THREADS / 64, MX_HD = 256;
 
 // ggml_vec_dot_f16's fold of the 32 chain values of one output (reduce_f16_acc, attn_impl.h)
 __device__ __forceinline__ float fold32(const mx4 acc[32], int r) {
