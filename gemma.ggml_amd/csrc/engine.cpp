@@ -770,6 +770,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
         t.nwg = e->ag.nwg; t.sbuf = e->att_sbuf; t.sync = e->att_sync; t.err = e->att_sync + e->ag.sync_ints;
         if (srcB == HANDOFF) t.out_q8k = e->kq_xa;  // each head's 256 outputs are one super-block
         else if (t.mode == ATTN_PER_HEAD) t.dsplit = e->att_dsplit;
+        t.dbg_t = stamp_region(e, il, 1);  // diagnostics (stamps build): the attention's phases
         if (launch_attn_decode(t, s)) return -1;
         const img in_b{srcB, e->kq_xa, KQP_F32, e->attn, nullptr};
         if (launch_img(in_b, e->qw)) return -1;

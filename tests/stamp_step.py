@@ -16,11 +16,12 @@ from bench import GEMMA_2B, GEMMA_7B, make_prompt
 
 layer = int(sys.argv[1]) if len(sys.argv) > 1 else 9
 shape = GEMMA_7B if (len(sys.argv) > 2 and sys.argv[2] == "7b") else GEMMA_2B
-e = G.Engine(shape, n_ctx=512, device=0)
+wtype = G.GGML_TYPE_Q4_K if os.environ.get("KQ") == "1" else G.GGML_TYPE_Q4_0  # KQ=1: the Q4_K_M layout
+e = G.Engine(shape, n_ctx=512, device=0, wtype=wtype)
 if os.environ.get("PLAN"):  # qkv, o, gate/up, down, logits: ks,rpw,img triples
     v = [int(t) for t in os.environ["PLAN"].split(",")]
     e.set_plan({k: (v[3 * i], v[3 * i + 1], v[3 * i + 2]) for i, k in enumerate(e.PLAN_CLASSES)})
-print("plan", e.plan())
+print("plan", e.plan() if wtype == G.GGML_TYPE_Q4_0 else "K-quant")
 e.begin(make_prompt(128, shape["n_vocab"]))
 e.step(140, use_graph=True)
 names = ["qkv", "attention", "attn-out", "gate/up", "down", "logits"]
