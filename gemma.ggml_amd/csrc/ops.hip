@@ -876,7 +876,8 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
         }
         // the workgroup's V rows by LDS-DMA when they fit beside the scores (GHIP_ATT_VDMA=1; off by
         // default: measured neutral to -0.5 % per decode step)
-        static const bool vdma_env = getenv("GHIP_ATT_VDMA") && atoi(getenv("GHIP_ATT_VDMA")) != 0;
+        const char *vdma_s = getenv("GHIP_ATT_VDMA");  // read per launch (graphs bake it in at capture)
+        const bool vdma_env = vdma_s && atoi(vdma_s) != 0;
         attn_args la = a;
         const size_t v_off = (lds + 15) & ~(size_t)15, v_bytes = (size_t)(a.hd / a.dsplit) * ATT_VDMA_PITCH;
         if (vdma_env && v_off + v_bytes <= 160 * 1024) {

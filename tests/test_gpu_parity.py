@@ -94,6 +94,21 @@ def test_decode_gemma2b_attention_forms_bitexact(attention):
 
 
 @gpu
+@pytest.mark.parametrize("dsplit", ["4", "1"])
+def test_decode_attention_v_dma_bitexact(monkeypatch, dsplit):
+    """the decode attention with its V rows copied into LDS by DMA (GHIP_ATT_VDMA=1, off by default),
+    4 and 1 workgroups per head, through positions past 32 (several V steps) and the own-position
+    patch; tiny GQA and Gemma-2B shapes against the oracle"""
+    monkeypatch.setenv("GHIP_ATT_VDMA", "1")
+    monkeypatch.setenv("GHIP_ATT_DSPLIT", dsplit)
+    O.lib().orc_set_threads(16)
+    _check_decode(dict(O.TINY, n_head=4, n_head_kv=2, n_embd=1024), n_prompt=5, n_decode=40, n_ctx=128)
+    # past 256 positions the KQV reads V from the cache again (the LDS copy holds 256)
+    _check_decode(dict(O.TINY, n_head=4, n_head_kv=2, n_embd=1024), n_prompt=250, n_decode=20, n_ctx=512)
+    _check_decode(O.GEMMA_2B, n_prompt=6, n_decode=3, n_ctx=256)
+
+
+@gpu
 def test_decode_gemma2b_bitexact():
     O.lib().orc_set_threads(16)
     _check_decode(O.GEMMA_2B, n_prompt=6, n_decode=4, n_ctx=256)
