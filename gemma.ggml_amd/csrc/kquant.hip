@@ -1266,20 +1266,6 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         }                                                                                                     \
     } while (0)
     const bool wide = a.pro != KQP_COPY && a.nsb > 8;  // more than 2 super-blocks per wave
-    // the output head (tens of thousands of row groups, the stream dominates): GHIP_KQ_OPF super-blocks
-    // of weight loads in flight per round trip (default 2, like the other shapes)
-    static const int kq_opf = getenv("GHIP_KQ_OPF") ? atoi(getenv("GHIP_KQ_OPF")) : 2;
-    if (!a.w2 && !wide && groups >= 8192 && kq_opf == 4) {
-        if (a.tiled) {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, false, 2, true, 4>), grid, dim3(KQ_THREADS), lds, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, false, 2, true, 4>), grid, dim3(KQ_THREADS), lds, s, a);
-        } else {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, false, 2, false, 4>), grid, dim3(KQ_THREADS), lds, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, false, 2, false, 4>), grid, dim3(KQ_THREADS), lds, s, a);
-        }
-        GHIP_CHECK(hipGetLastError());
-        return 0;
-    }
     if (a.w2) {
         if (wide) GHIP_KQ_LAUNCH(true, 8);
         else GHIP_KQ_LAUNCH(true, 2);
