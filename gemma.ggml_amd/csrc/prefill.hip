@@ -7,6 +7,7 @@
 // across blocks differs from ggml's AVX2 lane order (one chain acc = fmaf(d_w*d_a, isum, acc) in
 // block order instead of 8 lane chains + fold), so prefill logits match the CPU path to ~1e-6
 // relative (tests: 1e-3), while the per-token decode path stays bit-exact.
+#include <algorithm>
 #include <type_traits>
 
 #include "device_util.h"
@@ -16,6 +17,49 @@ namespace ghip {
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
+
+// quantize_row_q8_0 (AVX2) of one 32-element block held by a quad (8 values per lane):
+// amax, d = amax/127 (fp16 RNE), id = 127/amax, rint; the int8 image and/or the same integers as f16
+// (the exact GEMM's MFMA operand), and the block scale
+__device__ __forceinline__ void quant_block_q8(const qrow_args &a, int64_t t, int64_t b, int q, const float v[8]) {
+    float amax = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    amax = fmaxf(amax, dpp_f<0xB1>(amax));
+    amax = fmaxf(amax, dpp_f<0x4E>(amax));
+    const uint32_t d16 = f2h(amax / 127.f);
+    const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+    uint32_t pk[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        int qi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qi[k] = (int)__builtin_rintf(v[4 * h + k] * id);
+        pk[h] = (uint32_t)(qi[0] & 0xFF) | ((uint32_t)(qi[1] & 0xFF) << 8) | ((uint32_t)(qi[2] & 0xFF) << 16) |
+                ((uint32_t)(qi[3] & 0xFF) << 24);
+    }
+    if (a.q) *(uint2 *)(a.q + t * a.ldq + b * 32 + q * 8) = make_uint2(pk[0], pk[1]);
+    if (a.qh) {
+        uint32_t hv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q0 = (int8_t)(pk[k >> 1] >> (16 * (k & 1))), q1 = (int8_t)(pk[k >> 1] >> (16 * (k & 1) + 8));
+            hv[k] = f2h((float)q0) | (f2h((float)q1) << 16);
+        }
+        *(uint4 *)(a.qh + t * a.ldq + b * 32 + q * 8) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+    }
+    if (q == 0) a.da[t * a.ldd + b] = h2f(d16);
+}
+
+// zero the K padding of row t's images (the GEMMs stage whole 256-element chunks)
+__device__ __forceinline__ void quant_pad(const qrow_args &a, int64_t t, int tid, int nth) {
+    const int64_t K = a.K, nb = K / 32;
+    if (a.q)
+        for (int64_t i = K + tid * 4; i < a.ldq; i += nth * 4) *(uint32_t *)(a.q + t * a.ldq + i) = 0;
+    if (a.qh)
+        for (int64_t i = K + tid * 2; i < a.ldq; i += nth * 2) *(uint32_t *)(a.qh + t * a.ldq + i) = 0;
+    for (int64_t b = nb + tid; b < a.ldd; b += nth) a.da[t * a.ldd + b] = 0.0f;
+}
 
 // ---- rows -> Q8_0 (int8 image + f32 of the fp16 block scale) --------------------------------
 // One 256-thread workgroup per token row; a quad of threads owns a block (8 elements each).
@@ -90,8 +134,6 @@ __global__ void __launch_bounds__(256) k_quant_rows(qrow_args a) {
         const float mean = (float)(sum / (double)K);
         scale = 1.0f / sqrtf(mean + a.eps);
     }
-    int8_t *qo = a.q + (int64_t)t * a.ldq;
-    float *dout = a.da + (int64_t)t * a.ldd;
     for (int64_t b = tid >> 2; b < nb; b += 64) {
         float v[8];
         load(b * 32 + q * 8, v);
@@ -102,41 +144,42 @@ __global__ void __launch_bounds__(256) k_quant_rows(qrow_args a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = (v[j] * scale) * wv[j];  // rms_norm, then ggml_mul
         }
-        // quantize_row_q8_0 (AVX2): amax, d = amax/127 (fp16 RNE), id = 127/amax, rint
-        float amax = 0.0f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
-        amax = fmaxf(amax, dpp_f<0xB1>(amax));
-        amax = fmaxf(amax, dpp_f<0x4E>(amax));
-        const uint32_t d16 = f2h(amax / 127.f);
-        const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
-        uint32_t pk[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            int qi[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) qi[k] = (int)__builtin_rintf(v[4 * h + k] * id);
-            pk[h] = (uint32_t)(qi[0] & 0xFF) | ((uint32_t)(qi[1] & 0xFF) << 8) | ((uint32_t)(qi[2] & 0xFF) << 16) |
-                    ((uint32_t)(qi[3] & 0xFF) << 24);
-        }
-        if (a.q) *(uint2 *)(qo + b * 32 + q * 8) = make_uint2(pk[0], pk[1]);
-        if (a.qh) {  // the same integers as f16 (exact): the exact GEMM's MFMA operand
-            uint32_t hv[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int q0 = (int8_t)(pk[k >> 1] >> (16 * (k & 1))), q1 = (int8_t)(pk[k >> 1] >> (16 * (k & 1) + 8));
-                hv[k] = f2h((float)q0) | (f2h((float)q1) << 16);
-            }
-            *(uint4 *)(a.qh + (int64_t)t * a.ldq + b * 32 + q * 8) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
-        }
-        if (q == 0) dout[b] = h2f(d16);
+        quant_block_q8(a, t, b, q, v);
     }
-    // zero the K padding of the images (the GEMMs stage whole 256-element chunks)
-    if (a.q)
-        for (int64_t i = K + tid * 4; i < a.ldq; i += 256 * 4) *(uint32_t *)(qo + i) = 0;
-    if (a.qh)
-        for (int64_t i = K + tid * 2; i < a.ldq; i += 256 * 2) *(uint32_t *)(a.qh + (int64_t)t * a.ldq + i) = 0;
-    for (int64_t b = nb + tid; b < a.ldd; b += 256) dout[b] = 0.0f;
+    quant_pad(a, t, tid, 256);
+}
+
+// QR_GELU with the fp16 gelu table in LDS (128 KiB, loaded once per workgroup; one workgroup per CU
+// walks rows t = blockIdx.x, + gridDim.x, ...): the per-element table lookups are LDS reads instead
+// of dependent global loads.  Same values as k_quant_rows<QR_GELU> (the table's entries, the clamp
+// rule, g * up, the same block quantizer): bit-identical.
+constexpr int QG_THREADS = 1024;
+__global__ void __launch_bounds__(QG_THREADS) k_quant_gelu_lds(qrow_args a, int T) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t gtab[];  // 65536 fp16 entries
+    const int tid = threadIdx.x, q = tid & 3;
+    for (int i = tid; i < 65536 / 8; i += QG_THREADS) ((uint4 *)gtab)[i] = ((const uint4 *)a.gelu_tab)[i];
+    __syncthreads();
+    const int64_t K = a.K, nb = K / 32;
+    for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
+        const float *x = a.x + t * a.ldx, *x2 = a.x2 + t * a.ldx;
+        for (int64_t b = tid >> 2; b < nb; b += QG_THREADS / 4) {
+            const int64_t i0 = b * 32 + q * 8;
+            const float4 u0 = *(const float4 *)(x + i0), u1 = *(const float4 *)(x + i0 + 4);
+            const float4 g0 = *(const float4 *)(x2 + i0), g1 = *(const float4 *)(x2 + i0 + 4);
+            float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+            const float up[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float g;
+                if (a.gelu_clamp && v[j] <= -10.0f) g = 0.0f;
+                else if (a.gelu_clamp && v[j] >= 10.0f) g = v[j];
+                else g = h2f(gtab[f2h(v[j])]);
+                v[j] = g * up[j];
+            }
+            quant_block_q8(a, t, b, q, v);
+        }
+        quant_pad(a, t, tid, QG_THREADS);
+    }
 }
 
 // ---- int8 MFMA GEMM: Y[t][r] = sum_b (d_w[r][b] * d_a[t][b]) * isum_b(W[r], Xq[t]) ------------
@@ -885,7 +928,21 @@ int launch_quant_rows(int mode, const qrow_args &a, int T, hipStream_t s) {
         case QR_F32: hipLaunchKernelGGL(k_quant_rows<QR_F32>, dim3(T), dim3(256), 0, s, a); break;
         case QR_NORM: hipLaunchKernelGGL(k_quant_rows<QR_NORM>, dim3(T), dim3(256), 0, s, a); break;
         case QR_EMBED_NORM: hipLaunchKernelGGL(k_quant_rows<QR_EMBED_NORM>, dim3(T), dim3(256), 0, s, a); break;
-        case QR_GELU: hipLaunchKernelGGL(k_quant_rows<QR_GELU>, dim3(T), dim3(256), 0, s, a); break;
+        case QR_GELU: {
+            // the LDS-table form (GHIP_QR_GELU_LDS=1; the per-row form by default)
+            const char *env = getenv("GHIP_QR_GELU_LDS");
+            if (env && atoi(env)) {
+                static bool attr = false;
+                if (!attr) {
+                    GHIP_CHECK(hipFuncSetAttribute((const void *)k_quant_gelu_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 65536 * 2));
+                    attr = true;
+                }
+                hipLaunchKernelGGL(k_quant_gelu_lds, dim3((unsigned)std::min(T, 256)), dim3(QG_THREADS), 65536 * 2, s, a, T);
+            } else {
+                hipLaunchKernelGGL(k_quant_rows<QR_GELU>, dim3(T), dim3(256), 0, s, a);
+            }
+            break;
+        }
         default: set_error("quant_rows: bad mode"); return -1;
     }
     GHIP_CHECK(hipGetLastError());
