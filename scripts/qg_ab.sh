@@ -1,5 +1,5 @@
 #!/bin/bash
-# prefill GELU quantizer with the table in LDS (GHIP_QR_GELU_LDS=1) vs the per-row form: parity, then T = 2048 time
+# prefill GELU quantizer with the table in LDS (default) vs the per-row form (GHIP_QR_GELU_LDS=0): parity, then T = 2048 time
 set -o pipefail
 O=gpurun_out/${1:-qg}
 mkdir -p $O
