@@ -209,6 +209,19 @@ constexpr int AH_VPF = GHIP_AH_VPF;  // V steps (of 32 positions) prefetched per
     do {                                                                                                    \
         if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[(int64_t)h * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// stamps build 3: the workgroup's shader-clock cycles (s_memtime) and 10 ns ticks (s_memrealtime)
+// from its start to its end in slots 5 / 6 (split 0 only), so the host reads the core clock it ran at
+#define AH_CLK0()                                                                                           \
+    unsigned long long clk_c0 = 0, clk_r0 = 0;                                                              \
+    if (GHIP_STAMPS == 3) { clk_c0 = __builtin_amdgcn_s_memtime(); clk_r0 = __builtin_amdgcn_s_memrealtime(); }
+#define AH_CLK1()                                                                                           \
+    do {                                                                                                    \
+        if (GHIP_STAMPS == 3 && a.dbg_t && tid == 0 && sp == 0) {                                           \
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime(); \
+            a.dbg_t[(int64_t)h * 8 + 5] = c1 - clk_c0;                                                      \
+            a.dbg_t[(int64_t)h * 8 + 6] = r1 - clk_r0;                                                      \
+        }                                                                                                   \
+    } while (0)
 
 // Workgroup barrier on LDS traffic only (s_waitcnt lgkmcnt(0); s_barrier): __syncthreads() would
 // also drain vmcnt, i.e. hold every wave at the RoPE barrier until its K / V prefetch has landed.
@@ -273,6 +286,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     const int lane = tid & 63, wave = tid >> 6, nwave = NTH / 64;
     const int G = a.H / a.Hkv, kvh = h / G;
     AH_STAMP(0);
+    AH_CLK0();
     const int kvw = a.Hkv * hd;
     const float *qh = a.qkv + (int64_t)h * hd;
     const float *kh = a.qkv + (int64_t)a.H * hd + (int64_t)kvh * hd;
@@ -422,7 +436,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     {
         const uint32_t key = *mx_key;
         const float mx = __builtin_bit_cast(float, (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key);
-        if (GHIP_STAMPS != 2) AH_STAMP(5);
+        if (GHIP_STAMPS == 1) AH_STAMP(5);
         unsigned long long isum = 0;
         for (int j = quad; j < n_kv; j += NTH / 4) {
             if (t4 != 0) break;
@@ -434,10 +448,10 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         isum = wave_sum_u64(isum);
         if (lane == 0 && isum) atomicAdd(e_sum, isum);
         attn_barrier();  // LDS only: the K / V prefetch stays in flight
-        if (GHIP_STAMPS != 2) AH_STAMP(6);
+        if (GHIP_STAMPS == 1) AH_STAMP(6);
         const double sum = (double)*e_sum * (1.0 / 16777216.0);
         const float inv = (float)(1.0 / sum);
-        if (GHIP_STAMPS != 2) AH_STAMP(7);
+        if (GHIP_STAMPS == 1) AH_STAMP(7);
         if (a.dbg_inv && tid == 0) a.dbg_inv[h] = inv;
         for (int j = quad; j < n_kv; j += NTH / 4) {
             if (t4 != 0) break;
@@ -560,6 +574,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             q8K_store(xv, tid, a.out_q8k + (int64_t)h * 292);
         }
     }
+    AH_CLK1();
     AH_STAMP(4);
 }
 

@@ -45,5 +45,8 @@ for k, nm in enumerate(names):
           f"span {int((end - t0) * 10)} ns")
     print("   median " + " ".join(f"{p}={int(v)}" for p, v in zip(["start"] + ph, np.median(rel, axis=0))))
     print("   max    " + " ".join(f"{p}={int(v)}" for p, v in zip(["start"] + ph, rel.max(axis=0))))
+    if k == 1 and os.environ.get("CLK") == "1":  # stamps build 3: s_memtime beside stamps 0 / 4 (slots 5 / 6: cycles, ticks)
+        ghz = r[:, 5] / np.maximum(r[:, 6] * 10, 1)  # cycles / ns of split 0's workgroups
+        print(f"   core clock GHz median {np.median(ghz):.3f} min {ghz.min():.3f} max {ghz.max():.3f}")
     prev_end = end
 e.close()
