@@ -28,11 +28,16 @@ namespace {
 
 typedef uint32_t v4u_nt __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u_nt __attribute__((ext_vector_type(2)));
+#ifndef GHIP_MV_NT
+#define GHIP_MV_NT 1  // weight loads non-temporal (0: plain loads, an A/B switch)
+#endif
 __device__ __forceinline__ uint4 ld_nt16(const uint8_t *p) {
+    if constexpr (!GHIP_MV_NT) return *(const uint4 *)p;
     const v4u_nt v = __builtin_nontemporal_load((const v4u_nt *)p);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ uint2 ld_nt8(const uint8_t *p) {
+    if constexpr (!GHIP_MV_NT) return *(const uint2 *)p;
     const v2u_nt v = __builtin_nontemporal_load((const v2u_nt *)p);
     return make_uint2(v.x, v.y);
 }
