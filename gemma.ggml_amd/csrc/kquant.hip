@@ -48,22 +48,25 @@ template <> struct kq_raw<T_Q6_K> { uint32_t qla[2], qlb[2], qh[2], sc[4]; uint3
 //     -> 128i + 16l + 4k, qh dword j (ggml byte 128 + 32j + 4l) -> 1024 + 64i + 8l + 4j; scales
 //     -> 1536 + 16i, d -> 1664 + 2i: four loads per lane instead of ~21 two-byte-aligned ones.
 // Same bytes, same arithmetic: the dots are unchanged.
-// Non-temporal lane-contiguous weight loads (GHIP_KQ_NT=1, as the Q4_0 matvecs load theirs):
-// measured slower, Q4_K_M decode 1,055-1,062 -> 1,036-1,041 tok/s (same box, interleaved) — off
+// Non-temporal lane-contiguous weight loads (GHIP_KQ_NT bits: 1 Q4_K, 2 Q6_K; as the Q4_0 matvecs load theirs):
+// measured slower, Q4_K_M decode 1,059-1,064 (plain) vs 1,036-1,037 (Q4_K nt) / 1,019-1,028 (Q6_K nt)
+// tok/s (same box, interleaved) — off
 #ifndef GHIP_KQ_NT
 #define GHIP_KQ_NT 0
 #endif
 typedef uint32_t kq_v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t kq_v2u __attribute__((ext_vector_type(2)));
+template <int WT>
 __device__ __forceinline__ uint4 kq_ld16(const uint8_t *p) {
-    if constexpr (GHIP_KQ_NT) {
+    if constexpr (GHIP_KQ_NT & (WT == T_Q4_K ? 1 : 2)) {
         const kq_v4u v = __builtin_nontemporal_load((const kq_v4u *)p);
         return make_uint4(v.x, v.y, v.z, v.w);
     }
     return *(const uint4 *)p;
 }
+template <int WT>
 __device__ __forceinline__ uint2 kq_ld8(const uint8_t *p) {
-    if constexpr (GHIP_KQ_NT) {
+    if constexpr (GHIP_KQ_NT & (WT == T_Q4_K ? 1 : 2)) {
         const kq_v2u v = __builtin_nontemporal_load((const kq_v2u *)p);
         return make_uint2(v.x, v.y);
     }
@@ -74,17 +77,17 @@ __device__ __forceinline__ kq_raw<WT> kq_load(const uint8_t *wrow, int s, int l)
     kq_raw<WT> r;
     if constexpr (TL && WT == T_Q4_K) {
         const uint8_t *blk = wrow + (int64_t)s * 144;
-        r.h = kq_ld16(blk);
-        const uint4 q = kq_ld16(blk + 16 + 16 * l);
+        r.h = kq_ld16<WT>(blk);
+        const uint4 q = kq_ld16<WT>(blk + 16 + 16 * l);
         r.q[0] = q.x; r.q[1] = q.y; r.q[2] = q.z; r.q[3] = q.w;
         return r;
     }
     if constexpr (TL && WT == T_Q6_K) {
         const uint8_t *g = wrow + (int64_t)(s >> 3) * 1680;
         const int i = s & 7;
-        const uint4 ql = kq_ld16(g + 128 * i + 16 * l);
-        const uint2 qh = kq_ld8(g + 1024 + 64 * i + 8 * l);
-        const uint4 sc = kq_ld16(g + 1536 + 16 * i);
+        const uint4 ql = kq_ld16<WT>(g + 128 * i + 16 * l);
+        const uint2 qh = kq_ld8<WT>(g + 1024 + 64 * i + 8 * l);
+        const uint4 sc = kq_ld16<WT>(g + 1536 + 16 * i);
         r.qla[0] = ql.x; r.qlb[0] = ql.y; r.qla[1] = ql.z; r.qlb[1] = ql.w;
         r.qh[0] = qh.x; r.qh[1] = qh.y;
         r.sc[0] = sc.x; r.sc[1] = sc.y; r.sc[2] = sc.z; r.sc[3] = sc.w;
