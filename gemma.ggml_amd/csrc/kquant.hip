@@ -48,25 +48,25 @@ template <> struct kq_raw<T_Q6_K> { uint32_t qla[2], qlb[2], qh[2], sc[4]; uint3
 //     -> 128i + 16l + 4k, qh dword j (ggml byte 128 + 32j + 4l) -> 1024 + 64i + 8l + 4j; scales
 //     -> 1536 + 16i, d -> 1664 + 2i: four loads per lane instead of ~21 two-byte-aligned ones.
 // Same bytes, same arithmetic: the dots are unchanged.
-// Non-temporal lane-contiguous weight loads (GHIP_KQ_NT bits: 1 Q4_K, 2 Q6_K; as the Q4_0 matvecs load theirs):
+// Non-temporal lane-contiguous weight loads (GHIP_KQ_NT bits: 1 Q4_K, 2 Q6_K, 4 the lane-own quant bytes only; as the Q4_0 matvecs load theirs):
 // measured slower, Q4_K_M decode 1,059-1,064 (plain) vs 1,036-1,037 (Q4_K nt) / 1,019-1,028 (Q6_K nt)
-// tok/s (same box, interleaved) — off
+// tok/s, 1,028-1,034 (lane-own quant bytes nt, headers plain) (same box, interleaved) — off
 #ifndef GHIP_KQ_NT
 #define GHIP_KQ_NT 0
 #endif
 typedef uint32_t kq_v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t kq_v2u __attribute__((ext_vector_type(2)));
-template <int WT>
+template <int WT, bool LANE = false>  // LANE: each lane its own bytes (not a wave-shared header)
 __device__ __forceinline__ uint4 kq_ld16(const uint8_t *p) {
-    if constexpr (GHIP_KQ_NT & (WT == T_Q4_K ? 1 : 2)) {
+    if constexpr ((GHIP_KQ_NT & (WT == T_Q4_K ? 1 : 2)) || (LANE && (GHIP_KQ_NT & 4))) {
         const kq_v4u v = __builtin_nontemporal_load((const kq_v4u *)p);
         return make_uint4(v.x, v.y, v.z, v.w);
     }
     return *(const uint4 *)p;
 }
-template <int WT>
+template <int WT, bool LANE = false>
 __device__ __forceinline__ uint2 kq_ld8(const uint8_t *p) {
-    if constexpr (GHIP_KQ_NT & (WT == T_Q4_K ? 1 : 2)) {
+    if constexpr ((GHIP_KQ_NT & (WT == T_Q4_K ? 1 : 2)) || (LANE && (GHIP_KQ_NT & 4))) {
         const kq_v2u v = __builtin_nontemporal_load((const kq_v2u *)p);
         return make_uint2(v.x, v.y);
     }
@@ -78,15 +78,15 @@ __device__ __forceinline__ kq_raw<WT> kq_load(const uint8_t *wrow, int s, int l)
     if constexpr (TL && WT == T_Q4_K) {
         const uint8_t *blk = wrow + (int64_t)s * 144;
         r.h = kq_ld16<WT>(blk);
-        const uint4 q = kq_ld16<WT>(blk + 16 + 16 * l);
+        const uint4 q = kq_ld16<WT, true>(blk + 16 + 16 * l);
         r.q[0] = q.x; r.q[1] = q.y; r.q[2] = q.z; r.q[3] = q.w;
         return r;
     }
     if constexpr (TL && WT == T_Q6_K) {
         const uint8_t *g = wrow + (int64_t)(s >> 3) * 1680;
         const int i = s & 7;
-        const uint4 ql = kq_ld16<WT>(g + 128 * i + 16 * l);
-        const uint2 qh = kq_ld8<WT>(g + 1024 + 64 * i + 8 * l);
+        const uint4 ql = kq_ld16<WT, true>(g + 128 * i + 16 * l);
+        const uint2 qh = kq_ld8<WT, true>(g + 1024 + 64 * i + 8 * l);
         const uint4 sc = kq_ld16<WT>(g + 1536 + 16 * i);
         r.qla[0] = ql.x; r.qlb[0] = ql.y; r.qla[1] = ql.z; r.qlb[1] = ql.w;
         r.qh[0] = qh.x; r.qh[1] = qh.y;
