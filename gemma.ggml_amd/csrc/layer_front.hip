@@ -101,9 +101,9 @@ __device__ void rr_tiles(const mv_args &a, int64_t rt0, int64_t rt1, uint8_t *sm
             const int64_t tile = (r == 0 || rt1 < 0 ? rt0 : rt1) * a.n_bt + wave;
             qb[r] = ld_nt16(a.qs + tile * 1024 + q_off);
             if (WT == T_Q4_0) {
-                sb[r] = ld_nt16(a.sc + tile * 8 * SB + s_off);
+                sb[r] = ld_sc16(a.sc + tile * 8 * SB + s_off);
             } else {
-                const uint2 v = ld_nt8(a.sc + tile * 8 * SB + s_off);
+                const uint2 v = ld_sc8(a.sc + tile * 8 * SB + s_off);
                 sb[r] = make_uint4(v.x, v.y, 0, 0);
             }
         }

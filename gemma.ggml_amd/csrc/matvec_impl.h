@@ -41,6 +41,17 @@ __device__ __forceinline__ uint2 ld_nt8(const uint8_t *p) {
     const v2u_nt v = __builtin_nontemporal_load((const v2u_nt *)p);
     return make_uint2(v.x, v.y);
 }
+#ifndef GHIP_MV_SCNT
+#define GHIP_MV_SCNT 1  // the scale loads' policy on its own (0: plain, an A/B switch)
+#endif
+__device__ __forceinline__ uint4 ld_sc16(const uint8_t *p) {
+    if constexpr (!GHIP_MV_SCNT) return *(const uint4 *)p;
+    return ld_nt16(p);
+}
+__device__ __forceinline__ uint2 ld_sc8(const uint8_t *p) {
+    if constexpr (!GHIP_MV_SCNT) return *(const uint2 *)p;
+    return ld_nt8(p);
+}
 
 __device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
@@ -759,8 +770,8 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     uint4 scl_g = make_uint4(0, 0, 0, 0), scl_u = scl_g;
     if constexpr (SCL) {
         const int64_t rts = n_items ? rt0 : 0;
-        scl_g = ld_nt16(a.sc + rts * 1024 + lane * 16);
-        scl_u = ld_nt16(a.sc2 + rts * 1024 + lane * 16);
+        scl_g = ld_sc16(a.sc + rts * 1024 + lane * 16);
+        scl_u = ld_sc16(a.sc2 + rts * 1024 + lane * 16);
     }
 
     // 1) fill the register ring: the HBM round trip overlaps the prologue below.  Loads are
@@ -787,9 +798,9 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
         (void)st;
 #else
         if (WT == T_Q4_0) {
-            sd = ld_nt16(st + s_off);
+            sd = ld_sc16(st + s_off);
         } else {
-            const uint2 v = ld_nt8(st + s_off);
+            const uint2 v = ld_sc8(st + s_off);
             sd = make_uint4(v.x, v.y, 0, 0);
         }
 #endif
@@ -1024,9 +1035,9 @@ __global__ void __launch_bounds__(512) k_matvec_gu2(mv_args a) {
         const int64_t tile = rt_i * a.n_bt + bt_i;
         qd = ld_nt16(qsm + tile * 1024 + q_off);
         if (WT == T_Q4_0) {
-            sd = ld_nt16(scm + tile * 8 * SB + s_off);
+            sd = ld_sc16(scm + tile * 8 * SB + s_off);
         } else {
-            const uint2 v = ld_nt8(scm + tile * 8 * SB + s_off);
+            const uint2 v = ld_sc8(scm + tile * 8 * SB + s_off);
             sd = make_uint4(v.x, v.y, 0, 0);
         }
         ++issued;

@@ -46,9 +46,9 @@ __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
         const int64_t tile = rt * a.n_bt + (loader ? wave : 0) + RR_NL * r;
         qb[r % D] = ld_nt16(a.qs + tile * 1024 + q_off);
         if (WT == T_Q4_0) {
-            sb[r % D] = ld_nt16(a.sc + tile * 8 * SB + s_off);
+            sb[r % D] = ld_sc16(a.sc + tile * 8 * SB + s_off);
         } else {
-            const uint2 v = ld_nt8(a.sc + tile * 8 * SB + s_off);
+            const uint2 v = ld_sc8(a.sc + tile * 8 * SB + s_off);
             sb[r % D] = make_uint4(v.x, v.y, 0, 0);
         }
     };
