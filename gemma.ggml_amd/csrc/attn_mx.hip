@@ -166,10 +166,13 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
         const double sum = (double)tot * (1.0 / 16777216.0);
         const float inv = (float)(1.0 / sum);
         // in place: iteration u reads S[64u + lane] and writes P16[64u + lane], bytes of S[32u ..]
-        // that earlier iterations (or this one, before its write) already read
+        // that earlier iterations (or this one, before its write) already read.  The float reads and
+        // the u16 writes alias by design: the empty asm with a memory clobber keeps every write behind
+        // its iteration's read whatever type-based alias analysis concludes
         for (int j = lane; j < L; j += 64) {
             float w = -INFINITY;
             if (j <= ip && j < n_kv) w = Sr[j];
+            asm volatile("" ::: "memory");
             const float e = w != -INFINITY ? h2f(exp_f16_of(f2h(w - mx))) : 0.0f;
             Pr[j] = (uint16_t)f2h(e * inv);
         }
@@ -218,32 +221,29 @@ __global__ void __launch_bounds__(MX_THREADS) k_attn_mx(attnp_args a) {
 
 }  // namespace
 
-// "" when the matrix-core form runs these shapes, else why not (the engine then runs k_attn_rows)
-std::string attn_mx_unsupported(const attnp_args &a) {
+// nullptr when the matrix-core form runs these shapes, else why not (the engine then runs k_attn_rows)
+const char *attn_mx_unsupported(const attnp_args &a) {
     if (a.hd != MX_HD) return "head_dim != 256";
     if (a.Hkv <= 0 || a.H % a.Hkv) return "heads";
     const int G = a.H / a.Hkv;
     if (G > 16 || 16 % G) return "query heads per kv head must divide 16";
     if (a.ctx % 32 || a.n_kv % 32 || a.n_kv > a.ctx || a.T <= 0 || a.T > a.n_kv) return "context";
-    const int P = 16 / G, i_last = a.T - 1;
-    (void)P;
-    int L = 32 * ((i_last + 1) / 32 + 1);
+    int L = 32 * (a.T / 32 + 1);  // the last row's padded n_kv
     if (L > a.n_kv) L = a.n_kv;
     if ((size_t)16 * (L + 4) * 4 > 160 * 1024) return "scores of 16 rows exceed the LDS (n_kv > 2556)";
-    return "";
+    return nullptr;
 }
 
 int launch_attn_mx(const attnp_args &a, hipStream_t s) {
-    const std::string why = attn_mx_unsupported(a);
-    if (!why.empty()) {
-        set_error("attn_mx: " + why);
+    if (const char *why = attn_mx_unsupported(a)) {
+        set_error(std::string("attn_mx: ") + why);
         return -1;
     }
     const int G = a.H / a.Hkv, P = 16 / G;
     int L = 32 * (a.T / 32 + 1);
     if (L > a.n_kv) L = a.n_kv;
     const size_t lds = (size_t)16 * (L + 4) * 4;
-    GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_mx, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (allow_full_lds((const void *)k_attn_mx, LDS_SLOT_ATTN_MX)) return -1;
     const int nblk = (a.T + P - 1) / P;
     hipLaunchKernelGGL(k_attn_mx, dim3((unsigned)(nblk * a.Hkv)), dim3(MX_THREADS), lds, s, a);
     GHIP_CHECK(hipGetLastError());

@@ -88,6 +88,56 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
     return s;
 }
 
+// ---- ggml's rms_norm mean, provably --------------------------------------------------
+// ggml: sum = Σ_i (double)(x_i*x_i) in index order, rounded after every add; mean = (float)(sum/n).
+// The kernels add the same double terms in a tree T and form mean = (float)(T/n).  All terms are
+// ≥ 0, so ANY summation order of them lies within γ_{n−1}·E of the exact sum E (γ_k = k·u/(1 − k·u),
+// u = 2^−53; Higham, Accuracy and Stability of Numerical Algorithms, §4.2): |S − T| ≤ 2·γ_{n−1}·E
+// ≤ 2(n−1)·u·T·(1 + O(n·u)) ≤ m = n·2^−51·T (= 4·n·u·T).  mean's float rounding interval is bounded
+// by the midpoints mid_lo / mid_hi to its neighbours (exact in double).  rms_mean_certain checks
+//   T·(1 − r) > mid_lo·n  and  T·(1 + r) < mid_hi·n,   r = n·2^−51 + 2^−48,
+// with multiplications only (no division on the prologue's critical path): r covers m plus the
+// rounding of these four products and keeps S/n more than a double ulp inside the interval, so
+// fl64(S/n) rounds to the same float — the tree's mean IS ggml's.  When the check fails (S and T may
+// sit on two sides of a rounding boundary: ≈ 2·r·2^23 ≈ 2^−15 of the norms at n = 2048, or a
+// zero / subnormal / largest-float mean) the caller runs ggml's sequential sum, seq_sumsq_wave.
+// 0, inf and NaN sums are the same in every order.
+__device__ __forceinline__ bool rms_mean_certain(double T, int64_t n, float mean) {
+    const uint32_t mb = __builtin_bit_cast(uint32_t, mean);
+    const bool special = !(T > 0.0) | !(T < __builtin_inf());               // 0, inf, NaN: certain
+    const bool edge = (mb < 0x00800000u) | (mb >= 0x7F7FFFFFu);             // zero / subnormal / FLT_MAX
+    const double a = (double)mean, lo = (double)__builtin_bit_cast(float, mb - 1),
+                 hi = (double)__builtin_bit_cast(float, mb + 1);
+    const double dn = (double)n, r = dn * 0x1p-51 + 0x1p-48;
+    // both sides evaluated (no short-circuit branch): straight-line code the scheduler can overlap
+    return special | (!edge & (T * (1.0 - r) > (a + lo) * 0.5 * dn) & (T * (1.0 + r) < (a + hi) * 0.5 * dn));
+}
+
+// ggml's sequential sum Σ (double)(x_i*x_i), i = 0 … n−1 in order, by ONE wave (all 64 lanes
+// active, converged control flow); every lane returns it.  load8(i, v) writes elements i … i+7 (i a
+// multiple of 8, i < n) as the caller's tree saw them (elements at or past n as 0: adding +0 to a
+// non-negative double leaves it unchanged).  Every wave that needs the value may run it itself (no
+// barrier); it is the rare slow path of rms_mean_certain (≈ n dependent double adds).
+template <class Load8>
+__device__ __forceinline__ double seq_sumsq_wave(int64_t n, Load8 load8) {
+    const int lane = (int)(threadIdx.x & 63);
+    double s = 0.0;
+    for (int64_t base = 0; base < n; base += 512) {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const int64_t i = base + (int64_t)lane * 8;
+        if (i < n) load8(i, v);
+        for (int L = 0; L < 64; ++L) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v[j]), L));
+                const float sq = x * x;
+                s += (double)sq;
+            }
+        }
+    }
+    return s;
+}
+
 // ggml's exp table entry table_exp_f16[x16] = fp16(expf(fp32(x16))) (ggml_init), computed instead of
 // gathered (the gather is a dependent global round trip in the softmax).  The f16 rounding absorbs
 // the f32 error of the hardware exp: for every non-positive f16 input (the only ones the softmax

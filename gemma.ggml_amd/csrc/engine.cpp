@@ -208,6 +208,7 @@ struct gemma_engine {
     uint16_t *kc = nullptr, *vc = nullptr;  // [L][ctx][kvw], [L][kvw][ctx]
     std::vector<uint16_t *> kc_ext, vc_ext;  // external per-layer caches (ggml executor), else empty
     float *ext_stage = nullptr;               // pinned logits row (ggml executor path)
+    int *ext_err = nullptr;                   // pinned copy of the persistent launch's sticky word (same path)
     int att_mode = ATTN_PER_HEAD;
     // row-split tensor parallelism: this rank's contiguous row range of every
     // matrix; activations are full vectors, each matvec writes its shard in place and an in-place
@@ -436,10 +437,8 @@ static bool persist_on(const gemma_engine *e) {
 // step's numbers wrong.  Report it, clear it and fall back to the per-layer launches for later steps
 // (ADVICE r3); returns 1 when a timeout was seen.
 static void drop_graph(gemma_engine *e);
-static int persist_check(gemma_engine *e) {
-    if (!persist_on(e) || !e->tok_err) return 0;
-    int w[3] = {0, 0, 0};
-    if (hipMemcpy(w, e->tok_err, 12, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+// w = the persistent launch's sticky words [flag, site, layer] read back after the step
+static int persist_report(gemma_engine *e, const int *w) {
     if (!w[0]) return 0;
     (void)hipMemset(e->tok_err, 0, 64);
     e->persist = 0;
@@ -448,6 +447,13 @@ static int persist_check(gemma_engine *e) {
               std::to_string(w[2]) + "): the step's logits and KV rows are invalid; the engine now runs the "
               "per-layer launches");
     return 1;
+}
+
+static int persist_check(gemma_engine *e) {
+    if (!persist_on(e) || !e->tok_err) return 0;
+    int w[3] = {0, 0, 0};
+    if (hipMemcpy(w, e->tok_err, 12, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return persist_report(e, w);
 }
 
 static int enqueue_step(gemma_engine *e) {
@@ -1334,6 +1340,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->rank_keys) (void)hipFree(e->rank_keys);
     if (e->ext_stage) (void)hipHostFree(e->ext_stage);
+    if (e->ext_err) (void)hipHostFree(e->ext_err);
     drop_graph(e);
     free_tiled(e->embd);
     for (size_t i = 0; i < e->layers.size(); ++i) {
@@ -1906,16 +1913,20 @@ static int kq_expand(gemma_engine *e, const uint8_t *x, int64_t ld, int64_t K, i
 // The exact prefill attention: on the f32 matrix cores where the shapes allow it (attn_mx.hip:
 // v_mfma_f32_16x16x4_f32 is an fmaf chain over K, so vec_dot_f16's chains ride it bit for bit),
 // else per row with v_fma_mix (k_attn_rows).  GHIP_ATT_MX=0 forces the row form (tests, A/B).
-static int launch_attn_exact(const attnp_args &at, hipStream_t s) {
+// The form is resolved once per prefill (att_mx_form): the env switch and the shape check do not
+// change between its layers.
+static bool att_mx_form(const attnp_args &at) {
     const char *env = getenv("GHIP_ATT_MX");
-    const bool mx = !env || atoi(env) != 0;
-    if (mx && attn_mx_unsupported(at).empty()) return launch_attn_mx(at, s);
-    return launch_attn_rows(at, s);
+    return (!env || atoi(env) != 0) && !attn_mx_unsupported(at);
+}
+static int launch_attn_exact(const attnp_args &at, bool mx, hipStream_t s) {
+    return mx ? launch_attn_mx(at, s) : launch_attn_rows(at, s);
 }
 
 static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nullptr) {
     const gemma_hip_config &c = e->cfg;
     hipStream_t s = e->stream;
+    int mx_form = -1;  // the exact attention's form, resolved at the first layer
     auto &p = e->pf;
     const int wt = c.wtype;
     const int64_t E = c.n_embd, F = c.n_ff;
@@ -1961,7 +1972,8 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
         attnp_args at;
         at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
         at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
-        if (exact ? launch_attn_exact(at, s) : launch_attn_prefill(at, s)) return -1;
+        if (mx_form < 0) mx_form = att_mx_form(at);
+        if (exact ? launch_attn_exact(at, mx_form == 1, s) : launch_attn_prefill(at, s)) return -1;
         if (quant(QR_F32, p.ATT, nullptr, e->qw, nullptr)) return -1;
         if (gemm(L.o, EPI_ADD, p.X, p.SA, E)) return -1;
         if (quant(QR_NORM, p.SA, nullptr, E, L.ffn_norm)) return -1;
@@ -2015,6 +2027,7 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
 static int enqueue_prefill_kq(gemma_engine *e, int T) {
     const gemma_hip_config &c = e->cfg;
     hipStream_t s = e->stream;
+    int mx_form = -1;  // the exact attention's form, resolved at the first layer
     auto &p = e->pf;
     const int64_t E = c.n_embd, F = c.n_ff;
     const int64_t ldk = p.ldq / 256 * 292;  // Q8_K column stride in XQ
@@ -2067,7 +2080,8 @@ static int enqueue_prefill_kq(gemma_engine *e, int T) {
         attnp_args at;
         at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
         at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
-        if (launch_attn_exact(at, s)) return -1;
+        if (mx_form < 0) mx_form = att_mx_form(at);
+        if (launch_attn_exact(at, mx_form == 1, s)) return -1;
         if (launch_quant_q8_K(p.ATT, e->qw, e->qw, T, img, ldk, s) || expand(e->qw)) return -1;
         if (mv(K.o, p.SA, E, p.X, nullptr, nullptr)) return -1;  // + inpL
         if (launch_norm_q8K(p.SA, E, L.ffn_norm, (int)E, c.eps, T, img, ldk, s) || expand(E)) return -1;
@@ -2298,6 +2312,44 @@ extern "C" int gemma_test_exp_f16(uint16_t *out) {
     return r;
 }
 
+// Test hook: one rms_norm kernel on `rows` host rows of n f32.  kind 0: the ggml
+// executor's RMS_NORM (k_g_rms_norm), out = f32 rows x * scale; kind 1: k_norm_q8K (rms_norm * w then
+// quantize_row_q8_K, n a multiple of 256, <= 4096), out = Q8_K rows.
+extern "C" int gemma_test_rms_norm(int kind, const float *x, const float *w, int rows, int n, float eps, void *out) {
+    set_error("");
+    if (rows <= 0 || n <= 0 || (kind == 1 && (n % 256 || n > 4096)) || kind < 0 || kind > 1) {
+        set_error("gemma_test_rms_norm: unsupported shape or kind");
+        return -1;
+    }
+    const size_t in_b = (size_t)rows * n * 4, out_b = kind == 0 ? in_b : (size_t)rows * (n / 256) * 292;
+    float *dx = nullptr, *dw = nullptr;
+    uint8_t *dy = nullptr;
+    GHIP_CHECK(hipMalloc(&dx, in_b));
+    GHIP_CHECK(hipMalloc(&dw, (size_t)n * 4));
+    GHIP_CHECK(hipMalloc(&dy, out_b));
+    GHIP_CHECK(hipMemcpy(dx, x, in_b, hipMemcpyHostToDevice));
+    if (w) GHIP_CHECK(hipMemcpy(dw, w, (size_t)n * 4, hipMemcpyHostToDevice));
+    int r;
+    if (kind == 0) {
+        gt_desc a, d;
+        a.data = (char *)dx;
+        d.data = (char *)dy;
+        a.ne[0] = d.ne[0] = n;
+        a.ne[1] = d.ne[1] = rows;
+        a.nb[0] = d.nb[0] = 4;
+        a.nb[1] = d.nb[1] = (int64_t)n * 4;
+        a.nb[2] = d.nb[2] = a.nb[3] = d.nb[3] = (int64_t)n * rows * 4;
+        r = launch_g_rms_norm(a, d, eps, nullptr);
+    } else {
+        r = launch_norm_q8K(dx, n, dw, n, eps, rows, dy, (n / 256) * 292, nullptr);
+    }
+    if (r == 0) GHIP_CHECK(hipMemcpy(out, dy, out_b, hipMemcpyDeviceToHost));
+    (void)hipFree(dx);
+    (void)hipFree(dw);
+    (void)hipFree(dy);
+    return r;
+}
+
 // Measured HBM read roofline: a streaming read of `bytes` (>= 4 GB defeats the
 // Infinity Cache), `iters` passes timed with hipEvents; returns GB/s (negative on error).
 extern "C" double gemma_hbm_read_gbs(int device, size_t bytes, int iters) {
@@ -2395,26 +2447,33 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
     } else {
         GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
     }
-    if (persist_on(e)) {  // a hand-off timeout: redo this token on the per-layer launches (same bits)
-        GHIP_CHECK(hipStreamSynchronize(e->stream));
-        if (persist_check(e)) {
-            fprintf(stderr, "[gemma_hip] %s; token at position %d redone\n", last_error().c_str(), pos);
-            set_error("");
-            if (ext_set_position(e, token, pos) || enqueue_step(e)) return -1;
-        }
-    }
     if (prof) GHIP_CHECK(hipStreamSynchronize(e->stream));
     const double t1 = prof ? us() : 0.0;
-    // logits through a pinned staging row (a pageable device-to-host copy stages through the driver)
+    // logits through a pinned staging row (a pageable device-to-host copy stages through the driver);
+    // with the persistent launch its sticky timeout word rides along, so ONE sync covers both
     const size_t lb = (size_t)c.n_vocab * 4;
     static const int direct = getenv("GHIP_EXT_DIRECT") ? atoi(getenv("GHIP_EXT_DIRECT")) : 0;
-    if (direct) {  // A/B: straight into the (pageable) graph tensor
-        GHIP_CHECK(hipMemcpyAsync(logits, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
+    const bool pchk = persist_on(e) && e->tok_err;
+    auto copy_out = [&]() -> int {
+        if (pchk) {
+            if (!e->ext_err) GHIP_CHECK(hipHostMalloc((void **)&e->ext_err, 16, hipHostMallocDefault));
+            GHIP_CHECK(hipMemcpyAsync(e->ext_err, e->tok_err, 12, hipMemcpyDeviceToHost, e->stream));
+        }
+        if (direct) {  // A/B: straight into the (pageable) graph tensor
+            GHIP_CHECK(hipMemcpyAsync(logits, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
+        } else {
+            if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, lb, hipHostMallocDefault));
+            GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
+        }
         GHIP_CHECK(hipStreamSynchronize(e->stream));
-    } else {
-        if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, lb, hipHostMallocDefault));
-        GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
-        GHIP_CHECK(hipStreamSynchronize(e->stream));
+        return 0;
+    };
+    if (copy_out()) return -1;
+    if (pchk && persist_report(e, e->ext_err)) {  // a hand-off timeout: redo the token on the per-layer launches
+        fprintf(stderr, "[gemma_hip] %s; token at position %d redone\n", last_error().c_str(), pos);
+        set_error("");
+        if (ext_set_position(e, token, pos) || enqueue_step(e)) return -1;
+        if (copy_out()) return -1;
     }
     const double t2 = prof ? us() : 0.0;
     if (!direct) memcpy(logits, e->ext_stage, lb);

@@ -105,7 +105,8 @@ __global__ void k_g_elementwise(int op, gt_desc a, gt_desc b, gt_desc dst, float
     }
 }
 
-// RMS_NORM per row: sum of (double)(x*x) (a fixed tree; exact for same-scale terms),
+// RMS_NORM per row: sum of (double)(x*x) (a fixed tree, proven equal to ggml's sequential sum by
+// rms_mean_certain or replaced by that sum),
 // mean = (float)(sum/n), y = x * (1/sqrtf(mean + eps))
 __global__ void __launch_bounds__(256) k_g_rms_norm(gt_desc a, gt_desc dst, float eps) {
     const int64_t r = blockIdx.x, n = a.ne[0];
@@ -124,7 +125,12 @@ __global__ void __launch_bounds__(256) k_g_rms_norm(gt_desc a, gt_desc dst, floa
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    const float mean = (float)(red[0] / (double)n);
+    float mean = (float)(red[0] / (double)n);
+    if (!rms_mean_certain(red[0], n, mean))  // workgroup-uniform; rare: ggml's own order
+        mean = (float)(seq_sumsq_wave(n, [&](int64_t i0, float v[8]) {
+                           for (int j = 0; j < 8; ++j)
+                               v[j] = i0 + j < n ? *(const float *)(src + (i0 + j) * a.nb[0]) : 0.0f;
+                       }) / (double)n);
     const float scale = 1.0f / sqrtf(mean + eps);
     for (int64_t k = threadIdx.x; k < n; k += 256)
         *(float *)(out + k * dst.nb[0]) = *(const float *)(src + k * a.nb[0]) * scale;

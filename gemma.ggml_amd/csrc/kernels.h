@@ -250,8 +250,12 @@ int launch_attn_prefill(const attnp_args &a, hipStream_t s);
 int launch_attn_rows(const attnp_args &a, hipStream_t s);
 // the same rows on the f32 matrix cores (attn_mx.hip): v_mfma_f32_16x16x4_f32 is an fmaf chain over K,
 // so vec_dot_f16's 32 chains ride K four steps at a time; "" when it runs the shapes
-std::string attn_mx_unsupported(const attnp_args &a);
+const char *attn_mx_unsupported(const attnp_args &a);  // nullptr: the matrix-core form runs these shapes
 int launch_attn_mx(const attnp_args &a, hipStream_t s);
+// hipFuncAttributeMaxDynamicSharedMemorySize of a kernel raised to the CU's whole LDS, once per
+// (slot, device), thread-safe: slots LDS_SLOT_*
+enum { LDS_SLOT_ATTN_MX = 0, LDS_SLOT_GELU_LDS = 1, LDS_SLOTS = 2 };
+int allow_full_lds(const void *fn, int slot);
 int launch_row_argmax(const float *row, int64_t n, unsigned long long *keys, int parts, hipStream_t s);
 
 // ---- weights (ops.hip) ------------------------------------------------------------------------

@@ -245,6 +245,23 @@ __device__ __forceinline__ void kq_pro_load(const kq_args &a, int col, int wave,
     }
 }
 
+// 1/sqrtf(mean + eps) of the column's rms_norm from the prologue's tree sum T (*mean = the tree's
+// mean; the caller checks it with rms_mean_certain after the image is built)
+__device__ __forceinline__ float kq_norm_scale(const kq_args &a, double T, float *mean) {
+    *mean = (float)(T / (double)((int64_t)a.nsb * 256));
+    return 1.0f / sqrtf(*mean + a.eps);
+}
+// the same from ggml's sequential sum (every wave runs it itself: the rare slow path)
+__device__ __forceinline__ float kq_seq_scale(const kq_args &a, int col) {
+    const int64_t n = (int64_t)a.nsb * 256;
+    const float *x = a.xf + (int64_t)col * a.xf_col_stride;
+    const float mean = (float)(seq_sumsq_wave(n, [&](int64_t i0, float v[8]) {
+                                   const float4 u = *(const float4 *)(x + i0), w = *(const float4 *)(x + i0 + 4);
+                                   v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
+                               }) / (double)n);
+    return 1.0f / sqrtf(mean + a.eps);
+}
+
 template <int XJ>
 __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col, int tid, int nth,
                              const kq_pro_regs<XJ> &r) {
@@ -253,7 +270,8 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
         return;
     }
     const int nw = nth >> 6, lane = tid & 63, wave = tid >> 6;
-    float scale = 1.0f;
+    float scale = 1.0f, mean = 0.0f;
+    double tsum = 0.0;
     // this wave holds super-blocks wave and wave + nw: the tree's first level (h = nw*64) pairs
     // exactly them, so it runs in registers, and their two quantizations interleave
     const bool two = XJ == 2 && a.nsb == 2 * nw;
@@ -299,8 +317,8 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
                 m = h;
             }
             v = __shfl(v, 0);
-            const float mean = (float)(v / (double)(a.nsb * 256));
-            scale = 1.0f / sqrtf(mean + a.eps);
+            tsum = v;
+            scale = kq_norm_scale(a, v, &mean);
             n = 0;  // done
         } else if (two) {
             red[wave * 64 + lane] = part[0] + part[XJ - 1];
@@ -329,30 +347,36 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
             if (lane == 0) red[0] = v;
         }
         __syncthreads();
-        const float mean = (float)(red[0] / (double)(a.nsb * 256));
-        scale = 1.0f / sqrtf(mean + a.eps);
+        tsum = red[0];
+        scale = kq_norm_scale(a, tsum, &mean);
         }
     }
-    float y[XJ][4];
+    auto emit = [&](float sc) {
+        float y[XJ][4];
 #pragma unroll
-    for (int j = 0; j < XJ; ++j) {
-        y[j][0] = r.x[j].x; y[j][1] = r.x[j].y; y[j][2] = r.x[j].z; y[j][3] = r.x[j].w;
-        if (a.pro == KQP_NORM) {
-            y[j][0] = pin(y[j][0] * scale) * r.w[j].x;
-            y[j][1] = pin(y[j][1] * scale) * r.w[j].y;
-            y[j][2] = pin(y[j][2] * scale) * r.w[j].z;
-            y[j][3] = pin(y[j][3] * scale) * r.w[j].w;
+        for (int j = 0; j < XJ; ++j) {
+            y[j][0] = r.x[j].x; y[j][1] = r.x[j].y; y[j][2] = r.x[j].z; y[j][3] = r.x[j].w;
+            if (a.pro == KQP_NORM) {
+                y[j][0] = pin(y[j][0] * sc) * r.w[j].x;
+                y[j][1] = pin(y[j][1] * sc) * r.w[j].y;
+                y[j][2] = pin(y[j][2] * sc) * r.w[j].z;
+                y[j][3] = pin(y[j][3] * sc) * r.w[j].w;
+            }
         }
-    }
-    if (two) {
-        q8K_store_n<XJ>(y, lane, xs + (int64_t)wave * 292, nw * 292);
-        return;
-    }
+        if (two) {
+            q8K_store_n<XJ>(y, lane, xs + (int64_t)wave * 292, nw * 292);
+            return;
+        }
 #pragma unroll
-    for (int j = 0; j < XJ; ++j) {
-        const int sb = wave + nw * j;
-        if (sb < a.nsb) q8K_store(y[j], lane, xs + (int64_t)sb * 292);  // wave-uniform
-    }
+        for (int j = 0; j < XJ; ++j) {
+            const int sb = wave + nw * j;
+            if (sb < a.nsb) q8K_store(y[j], lane, xs + (int64_t)sb * 292);  // wave-uniform
+        }
+    };
+    emit(scale);
+    // checked after the image is built (off the critical path); rare, workgroup-uniform: ggml's own
+    // order, image rebuilt
+    if (a.pro == KQP_NORM && !rms_mean_certain(tsum, (int64_t)a.nsb * 256, mean)) emit(kq_seq_scale(a, col));
 }
 
 __device__ __forceinline__ double *kq_red(uint8_t *xs, int nsb) {
@@ -474,7 +498,12 @@ __device__ __forceinline__ void kq_handoff(const kq_args &a, int col, int64_t g,
         part[k] = p;
     }
     const double sum = kq_tree(part, nsb_y, lane, (double *)lds);
-    const float mean = (float)(sum / (double)a.rows);
+    float mean = (float)(sum / (double)a.rows);
+    if (!rms_mean_certain(sum, a.rows, mean))  // rare: ggml's own order, from the same sc1 loads
+        mean = (float)(seq_sumsq_wave(a.rows, [&](int64_t i0, float v[8]) {
+                           const float4 u = kq_ld4_sc1(y + i0, a.q8_abl & 8), w = kq_ld4_sc1(y + i0 + 4, a.q8_abl & 8);
+                           v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
+                       }) / (double)a.rows);
     const float scale = 1.0f / sqrtf(mean + a.eps);
     float yv[8][4];
 #pragma unroll
@@ -926,7 +955,14 @@ __global__ void __launch_bounds__(1024) k_norm_q8K(const float *x, int64_t ldx, 
         __syncthreads();
         n = h;
     }
-    const float mean = (float)(red[0] / (double)E);
+    float mean = (float)(red[0] / (double)E);
+    if (!rms_mean_certain(red[0], E, mean)) {  // workgroup-uniform; rare: ggml's own order
+        const float *xr = x + (int64_t)r * ldx;
+        mean = (float)(seq_sumsq_wave(E, [&](int64_t i0, float v[8]) {
+                           const float4 u = *(const float4 *)(xr + i0), w4 = *(const float4 *)(xr + i0 + 4);
+                           v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w4.x; v[5] = w4.y; v[6] = w4.z; v[7] = w4.w;
+                       }) / (double)E);
+    }
     const float scale = 1.0f / sqrtf(mean + eps);
     const float4 wv = *(const float4 *)(w + tid * 4);
     const float ww[4] = {wv.x, wv.y, wv.z, wv.w};

@@ -89,9 +89,11 @@ __device__ void rr_tiles(const mv_args &a, int64_t rt0, int64_t rt1, uint8_t *sm
     const bool loader = wave < RR_NL;
     const int nt = rt1 >= 0 ? 2 : 1;
     act_regs<R> ar;
+    norm_state ns;
     if (!WAIT) {
         prefetch_activation<WT, PRO, R, LF_NTH>(a, 0, ar);
-        build_activation<WT, PRO, R, NSA, LF_NTH>(a, 0, smem, m, ar);
+        ns = build_activation<WT, PRO, R, NSA, LF_NTH>(a, 0, smem, m, ar);
+        finish_activation<WT, PRO, R, NSA, LF_NTH>(a, 0, smem, m, ar, ns);  // the norm's check
     }
     uint4 qb[2], sb[2];
     const uint32_t q_off = (uint32_t)lane * 16u, s_off = (uint32_t)rr * SB;
@@ -122,7 +124,7 @@ __device__ void rr_tiles(const mv_args &a, int64_t rt0, int64_t rt1, uint8_t *sm
 #pragma unroll
             for (int k = 0; k < 4; ++k) dst[k] = __builtin_bit_cast(float, ld_sc1_u(p + k));
         }
-        build_activation<WT, PRO, R, NSA, LF_NTH>(a, 0, smem, m, ar);
+        build_activation<WT, PRO, R, NSA, LF_NTH>(a, 0, smem, m, ar);  // PRO_IMG: no norm
     }
     lds_barrier();
     if (wave == RR_NL) __builtin_amdgcn_s_setprio(3);

@@ -213,14 +213,75 @@ __device__ __forceinline__ void prefetch_activation(const mv_args &a, int col, a
     }
 }
 
+// The rms_norm's tree sum and mean (PRO_NORM / PRO_EMBED), kept for finish_activation's check.
+struct norm_state {
+    double tsum = 0.0;
+    float mean = 0.0f;
+};
+
+// element values of the activation and the image writer shared by build_ and finish_activation
 template <int WT, int PRO, int R, bool NSA, int NTH>
-__device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const lds_map &m, const act_regs<R> &r) {
+struct act_src {
+    const mv_args &a;
+    const act_regs<R> &r;
+    const float *x;
+    int64_t tok = 0;
+    int q;
+    __device__ act_src(const mv_args &a_, int col, const act_regs<R> &r_) : a(a_), r(r_) {
+        x = (const float *)((const uint8_t *)a.x + (int64_t)col * a.x_col_stride);
+        if (PRO == PRO_EMBED) tok = ((const int *)a.x)[*a.tok_pos];
+        q = threadIdx.x & 3;
+    }
+    // value of block (tid>>2) + i*nquads: from registers when cached, else loaded now (RELOAD: always
+    // loaded, so the registers are dead past the first image)
+    template <bool RELOAD = false>
+    __device__ __forceinline__ void get(int i, int64_t b, float v[8]) const {
+        constexpr bool CACHED = (PRO == PRO_F32 || PRO == PRO_NORM) && !RELOAD;
+        if (CACHED && i < R) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = r.x[i < R ? i : 0][j];
+        } else {
+            load8<WT, PRO>(a, x, tok, b * 32 + q * 8, v);
+        }
+    }
+    // the image of rms_norm(x)*norm_w (PRO_NORM / PRO_EMBED, scale sc) or of x (PRO_F32)
+    template <bool RELOAD = false>
+    __device__ void emit(uint8_t *smem, const lds_map &m, float sc) const {
+        const int nquads = NTH >> 2;
+        int i = 0;
+        for (int64_t b = threadIdx.x >> 2; b < a.nb; b += nquads, ++i) {
+            float v[8];
+            get<RELOAD>(i, b, v);
+            if (PRO == PRO_NORM || PRO == PRO_EMBED) {
+                float wv[8];
+                if (PRO == PRO_NORM && i < R && !RELOAD) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wv[j] = r.w[i < R ? i : 0][j];
+                } else {
+                    const float4 w0 = *(const float4 *)(a.norm_w + b * 32 + q * 8);
+                    const float4 w1 = *(const float4 *)(a.norm_w + b * 32 + q * 8 + 4);
+                    wv[0] = w0.x; wv[1] = w0.y; wv[2] = w0.z; wv[3] = w0.w;
+                    wv[4] = w1.x; wv[5] = w1.y; wv[6] = w1.z; wv[7] = w1.w;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float t = v[j] * sc;  // rms_norm output
+                    v[j] = t * wv[j];           // ggml_mul by the norm weight
+                }
+            }
+            put_quad<WT, NSA>(smem, m, b, q, v);
+        }
+    }
+};
+
+template <int WT, int PRO, int R, bool NSA, int NTH>
+__device__ norm_state build_activation(const mv_args &a, int col, uint8_t *smem, const lds_map &m, const act_regs<R> &r) {
     constexpr int BT = wfmt<WT>::BT;
-    constexpr bool CACHED = PRO == PRO_F32 || PRO == PRO_NORM;
     const int tid = threadIdx.x, nth = NTH;
     const int64_t nb = a.nb, nb_pad = a.n_bt * BT;
     const int q = tid & 3;
     const int nquads = nth >> 2;
+    norm_state ns;
     // padded tail blocks: zero (d = 0 makes every chain step an exact no-op)
     for (int64_t b = nb + (tid >> 2); b < nb_pad; b += nquads) {
         float z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -229,7 +290,7 @@ __device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const
     if (PRO == PRO_Q8) {
         const block_q8_0 *xb = (const block_q8_0 *)((const uint8_t *)a.x + (int64_t)col * a.x_col_stride);
         for (int64_t b = tid; b < nb; b += nth) put_block_q8<WT, NSA>(smem, m, b, xb + b);
-        return;
+        return ns;
     }
     if (PRO == PRO_IMG) {
         const int64_t n_act = nb * 2, T = n_act + nb / 4;
@@ -254,28 +315,19 @@ __device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const
                                    __builtin_bit_cast(uint32_t, src[2]), __builtin_bit_cast(uint32_t, src[3])));
         }
         for (int64_t it = tid + (int64_t)2 * R * nth; it < T; it += nth) put(it, *img_item(a, it));  // long K
-        return;
+        return ns;
     }
-    const float *x = (const float *)((const uint8_t *)a.x + (int64_t)col * a.x_col_stride);
-    int64_t tok = 0;
-    if (PRO == PRO_EMBED) tok = ((const int *)a.x)[*a.tok_pos];
-    // value of block (tid>>2) + i*nquads: from registers when cached, else loaded now
-    auto get = [&](int i, int64_t b, float v[8]) {
-        if (CACHED && i < R) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = r.x[i < R ? i : 0][j];
-        } else {
-            load8<WT, PRO>(a, x, tok, b * 32 + q * 8, v);
-        }
-    };
+    const act_src<WT, PRO, R, NSA, NTH> src(a, col, r);
     float scale = 1.0f;
     if (PRO == PRO_NORM || PRO == PRO_EMBED) {
-        // rms_norm: double sum of fp32 squares; fixed-order tree
+        // rms_norm: double sum of fp32 squares in a fixed tree.  Its mean is checked
+        // against ggml's sequential sum by finish_activation, which rebuilds the image from the
+        // sequential sum in the rare case the check fails
         double part = 0.0;
         int i = 0;
         for (int64_t b = tid >> 2; b < nb; b += nquads, ++i) {
             float v[8];
-            get(i, b, v);
+            src.get(i, b, v);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float sq = v[j] * v[j];
@@ -293,33 +345,29 @@ __device__ void build_activation(const mv_args &a, int col, uint8_t *smem, const
         __syncthreads();
         double sum = 0.0;
         for (int w = 0; w < nth / 64; ++w) sum += red[w];
-        const float mean = (float)(sum / (double)(nb * 32));
-        scale = 1.0f / sqrtf(mean + a.eps);
+        ns.mean = (float)(sum / (double)(nb * 32));
+        ns.tsum = sum;
+        scale = 1.0f / sqrtf(ns.mean + a.eps);
     }
-    int i = 0;
-    for (int64_t b = tid >> 2; b < nb; b += nquads, ++i) {
-        float v[8];
-        get(i, b, v);
-        if (PRO == PRO_NORM || PRO == PRO_EMBED) {
-            float wv[8];
-            if (PRO == PRO_NORM && i < R) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) wv[j] = r.w[i < R ? i : 0][j];
-            } else {
-                const float4 w0 = *(const float4 *)(a.norm_w + b * 32 + q * 8);
-                const float4 w1 = *(const float4 *)(a.norm_w + b * 32 + q * 8 + 4);
-                wv[0] = w0.x; wv[1] = w0.y; wv[2] = w0.z; wv[3] = w0.w;
-                wv[4] = w1.x; wv[5] = w1.y; wv[6] = w1.z; wv[7] = w1.w;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float t = v[j] * scale;  // rms_norm output
-                v[j] = t * wv[j];              // ggml_mul by the norm weight
-            }
-        }
-        put_quad<WT, NSA>(smem, m, b, q, v);
-    }
+    src.emit(smem, m, scale);
+    return ns;
 }
+
+// The norm's check (rms_mean_certain: multiplications only, a few dozen cycles after the image is
+// built), before the caller issues the rest of its weight ring (the fallback's registers beside a full
+// ring cost occupancy and spills).  Workgroup-uniform; in the rare failing case ggml's sequential sum
+// (seq_sumsq_wave, every wave) and the image rebuilt.
+template <int WT, int PRO, int R, bool NSA, int NTH>
+__device__ __forceinline__ void finish_activation(const mv_args &a, int col, uint8_t *smem, const lds_map &m,
+                                                  const act_regs<R> &r, const norm_state &ns) {
+    if (PRO != PRO_NORM && PRO != PRO_EMBED) return;
+    const int64_t n = a.nb * 32;
+    if (rms_mean_certain(ns.tsum, n, ns.mean)) return;
+    const act_src<WT, PRO, R, NSA, NTH> src(a, col, r);
+    const float mean = (float)(seq_sumsq_wave(n, [&](int64_t i0, float v[8]) { load8<WT, PRO>(a, src.x, src.tok, i0, v); }) /
+                               (double)n);
+    src.template emit<true>(smem, m, 1.0f / sqrtf(mean + a.eps));  // reloads x and w: the prologue's
+}                                                                  // registers are dead here
 
 // ---- one 8-row x BT-block tile for this thread's (row rr, lane l) ----------------------------
 // d = f32(dw) * da with the fp16 operand converted inside v_fma_mix_f32 (addend +0: the sign of a
@@ -832,7 +880,13 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
     if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 1] = __builtin_amdgcn_s_memrealtime();
 
     // 2) activation image in LDS
-    if (!(a.ablate & 1)) build_activation<WT, PRO, R, NSA, NTH>(a, col, smem, m, ar);
+    norm_state ns;
+    if (!(a.ablate & 1)) {  // timing ablations only
+        ns = build_activation<WT, PRO, R, NSA, NTH>(a, col, smem, m, ar);
+        // the norm's check before the rest of the ring: the fallback's registers would otherwise sit
+        // beside the whole ring's (measured: VGPRs 44 -> 74 on the rr kernel, spills on long K)
+        finish_activation<WT, PRO, R, NSA, NTH>(a, col, smem, m, ar, ns);
+    }
 #pragma unroll
     for (int u = UP; u < U; ++u) issue(qb[u], sb[u]);
     if (GHIP_STAMPS && a.dbg_t && tid == 0) a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 2] = __builtin_amdgcn_s_memrealtime();
@@ -1049,7 +1103,8 @@ __global__ void __launch_bounds__(512) k_matvec_gu2(mv_args a) {
     constexpr int UP = GHIP_UPRE < U ? GHIP_UPRE : U;
 #pragma unroll
     for (int u = 0; u < UP; ++u) issue(qb[u], sb[u]);
-    build_activation<WT, PRO_NORM, 1, NSA, NTH>(a, 0, smem, m, ar);
+    const norm_state ns = build_activation<WT, PRO_NORM, 1, NSA, NTH>(a, 0, smem, m, ar);
+    finish_activation<WT, PRO_NORM, 1, NSA, NTH>(a, 0, smem, m, ar, ns);
 #pragma unroll
     for (int u = UP; u < U; ++u) issue(qb[u], sb[u]);
     __syncthreads();

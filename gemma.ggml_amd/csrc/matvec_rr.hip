@@ -59,7 +59,10 @@ __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
     for (int r = 0; r < P; ++r) issue(r);
     act_regs<R> ar;
     prefetch_activation<WT, PRO, R, RR_NTH>(a, col, ar);
-    if (!(a.ablate & 1)) build_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar);  // timing ablations only
+    if (!(a.ablate & 1)) {  // timing ablations only
+        const norm_state ns = build_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar);
+        finish_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar, ns);  // the norm's check
+    }
     if (GHIP_STAMPS && stp && tid == 0) stp[10] = __builtin_amdgcn_s_memrealtime();
     // 1) the rest of the ring (loader w, round r -> block tile w + 8r; D rounds in flight per wave),
     //    issued after the image is used, so these loads may sit in a loader-only branch

@@ -8,6 +8,7 @@
 // block order instead of 8 lane chains + fold), so prefill logits match the CPU path to ~1e-6
 // relative (tests: 1e-3), while the per-token decode path stays bit-exact.
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 #include "device_util.h"
@@ -131,7 +132,9 @@ __global__ void __launch_bounds__(256) k_quant_rows(qrow_args a) {
         if ((tid & 63) == 0) red[tid >> 6] = part;
         __syncthreads();
         const double sum = red[0] + red[1] + red[2] + red[3];
-        const float mean = (float)(sum / (double)K);
+        float mean = (float)(sum / (double)K);
+        if (!rms_mean_certain(sum, K, mean))  // workgroup-uniform; rare: ggml's own order
+            mean = (float)(seq_sumsq_wave(K, [&](int64_t i0, float v[8]) { load(i0, v); }) / (double)K);
         scale = 1.0f / sqrtf(mean + a.eps);
     }
     for (int64_t b = tid >> 2; b < nb; b += 64) {
@@ -933,11 +936,7 @@ int launch_quant_rows(int mode, const qrow_args &a, int T, hipStream_t s) {
             // prefill 78.4 -> 77.5 ms (this kernel 109 -> ~57 us per layer)
             const char *env = getenv("GHIP_QR_GELU_LDS");
             if (!env || atoi(env)) {
-                static bool attr = false;
-                if (!attr) {
-                    GHIP_CHECK(hipFuncSetAttribute((const void *)k_quant_gelu_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 65536 * 2));
-                    attr = true;
-                }
+                if (allow_full_lds((const void *)k_quant_gelu_lds, LDS_SLOT_GELU_LDS)) return -1;
                 hipLaunchKernelGGL(k_quant_gelu_lds, dim3((unsigned)std::min(T, 256)), dim3(QG_THREADS), 65536 * 2, s, a, T);
             } else {
                 hipLaunchKernelGGL(k_quant_rows<QR_GELU>, dim3(T), dim3(256), 0, s, a);
@@ -1018,4 +1017,25 @@ int launch_attn_prefill(const attnp_args &a, hipStream_t s) {
     return 0;
 }
 
+}  // namespace ghip
+
+namespace ghip {
+// hipFuncAttributeMaxDynamicSharedMemorySize = the CU's 160 KiB, once per (slot, device): the
+// attribute only caps a launch's dynamic LDS, so the whole LDS serves every later size; std::call_once
+// makes it thread-safe and the per-device flag correct for engines on several GPUs.
+int allow_full_lds(const void *fn, int slot) {
+    static std::once_flag once[LDS_SLOTS][64];
+    static hipError_t err[LDS_SLOTS][64];
+    int dev = 0;
+    GHIP_CHECK(hipGetDevice(&dev));
+    if (slot < 0 || slot >= LDS_SLOTS || dev < 0 || dev >= 64) {
+        set_error("allow_full_lds: bad slot or device");
+        return -1;
+    }
+    std::call_once(once[slot][dev], [&] {
+        err[slot][dev] = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    GHIP_CHECK(err[slot][dev]);
+    return 0;
+}
 }  // namespace ghip

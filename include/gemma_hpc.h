@@ -161,6 +161,10 @@ double gemma_kq_time(int type, int64_t rows, int64_t K, int iters, double *algo_
 double gemma_hbm_read_gbs(int device, size_t bytes, int iters);
 /* per-op test entry: the softmax's exp(f16) for all 65536 codes (compared with ggml's table) */
 int gemma_test_exp_f16(uint16_t *out);
+/* per-op test entry: one rms_norm kernel on host rows (ggml rms_norm):
+ * kind 0 the ggml executor's RMS_NORM (out f32 rows), kind 1 k_norm_q8K (rms_norm * w, then
+ * quantize_row_q8_K; out Q8_K rows) */
+int gemma_test_rms_norm(int kind, const float *x, const float *w, int rows, int n, float eps, void *out);
 
 #ifdef __cplusplus
 }

@@ -220,6 +220,15 @@ class Model:
         p = self.L.orc_model_tensor(self.h, tid, C.byref(n))
         return np.ctypeslib.as_array((C.c_uint8 * n.value).from_address(p)).copy()
 
+    def poke(self, tid, offset, data):
+        """Overwrite bytes of one of the model's tensors in place (test construction of adversarial
+        weights; the oracle then computes with them as with its own)."""
+        n = C.c_int64()
+        p = self.L.orc_model_tensor(self.h, tid, C.byref(n))
+        data = np.ascontiguousarray(data).view(np.uint8).ravel()
+        assert p and 0 <= offset and offset + data.size <= n.value, (tid, offset, data.size, n.value)
+        C.memmove(p + offset, data.ctypes.data, data.size)
+
     def reset(self):
         self.L.orc_model_reset_kv(self.h)
 

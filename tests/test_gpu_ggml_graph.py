@@ -98,7 +98,8 @@ def _check_out(m, prompt, n_decode, V, opath):
     return seq
 
 
-def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fast=1, second_seed=None, register=1):
+def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fast=1, second_seed=None, register=1,
+         poke=None, prompt=None):
     """fast=1: the executor recognises the Gemma graph and runs the device-resident engine over the
     graph's weights and KV-cache mirrors (ggml_api.cpp try_fast); fast=0: node by node.
     second_seed: a second model of the same shapes (other weights) run after the first in the same
@@ -106,6 +107,8 @@ def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fa
     register (GGUF): the driver pre-uploads every quantized weight at load (hpc_register_weight) and
     the fast path's engine copies them device to device; 0: the engine uploads from the host."""
     m = O.Model(O.make_config(shape, n_ctx=ctx, wtype=wtype, kmix=kmix))
+    if poke is not None:  # adversarial weights (tests/test_gpu_norm_exact.py), oracle and file alike
+        poke(m)
     wpath, ppath, opath = tmp_path / ("m.gguf" if gguf else "w.bin"), tmp_path / "p.bin", tmp_path / "o.bin"
     if gguf:
         write_gguf(m, shape, wpath, kmix)
@@ -115,7 +118,9 @@ def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fa
     if second_seed is not None:
         m2 = O.Model(O.make_config(shape, n_ctx=ctx, wtype=wtype, kmix=kmix, seed=second_seed))
         _write_weights(m2, shape, tmp_path / "w2.bin")
-    prompt = np.array(O.make_prompt(n_prompt, shape["n_vocab"]), dtype=np.int32)
+    if prompt is None:
+        prompt = O.make_prompt(n_prompt, shape["n_vocab"])
+    prompt = np.array(prompt, dtype=np.int32)
     prompt.tofile(ppath)
     if gguf:
         args = [DRIVER, str(wpath), str(ppath), str(opath), str(ctx), str(n_decode)]

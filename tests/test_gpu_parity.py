@@ -378,3 +378,59 @@ def test_fused_layer_front_gemma2b_bitexact(wtype, fuse):
     assert list(e.tokens()[: len(seq_ref)]) == list(seq_ref)
     assert np.array_equal(lg[len(prompt) - 1:].view(np.uint32), lg_ref.view(np.uint32))
     e.close()
+
+
+def _bench_prompt(n):
+    # bench.make_prompt(n, 256000) (seed 1) is this very generator: the benched prompt rows
+    return O.make_prompt(n, O.GEMMA_2B["n_vocab"])
+
+
+@gpu
+def test_decode_gemma2b_bench_positions_bitexact():
+    """BASELINE config 2 exactly as bench.py runs it (src/gemma_model.cpp:548-563): Gemma-2B Q4_0,
+    n_ctx 512, the measured launch plan, the 128-token prompt stepped through the hipGraph, then
+    24 greedy decode steps — positions 128..151, the benched ones.  Every logit of the last prompt
+    row and of each decode step against the oracle's PREFILL + DECODE sequence."""
+    import gemma_hip as G
+    O.lib().orc_set_threads(16)
+    prompt = _bench_prompt(128)
+    m = O.Model(O.make_config(O.GEMMA_2B, n_ctx=512))
+    seq_ref, lg_ref = m.generate(prompt, 24)
+    m.close()
+    e = G.Engine(O.GEMMA_2B, n_ctx=512)
+    e.tune(6)
+    e.begin(prompt)
+    lg = e.step(len(prompt) + 24, want_logits=True, use_graph=True)
+    toks = list(e.tokens()[: len(seq_ref)])
+    e.close()
+    assert toks == list(seq_ref)
+    got = lg[len(prompt) - 1:]
+    bad = np.argwhere(got.view(np.uint32) != lg_ref.view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} logits differ, first {bad[:5]}"
+
+
+@gpu
+def test_decode_gemma2b_q8_0_full_bitexact():
+    """BASELINE config 5 at full size: Gemma-2B Q8_0 (all 18 layers, the 256,000-row output), the
+    measured plan, a 16-token prompt, 6 decode steps; also the batched exact prefill of that prompt."""
+    import gemma_hip as G
+    O.lib().orc_set_threads(16)
+    prompt = _bench_prompt(16)
+    m = O.Model(O.make_config(O.GEMMA_2B, n_ctx=256, wtype=O.Q8_0))
+    seq_ref, lg_ref = m.generate(prompt, 6)
+    m.reset()
+    tok_ref, _, all_ref = m.inference(prompt, 0, want_all=True)
+    m.close()
+    e = G.Engine(O.GEMMA_2B, n_ctx=256, wtype=G.GGML_TYPE_Q8_0)
+    e.tune(4)
+    e.begin(prompt)
+    lg = e.step(len(prompt) + 6, want_logits=True, use_graph=True)
+    assert list(e.tokens()[: len(seq_ref)]) == list(seq_ref)
+    got = lg[len(prompt) - 1:]
+    bad = np.argwhere(got.view(np.uint32) != lg_ref.view(np.uint32))
+    assert bad.size == 0, f"decode: {len(bad)} logits differ, first {bad[:5]}"
+    e.begin(prompt)
+    tok, _, allv = e.prefill(len(prompt), want_all=True)
+    e.close()
+    assert tok == tok_ref
+    assert np.array_equal(allv.view(np.uint32), all_ref.view(np.uint32))
