@@ -1120,7 +1120,9 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         e->kq_xa = e->kq_x + img;
         e->kq_xf = e->kq_x + 2 * img;
         e->kq_xh = e->kq_x + 3 * img;
-        e->kq_cnt_cap = (int)std::max<int64_t>(c.n_ff / 256, 1);
+        // counters: a quantize hand-off takes rows/256 (gate/up: n_ff/256), a norm hand-off rows/256 + 1
+        // (down, attn-out: n_embd/256 + 1 — more than n_ff/256 when n_ff <= n_embd)
+        e->kq_cnt_cap = (int)std::max<int64_t>(std::max<int64_t>(c.n_ff / 256, c.n_embd / 256 + 1), 1);
         GHIP_FATAL(hipMalloc(&e->kq_cnt, (size_t)e->kq_cnt_cap * 128));
         GHIP_FATAL(hipMemset(e->kq_cnt, 0, (size_t)e->kq_cnt_cap * 128));
         GHIP_FATAL(hipMalloc(&e->kq_g, (size_t)c.n_ff * 4));

@@ -20,7 +20,7 @@
 namespace ghip {
 namespace {
 
-template <int WT, int PRO, int EPI, int NR, int R, int DD, int PRE = 0>
+template <int WT, int PRO, int EPI, int NR, int R, int DD, int PRE = 0, bool EW = false>
 __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using G = rr_geom<WT>;
@@ -59,6 +59,15 @@ __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
     for (int r = 0; r < P; ++r) issue(r);
     act_regs<R> ar;
     prefetch_activation<WT, PRO, R, RR_NTH>(a, col, ar);
+    // EW: the ring goes out right behind the activation loads instead of after the image is built —
+    // the activation loads keep the front of the fabric queue (they were issued first), and the
+    // weights' round trip overlaps the image build instead of following it.  Every wave issues
+    // (the carrier's copies of loader 0's tiles are L2 hits, never used), so the build's waits on
+    // the older activation loads stay exact counted waits (no load inside a branch)
+    if (EW) {
+#pragma unroll
+        for (int r = P; r < D; ++r) issue(r);
+    }
     if (!(a.ablate & 1)) {  // timing ablations only
         const norm_state ns = build_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar);
         finish_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar, ns);  // the norm's check
@@ -66,7 +75,7 @@ __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
     if (GHIP_STAMPS && stp && tid == 0) stp[10] = __builtin_amdgcn_s_memrealtime();
     // 1) the rest of the ring (loader w, round r -> block tile w + 8r; D rounds in flight per wave),
     //    issued after the image is used, so these loads may sit in a loader-only branch
-    if (loader) {
+    if (!EW && loader) {
 #pragma unroll
         for (int r = P; r < D; ++r) issue(r);
     }
@@ -136,10 +145,17 @@ int launch_rr_t(const mv_args &a, hipStream_t s) {
     static const int dd_env = getenv("GHIP_RR_D") ? atoi(getenv("GHIP_RR_D")) : 4;
     const int dd = (PRO == PRO_IMG || PRO == PRO_F32) && EPI == EPI_ADD && NR >= 8 && dd_env ? dd_env : 64;
     // (PRE > 0, rounds of weights issued before the image, measured slower: 8.4 / 8.5 vs 7.95 us)
-    const void *fn = dd == 2 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 2>
-                   : dd == 4 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 4>
-                   : dd == 6 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 6>
-                             : (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 64>;
+    // GHIP_RR_EW (round 5): 1 = the ring issued right behind the activation loads (EW), 0 = after
+    // the image is built
+    static const int ew = getenv("GHIP_RR_EW") ? atoi(getenv("GHIP_RR_EW")) : 1;
+    const void *fn = ew ? (dd == 2 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 2, 0, true>
+                           : dd == 4 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 4, 0, true>
+                           : dd == 6 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 6, 0, true>
+                                     : (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 64, 0, true>)
+                        : (dd == 2 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 2>
+                           : dd == 4 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 4>
+                           : dd == 6 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 6>
+                                     : (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 64>);
     if (lds > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     mv_args la = a;
     void *args[] = {(void *)&la};

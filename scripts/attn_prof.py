@@ -11,7 +11,9 @@ from bench import GEMMA_2B, make_prompt  # noqa: E402
 
 e = G.Engine(GEMMA_2B, n_ctx=512, device=0)
 e.begin(make_prompt(128, GEMMA_2B["n_vocab"]))
-e.step(128 + 64, use_graph=True)
+# eager by default: a rocprofv3 kernel trace of graph replays crashed once inside the runtime
+# (the round-4 SIGSEGV); GHIP_PROF_GRAPH=1 profiles the hipGraph replay itself
+e.step(128 + 64, use_graph=os.environ.get("GHIP_PROF_GRAPH", "0") == "1")
 e.L.gemma_engine_sync(e.h)
 print("tokens", list(e.tokens()[128:136]))
 e.close()

@@ -4,7 +4,7 @@ the exact kernel template name, launches per token and the average duration over
 tokens (the decode positions; the prompt's tokens before them are skipped), so every
 `roofline.classes` fraction of the bench line can be recomputed from algorithmic bytes / avg µs.
 
-  python3 scripts/decode_classes.py run_kernel_trace.csv PROMPT STEPS [plan-string] > decode_kernels.md
+  python3 scripts/decode_classes.py {run_results.db | run_kernel_trace.csv} PROMPT STEPS [plan] > decode_kernels.md
 """
 import csv
 import re
@@ -14,12 +14,12 @@ from collections import OrderedDict
 # class: (name pattern, algorithmic bytes per launch: the engine's own count, gemma_engine_time's
 # algo_bytes, as the bench line's roofline.classes carries them — weights + f32 inputs + outputs)
 CLASSES = OrderedDict([
-    ("qkv matvec (+norm)", (r"^void k_matvec_rr<2, [13], 0,", 2975744)),
+    ("qkv matvec (+norm)", (r"^k_matvec_rr<2, [13], 0,", 2975744)),
     ("decode attention", (r"^k_attn_head|^k_attn_decode", None)),
-    ("attn-out matvec (+resid)", (r"^void k_matvec_rr<2, [04], 1, 1,", 2383872)),
-    ("ffn gate/up matvec (+norm, +gelu*mul)", (r"^void k_matvec<2, \d+, 1, 2,", 37830656)),
-    ("ffn down matvec (+resid)", (r"^void k_matvec_rr<2, 4, 1, (?!1,)\d+,|^void k_matvec<2, \d+, 4, 1,", 18909184)),
-    ("logits matvec (+argmax)", (r"^void k_matvec<2, \d+, 1, 3,", 295952384)),
+    ("attn-out matvec (+resid)", (r"^k_matvec_rr<2, [04], 1, 1,", 2383872)),
+    ("ffn gate/up matvec (+norm, +gelu*mul)", (r"^k_matvec<2, \d+, 1, 2,", 37830656)),
+    ("ffn down matvec (+resid)", (r"^k_matvec_rr<2, 4, 1, (?!1,)\d+,|^k_matvec<2, \d+, 4, 1,", 18909184)),
+    ("logits matvec (+argmax)", (r"^k_matvec<2, \d+, 1, 3,", 295952384)),
     ("advance (argmax merge, next token)", (r"^k_advance", None)),
 ])
 
@@ -28,11 +28,18 @@ def main():
     path, prompt, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     plan = sys.argv[4] if len(sys.argv) > 4 else ""
     rows = []
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            if r["Kind"] != "KERNEL_DISPATCH":
-                continue
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    if path.endswith(".db"):  # rocprofv3's default rocpd SQLite output: the `kernels` view
+        import sqlite3
+        rows = [(int(a), int(b), n) for a, b, n in sqlite3.connect(path).execute("select start, end, name from kernels")]
+    else:  # --output-format csv: *_kernel_trace.csv
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                if r["Kind"] != "KERNEL_DISPATCH":
+                    continue
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    # one naming for both outputs: "k_matvec<...>(ghip::mv_args)" (no "void ", no namespaces)
+    rows = [(a, b, n.replace("void ", "", 1).replace("ghip::(anonymous namespace)::", "").replace("ghip::", ""))
+            for a, b, n in rows]
     rows.sort()
     # one k_advance closes every token: the last `steps` tokens are the dispatches after the
     # (steps+1)-th last k_advance

@@ -1,16 +1,15 @@
 #!/bin/bash
-# env-variable A/B (default: HIP runtime launch-path settings) on the decode bench (Q4_0 engine + ggml-API leg).
-# usage (GPU box, repo root): [VARIANTS="name:VAR=val ..."] [Q8STEPS=n] bash scripts/env_ab.sh [tag]
+# A/B of an environment switch on one box, interleaved: ENVA / ENVB (e.g. "GHIP_RR_EW=0" / "GHIP_RR_EW=1"),
+# decode bench legs (no CPU, prefill, TP, Q8_0, ggml legs unless BENCH_ARGS adds them), REPS rounds
 set -o pipefail
-TAG=${1:-envab}; OUT=gpurun_out/$TAG; mkdir -p $OUT
-export TMPDIR=/tmp
-run() {  # name, env assignments...
-  local name=$1; shift
-  env "$@" timeout -k 10 240 python bench.py --no-cpu --prefill 0 --tp-steps 0 --q8-steps ${Q8STEPS:-0} --ggml-steps ${GGSTEPS:-48} \
-      > $OUT/$name.json 2> $OUT/$name.err || { tail -20 $OUT/$name.err; return 1; }
-  python3 -c "import json,sys; d=json.load(open('$OUT/$name.json')); print('$name', d['value'], d['ms_per_step'], d.get('ggml_path_decode_tok_s'), (d.get('q4_k_m_decode') or {}).get('tok_s'))"
-}
-VARIANTS=${VARIANTS:-"base:A=0 devkarg:HIP_FORCE_DEV_KERNARG=1 nocapt:DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 capt:DEBUG_CLR_GRAPH_PACKET_CAPTURE=1"}
-for rep in 1 2; do
-  for v in $VARIANTS; do run ${v%%:*}$rep ${v#*:} || exit 1; done
+O=gpurun_out/${OUT:-envab}
+mkdir -p $O
+for rep in $(seq 1 ${REPS:-3}); do
+  for v in A B; do
+    if [ $v = A ]; then E="$ENVA"; else E="$ENVB"; fi
+    env $E timeout -k 10 240 python bench.py --no-cpu --prefill 0 --tp-steps 0 --q8-steps 0 --ggml-steps 0 ${BENCH_ARGS} > $O/$v$rep.json 2> $O/$v$rep.err || { tail -20 $O/$v$rep.err; exit 1; }
+    python3 -c "
+import json; d=json.load(open('$O/$v$rep.json')); c=d['roofline']['classes']
+print('$v [$E]', d['value'], d['ms_per_step'], (d.get('q4_k_m_decode') or {}).get('tok_s'), ' '.join('%s=%.2f' % (k.split()[0], v['avg_us']) for k, v in c.items()))"
+  done
 done

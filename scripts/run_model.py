@@ -14,11 +14,11 @@ e = G.Engine(SHAPES[name], n_ctx=256, device=0, tp=(tpv, 0, None) if tpv > 1 els
 if os.environ.get("PLAN"):  # e.g. PLAN=1,1,0,4,1,0,1,1,0,8,2,0,1,16,0 (qkv, o, gate/up, down, logits: ks,rpw,img)
     v = [int(t) for t in os.environ["PLAN"].split(",")]
     e.set_plan({k: (v[3 * i], v[3 * i + 1], v[3 * i + 2]) for i, k in enumerate(e.PLAN_CLASSES)})
-elif os.environ.get("TUNE", "1") == "1":  # (tuning under rocprofv3 crashes the profiler: pass PLAN)
+elif os.environ.get("TUNE", "1") == "1":  # tuning replays ~20 captured graphs: under rocprofv3 pass PLAN
     print("plan", e.tune(6))
 print("plan", e.plan())
 e.begin([2, 100, 200, 300])
-e.step(4 + steps, use_graph=True)
+e.step(4 + steps, use_graph=os.environ.get("GHIP_PROF_GRAPH", "0") == "1")  # eager under the profiler
 e.L.gemma_engine_sync(e.h)
 print("tokens", list(e.tokens()[:12]))
 e.close()
