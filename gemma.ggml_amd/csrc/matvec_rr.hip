@@ -68,10 +68,8 @@ __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
 #pragma unroll
         for (int r = P; r < D; ++r) issue(r);
     }
-    if (!(a.ablate & 1)) {  // timing ablations only
-        const norm_state ns = build_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar);
-        finish_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar, ns);  // the norm's check
-    }
+    norm_state ns;
+    if (!(a.ablate & 1)) ns = build_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar);  // timing ablations only
     if (GHIP_STAMPS && stp && tid == 0) stp[10] = __builtin_amdgcn_s_memrealtime();
     // 1) the rest of the ring (loader w, round r -> block tile w + 8r; D rounds in flight per wave),
     //    issued after the image is used, so these loads may sit in a loader-only branch
@@ -79,6 +77,10 @@ __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
 #pragma unroll
         for (int r = P; r < D; ++r) issue(r);
     }
+    // the norm's check (PRO_NORM / PRO_EMBED) with the weights already in flight: off the path to
+    // the first weight load (measured: +0.35-0.45 us on qkv with the check in front of the issue);
+    // the fallback reloads x and w, so only the ring's D rounds stay live beside it
+    if (!(a.ablate & 1)) finish_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar, ns);
     if (GHIP_STAMPS && stp && tid == 0) stp[11] = __builtin_amdgcn_s_memrealtime();
     lds_barrier();
     if (GHIP_STAMPS && stp && tid == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
@@ -147,7 +149,10 @@ int launch_rr_t(const mv_args &a, hipStream_t s) {
     // (PRE > 0, rounds of weights issued before the image, measured slower: 8.4 / 8.5 vs 7.95 us)
     // GHIP_RR_EW (round 5): 1 = the ring issued right behind the activation loads (EW), 0 = after
     // the image is built
-    static const int ew = getenv("GHIP_RR_EW") ? atoi(getenv("GHIP_RR_EW")) : 1;
+    // (measured: EW 1,449-1,456 vs 1,513-1,517 tok/s — down 8.2 -> 9.2-10.2 us, attn-out 3.57 -> 3.34-3.53:
+    // off by default; GHIP_RR_EW=2 takes it for the one-round EPI_ADD shape (attn-out) only)
+    static const int ew_env = getenv("GHIP_RR_EW") ? atoi(getenv("GHIP_RR_EW")) : 0;
+    const bool ew = ew_env == 1 || (ew_env == 2 && NR == 1 && EPI == EPI_ADD);
     const void *fn = ew ? (dd == 2 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 2, 0, true>
                            : dd == 4 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 4, 0, true>
                            : dd == 6 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 6, 0, true>
