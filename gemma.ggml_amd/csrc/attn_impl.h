@@ -201,6 +201,9 @@ constexpr int AH_THREADS = 1024;  // per-head form: 256 quads = 256 KQ positions
 constexpr int AH_KPF = GHIP_AH_KPF;  // K steps (of 32 elements) prefetched per lane: hd <= 256
 constexpr int AH_VPF = GHIP_AH_VPF;  // V steps (of 32 positions) prefetched per lane: n_kv <= 256
 
+#ifndef GHIP_AH_TRIM
+#define GHIP_AH_TRIM 0  // 1: no dead V load instructions (wave-uniform skips) — measured 0.3 % slower
+#endif
 #ifndef GHIP_AH_ABL
 #define GHIP_AH_ABL 0  // timing ablations only (wrong results): 1 every K load reads row 0, 2 no KQ dots,
                        // 4 no KQ phase at all, 8 no KQV dots, 16 KQ dots over 4 of 8 steps
@@ -248,6 +251,9 @@ __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, a
         for (int s = 0; s < KPF; ++s) p.k[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
     }
     if (a.v_lds) return;  // the V rows come by LDS-DMA (attn_vdma)
+    // only the waves whose quads own output dims load V (wave-uniform: quad & ~15 = 16 * wave);
+    // the others' loads were dead, and each costs the CU's load path its cycles
+    if (GHIP_AH_TRIM && d_lo + (quad & ~15) >= (hd < d_hi ? hd : d_hi)) return;
     const int d0 = d_lo + quad < (hd < d_hi ? hd : d_hi) ? d_lo + quad : d_lo;
     const uint16_t *vrow0 = a.vc + ((int64_t)kvh * hd + d0) * a.ctx;
 #pragma unroll
@@ -366,6 +372,10 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     uint4 qr[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) qr[s] = *(const uint4 *)(q16 + (s * 32 < hd ? s * 32 : 0) + t4 * 8);
+    if (GHIP_STAMPS == 4) {  // KQ sub-stamps (stamps build 4): q in registers
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        AH_STAMP(5);
+    }
     for (int j0 = 0; j0 < n_kv; j0 += NTH / 4) {
         const int j = j0 + quad;
         // a wave whose 16 positions all lie past n_kv has nothing to store: skip its dots (wave-
@@ -395,6 +405,10 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
                 for (int s = 0; s < 8; ++s)
                     if (s * 32 < hd) kx[s] = *(const uint4 *)(k16 + s * 32 + t4 * 8);
             }
+            if (GHIP_STAMPS == 4 && j0 + wave * 16 == 0) {  // the first K steps have landed
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                AH_STAMP(6);
+            }
             if (GHIP_AH_ABL & 2) {
 #pragma unroll
                 for (int s = 0; s < 8; ++s) acc[s] = __builtin_bit_cast(float, kx[s].x ^ qr[s].y);
@@ -414,6 +428,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
                 if (s * 32 < hd) f16_step8(acc, *(const uint4 *)(krow + s * 32 + t4 * 8), qr[s]);
         }
         const float kq = quad_reduce_f16(acc);
+        if (GHIP_STAMPS == 4 && j0 == 0) AH_STAMP(7);  // dots folded (wave 0)
         if (t4 == 0 && j < n_kv) {
             const float w = (j > pos) ? -INFINITY : kq * 1.0f + 0.0f;
             S[j] = w;
@@ -499,11 +514,14 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
                 for (int s = 0; s < 8; ++s) {
                     const int e0 = s * 32 + t4 * 8;
                     if (s < VPF && first) xs8[s] = vpre[s < VPF ? s : 0];
-                    else xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
+                    else if (!GHIP_AH_TRIM || s * 32 < n_kv) xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
+                    else xs8[s] = make_uint4(0, 0, 0, 0);  // past n_kv: never used (no load issued)
                 }
             }
 #pragma unroll
-            for (int s = 0; s < 8; ++s) pr8[s] = *(const uint4 *)(P16 + (s * 32 < n_kv ? s * 32 : 0) + t4 * 8);
+            for (int s = 0; s < 8; ++s)
+                pr8[s] = (!GHIP_AH_TRIM || s * 32 < n_kv) ? *(const uint4 *)(P16 + (s * 32 < n_kv ? s * 32 : 0) + t4 * 8)
+                                                          : make_uint4(0, 0, 0, 0);
             if (GHIP_STAMPS == 2 && d == d_lo + quad) {  // operands in registers (stamps build 2)
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                 AH_STAMP(5);

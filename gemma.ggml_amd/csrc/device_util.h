@@ -90,27 +90,28 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 
 // ---- ggml's rms_norm mean, provably --------------------------------------------------
 // ggml: sum = Σ_i (double)(x_i*x_i) in index order, rounded after every add; mean = (float)(sum/n).
-// The kernels add the same double terms in a tree T and form mean = (float)(T/n).  All terms are
-// ≥ 0, so ANY summation order of them lies within γ_{n−1}·E of the exact sum E (γ_k = k·u/(1 − k·u),
-// u = 2^−53; Higham, Accuracy and Stability of Numerical Algorithms, §4.2): |S − T| ≤ 2·γ_{n−1}·E
-// ≤ 2(n−1)·u·T·(1 + O(n·u)) ≤ m = n·2^−51·T (= 4·n·u·T).  mean's float rounding interval is bounded
-// by the midpoints mid_lo / mid_hi to its neighbours (exact in double).  rms_mean_certain checks
-//   T·(1 − r) > mid_lo·n  and  T·(1 + r) < mid_hi·n,   r = n·2^−51 + 2^−48,
-// with multiplications only (no division on the prologue's critical path): r covers m plus the
-// rounding of these four products and keeps S/n more than a double ulp inside the interval, so
-// fl64(S/n) rounds to the same float — the tree's mean IS ggml's.  When the check fails (S and T may
-// sit on two sides of a rounding boundary: ≈ 2·r·2^23 ≈ 2^−15 of the norms at n = 2048, or a
-// zero / subnormal / largest-float mean) the caller runs ggml's sequential sum, seq_sumsq_wave.
-// 0, inf and NaN sums are the same in every order.
-__device__ __forceinline__ bool rms_mean_certain(double T, int64_t n, float mean) {
-    const uint32_t mb = __builtin_bit_cast(uint32_t, mean);
-    const bool special = !(T > 0.0) | !(T < __builtin_inf());               // 0, inf, NaN: certain
-    const bool edge = (mb < 0x00800000u) | (mb >= 0x7F7FFFFFu);             // zero / subnormal / FLT_MAX
-    const double a = (double)mean, lo = (double)__builtin_bit_cast(float, mb - 1),
-                 hi = (double)__builtin_bit_cast(float, mb + 1);
-    const double dn = (double)n, r = dn * 0x1p-51 + 0x1p-48;
-    // both sides evaluated (no short-circuit branch): straight-line code the scheduler can overlap
-    return special | (!edge & (T * (1.0 - r) > (a + lo) * 0.5 * dn) & (T * (1.0 + r) < (a + hi) * 0.5 * dn));
+// The kernels add the same double terms in a tree T and form q = fl64(T/n), mean = (float)q.  All
+// terms are ≥ 0, so ANY summation order of them lies within γ_{n−1}·E of the exact sum E (γ_k =
+// k·u/(1 − k·u), u = 2^−53; Higham, Accuracy and Stability of Numerical Algorithms, §4.2):
+// |S − T| ≤ 2·γ_{n−1}·E ≤ n·2^−52·T·(1 + O(n·u)), so fl64(S/n) lies in q·[1 − ρ, 1 + ρ] with
+// ρ = n·2^−51 + 2^−48 (twice that bound plus both divisions' roundings).  Float rounding of a double
+// q in the float normal range is decided by the 29 low mantissa bits it drops: the rounding
+// boundary (the midpoint to the next float) is where they equal 2^28, and ρ·q is under ρ·2^53 =
+// 4n + 32 units of q's last place.  rms_mean_certain checks |low29(q) − 2^28| > 4n + 40: no
+// boundary inside q·[1 ± ρ], so S/n and T/n round to the same float — the tree's mean IS ggml's.
+// Integer ops on q's bits only (no division, no double compares on the prologue's critical path).
+// When it fails (≈ 2·(4n+40)/2^29 ≈ 2^−15 of the norms at n = 2048, or a mean outside the float
+// normal range) the caller runs ggml's sequential sum, seq_sumsq_wave.  The binade edge needs no
+// case: the float 2^k there is representable and the nearest boundary below it is 2^27 units of q
+// away (n ≤ 2^22 keeps 4n + 40 < 2^27).  0, inf and NaN sums are the same in every order.
+__device__ __forceinline__ bool rms_mean_certain(double q, int64_t n) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, q);
+    const uint32_t ex = (uint32_t)(b >> 52) & 0x7FFu;                       // q ≥ 0: no sign bit
+    const uint32_t low = (uint32_t)b & 0x1FFFFFFFu;                         // the bits a float drops
+    const uint32_t dist = low >= 0x10000000u ? low - 0x10000000u : 0x10000000u - low;
+    const bool special = (b == 0) | (ex == 0x7FFu);                         // 0, inf, NaN: certain
+    const bool normal = (ex >= 1023u - 126u) & (ex <= 1023u + 127u) & (n <= ((int64_t)1 << 22));
+    return special | (normal & (dist > (uint32_t)(4 * n + 40)));
 }
 
 // ggml's sequential sum Σ (double)(x_i*x_i), i = 0 … n−1 in order, by ONE wave (all 64 lanes

@@ -245,11 +245,11 @@ __device__ __forceinline__ void kq_pro_load(const kq_args &a, int col, int wave,
     }
 }
 
-// 1/sqrtf(mean + eps) of the column's rms_norm from the prologue's tree sum T (*mean = the tree's
-// mean; the caller checks it with rms_mean_certain after the image is built)
-__device__ __forceinline__ float kq_norm_scale(const kq_args &a, double T, float *mean) {
-    *mean = (float)(T / (double)((int64_t)a.nsb * 256));
-    return 1.0f / sqrtf(*mean + a.eps);
+// 1/sqrtf(mean + eps) of the column's rms_norm from the prologue's tree sum T (*q = T/n; the caller
+// checks it with rms_mean_certain after the image is built)
+__device__ __forceinline__ float kq_norm_scale(const kq_args &a, double T, double *q) {
+    *q = T / (double)((int64_t)a.nsb * 256);
+    return 1.0f / sqrtf((float)*q + a.eps);
 }
 // the same from ggml's sequential sum (every wave runs it itself: the rare slow path)
 __device__ __forceinline__ float kq_seq_scale(const kq_args &a, int col) {
@@ -270,8 +270,8 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
         return;
     }
     const int nw = nth >> 6, lane = tid & 63, wave = tid >> 6;
-    float scale = 1.0f, mean = 0.0f;
-    double tsum = 0.0;
+    float scale = 1.0f;
+    double q = 0.0;  // the tree's T/n (rms_mean_certain)
     // this wave holds super-blocks wave and wave + nw: the tree's first level (h = nw*64) pairs
     // exactly them, so it runs in registers, and their two quantizations interleave
     const bool two = XJ == 2 && a.nsb == 2 * nw;
@@ -317,8 +317,7 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
                 m = h;
             }
             v = __shfl(v, 0);
-            tsum = v;
-            scale = kq_norm_scale(a, v, &mean);
+            scale = kq_norm_scale(a, v, &q);
             n = 0;  // done
         } else if (two) {
             red[wave * 64 + lane] = part[0] + part[XJ - 1];
@@ -347,8 +346,7 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
             if (lane == 0) red[0] = v;
         }
         __syncthreads();
-        tsum = red[0];
-        scale = kq_norm_scale(a, tsum, &mean);
+        scale = kq_norm_scale(a, red[0], &q);
         }
     }
     auto emit = [&](float sc) {
@@ -376,7 +374,7 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
     emit(scale);
     // checked after the image is built (off the critical path); rare, workgroup-uniform: ggml's own
     // order, image rebuilt
-    if (a.pro == KQP_NORM && !rms_mean_certain(tsum, (int64_t)a.nsb * 256, mean)) emit(kq_seq_scale(a, col));
+    if (a.pro == KQP_NORM && !rms_mean_certain(q, (int64_t)a.nsb * 256)) emit(kq_seq_scale(a, col));
 }
 
 __device__ __forceinline__ double *kq_red(uint8_t *xs, int nsb) {
@@ -498,8 +496,9 @@ __device__ __forceinline__ void kq_handoff(const kq_args &a, int col, int64_t g,
         part[k] = p;
     }
     const double sum = kq_tree(part, nsb_y, lane, (double *)lds);
-    float mean = (float)(sum / (double)a.rows);
-    if (!rms_mean_certain(sum, a.rows, mean))  // rare: ggml's own order, from the same sc1 loads
+    const double q = sum / (double)a.rows;
+    float mean = (float)q;
+    if (!rms_mean_certain(q, a.rows))  // rare: ggml's own order, from the same sc1 loads
         mean = (float)(seq_sumsq_wave(a.rows, [&](int64_t i0, float v[8]) {
                            const float4 u = kq_ld4_sc1(y + i0, a.q8_abl & 8), w = kq_ld4_sc1(y + i0 + 4, a.q8_abl & 8);
                            v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
@@ -955,8 +954,9 @@ __global__ void __launch_bounds__(1024) k_norm_q8K(const float *x, int64_t ldx, 
         __syncthreads();
         n = h;
     }
-    float mean = (float)(red[0] / (double)E);
-    if (!rms_mean_certain(red[0], E, mean)) {  // workgroup-uniform; rare: ggml's own order
+    const double q = red[0] / (double)E;
+    float mean = (float)q;
+    if (!rms_mean_certain(q, E)) {  // workgroup-uniform; rare: ggml's own order
         const float *xr = x + (int64_t)r * ldx;
         mean = (float)(seq_sumsq_wave(E, [&](int64_t i0, float v[8]) {
                            const float4 u = *(const float4 *)(xr + i0), w4 = *(const float4 *)(xr + i0 + 4);

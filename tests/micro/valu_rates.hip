@@ -21,7 +21,10 @@ __global__ void k(uint32_t *out, unsigned long long *cyc, int iters, uint32_t se
     if (OP == 3) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(r[i]) : "v"(a));                          \
     if (OP == 4) asm volatile("v_dot4c_i32_i8 %0, %1, %2" : "+v"(r[i]) : "v"(a), "v"(b));             \
     if (OP == 5) asm volatile("v_add_f32 %0, %1, %0" : "+v"(r[i]) : "v"(a));                          \
-    if (OP == 6) asm volatile("v_sub_u32 %0, %1, %0" : "+v"(r[i]) : "v"(a));
+    if (OP == 6) asm volatile("v_sub_u32 %0, %1, %0" : "+v"(r[i]) : "v"(a));                          \
+    if (OP == 7) asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,1,0]" : "+v"(r[i]) : "v"(a), "v"(b)); \
+    if (OP == 8) asm volatile("v_cvt_f32_f16 %0, %1" : "=v"(r[i]) : "v"(r[i]));                       \
+    if (OP == 9) asm volatile("v_dot2_f32_f16 %0, %1, %2, %0" : "+v"(r[i]) : "v"(a), "v"(b));
         REP16(OPX)
     }
     unsigned long long t1 = __builtin_readcyclecounter();
@@ -85,6 +88,9 @@ int main() {
         run("mul_f32", k<3>, 16, w);
         run("add_f32", k<5>, 16, w);
         run("sub_u32", k<6>, 16, w);
+        run("fma_mix_f32", k<7>, 16, w);
+        run("cvt_f32_f16", k<8>, 16, w);
+        run("dot2_f32_f16", k<9>, 16, w);
         run("pk_fma_f32", kpk<0>, 8, w);
         run("pk_mul_f32", kpk<1>, 8, w);
         run("pk_add_f32", kpk<2>, 8, w);
