@@ -204,6 +204,18 @@ constexpr int AH_VPF = GHIP_AH_VPF;  // V steps (of 32 positions) prefetched per
 #ifndef GHIP_AH_TRIM
 #define GHIP_AH_TRIM 0  // 1: no dead V load instructions (wave-uniform skips) — measured 0.3 % slower
 #endif
+#ifndef GHIP_AH_SPOS
+#define GHIP_AH_SPOS 1  // the position by a scalar load, the wave index uniform (readfirstlane)
+#endif
+#ifndef GHIP_AH_RW
+#define GHIP_AH_RW 0  // 1: the last wave does the RoPE, its prefetch after it (measured ~1 % slower)
+#endif
+#ifndef GHIP_AH_VEARLY
+#define GHIP_AH_VEARLY 0  // 1 (with VPF 0): V loads after the K dots (spills at 1024 threads: slower)
+#endif
+#ifndef GHIP_AH_KTRIM
+#define GHIP_AH_KTRIM 0
+#endif
 #ifndef GHIP_AH_ABL
 #define GHIP_AH_ABL 0  // timing ablations only (wrong results): 1 every K load reads row 0, 2 no KQ dots,
                        // 4 no KQ phase at all, 8 no KQV dots, 16 KQ dots over 4 of 8 steps
@@ -243,8 +255,22 @@ __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, a
                                               int d_hi = 1 << 30, int tid_in = -1) {
     const int hd = a.hd, tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, t4 = tid & 3, quad = tid >> 2;
     const int G = a.H / a.Hkv, kvh = h / G, kvw = a.Hkv * hd;
-    p.pos_v = ((const int *)a.rope_cur)[hd];  // published with the row (k_advance / begin)
-    {
+    // published with the row (k_advance / begin); a scalar load (constant address space): its own
+    // counter, so reading pos waits for no vector load
+#if GHIP_AH_SPOS
+    p.pos_v = *((const __attribute__((address_space(4))) int *)a.rope_cur + hd);
+#else
+    p.pos_v = ((const int *)a.rope_cur)[hd];
+#endif
+    // GHIP_AH_KTRIM: the position by a scalar load first (its own counter: the RoPE loads already
+    // in flight are not waited for), then K rows only for the waves whose positions lie below n_kv
+    bool kload = true;
+    if (GHIP_AH_KTRIM) {
+        const int ps = *((const __attribute__((address_space(4))) int *)a.rope_cur + hd);
+        const int nk = 32 * (ps / 32 + 1);
+        kload = (quad & ~15) < (nk < a.ctx ? nk : a.ctx);
+    }
+    if (kload) {
         const int j = (GHIP_AH_ABL & 1) ? 0 : quad < a.ctx ? quad : 0;  // no dependency on pos: rows >= pos are masked
         const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
 #pragma unroll
@@ -289,7 +315,8 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     // this function's per-lane addresses live across its other phases
     const int hd = a.hd, half = hd / 2, tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, t4 = tid & 3, quad = tid >> 2;
     const int dsz = hd / (a.dsplit > 1 ? a.dsplit : 1), d_lo = sp * dsz, d_hi = d_lo + dsz;
-    const int lane = tid & 63, wave = tid >> 6, nwave = NTH / 64;
+    // wave: uniform for the compiler too (readfirstlane), so branches on it are scalar branches
+    const int lane = tid & 63, wave = GHIP_AH_SPOS ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6, nwave = NTH / 64;
     const int G = a.H / a.Hkv, kvh = h / G;
     AH_STAMP(0);
     AH_CLK0();
@@ -299,27 +326,28 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     const float *vh = a.qkv + (int64_t)a.H * hd + kvw + (int64_t)kvh * hd;
     const float *cs = a.rope_cur, *sn = a.rope_cur + half;
     // ---- early loads (issue order = wait order): RoPE inputs + pos, then K rows, then V rows
-    // RoPE inputs: only the waves holding a pair load them (every load instruction costs the CU's
-    // load path ~16 clk whatever its addresses; a wave-uniform branch skips the others)
-    const int n4 = half / 4, i4 = (tid < n4 ? tid : 0) * 4;
+    // RoPE inputs: only the RoPE wave loads them (every load instruction costs the CU's load path
+    // ~16 clk whatever its addresses; a wave-uniform branch skips the others).  GHIP_AH_RW: the
+    // RoPE wave is the LAST wave and it issues its own K / V prefetch only after the RoPE: the
+    // RoPE's wait for its inputs sits after a branch, where the compiler can only drain every load
+    // (s_waitcnt vmcnt(0)), so a RoPE wave that had issued its prefetch first waited for all of it
+    // before the workgroup barrier (stamps build 4: RoPE done 1.2-1.5 µs, the prefetch's landing)
+    constexpr int RW = GHIP_AH_RW ? NTH / 64 - 1 : 0;  // the RoPE wave (hd <= 512: 64 lanes suffice)
+    const int rl = tid - RW * 64;
+    const int n4 = half / 4, i4 = (rl >= 0 && rl < n4 ? rl : 0) * 4;
     float4 qa{}, qb{}, ka{}, kb{}, ca{}, sa{};
-    if (wave * 64 < n4) {
+    if (GHIP_AH_RW ? wave == RW : wave * 64 < n4) {
         qa = ld4<SC1>(qh + i4); qb = ld4<SC1>(qh + i4 + half);
         ka = ld4<SC1>(kh + i4); kb = ld4<SC1>(kh + i4 + half);
         ca = *(const float4 *)(cs + i4); sa = *(const float4 *)(sn + i4);
     }
     attn_pre<KPF, VPF> own;
-    if (!PRE) attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi, tid);
+    if (!PRE && (!GHIP_AH_RW || wave != RW)) attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi, tid);
     if (a.v_lds) attn_vdma(a, kvh, d_lo, dsz, smem, wave, nwave, lane);
     const attn_pre<KPF, VPF> &P = PRE ? *pre : own;
-    const int pos_v = P.pos_v;
     const uint4 *kpre = P.k, *vpre = P.v;
     const int d0 = d_lo + quad < d_hi ? d_lo + quad : d_lo;
     const float vx0 = ld1<SC1>(vh + d0);
-    const int pos = __builtin_amdgcn_readfirstlane(pos_v);
-    const int n_total = pos + 1;
-    int n_kv = 32 * (n_total / 32 + 1);  // src/gemma_model.cpp:429
-    if (n_kv > a.ctx) n_kv = a.ctx;
 
     uint16_t *q16 = (uint16_t *)smem;  // hd
     uint16_t *k16 = q16 + hd;          // hd (this token's k, post-rope)
@@ -348,14 +376,22 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         *(uint2 *)lo = make_uint2(l2[0], l2[1]);
         *(uint2 *)hi = make_uint2(h2[0], h2[1]);
     };
-    if (tid < n4) {
+    if (rl >= 0 && rl < n4) {
         rope4(qa, qb, a.q_scale, true, q16 + i4, q16 + i4 + half);
         rope4(ka, kb, 1.0f, false, k16 + i4, k16 + i4 + half);
     }
-    if (tid == 0) {
+    if (rl == 0) {  // (the RoPE wave: its loads are drained here; another wave could wait on them)
         *mx_key = 0u;  // below the key of every float, -inf included
         *e_sum = 0ull;
     }
+    if (GHIP_AH_RW && !PRE && wave == RW) {
+        asm volatile("" ::: "memory");  // (issued after the RoPE, not hoisted above it)
+        attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi, tid);
+    }
+    const int pos = __builtin_amdgcn_readfirstlane(P.pos_v);
+    const int n_total = pos + 1;
+    int n_kv = 32 * (n_total / 32 + 1);  // src/gemma_model.cpp:429
+    if (n_kv > a.ctx) n_kv = a.ctx;
     attn_barrier();  // LDS only: the K / V prefetch stays in flight
     AH_STAMP(1);
     // this token's cache entries (src/gemma_model.cpp:506-517), by the group's first head; readers
@@ -437,6 +473,16 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         }
     }
     // the row max, partial per wave (DPP) then one LDS max per wave, in the same barrier as S
+    // GHIP_AH_VEARLY: the V rows of this quad's first KQV dim issued here, after the K dots (their
+    // registers are free again), so they land during the softmax; only the waves owning dims load
+    // (a scalar branch on the uniform wave index), only steps below n_kv
+    uint4 ve[8];
+    const bool vearly = GHIP_AH_VEARLY && VPF == 0 && !a.v_lds && n_kv <= 256 && d_lo + wave * 16 < d_hi;
+    if (vearly) {
+        const uint16_t *vr0 = a.vc + ((int64_t)kvh * hd + d0) * a.ctx + t4 * 8;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) ve[s] = s * 32 < n_kv ? *(const uint4 *)(vr0 + s * 32) : make_uint4(0, 0, 0, 0);
+    }
     lmax = wave_max(lmax);
     if (lane == 0) {
         const uint32_t b = __builtin_bit_cast(uint32_t, lmax);
@@ -513,7 +559,8 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
 #pragma unroll
                 for (int s = 0; s < 8; ++s) {
                     const int e0 = s * 32 + t4 * 8;
-                    if (s < VPF && first) xs8[s] = vpre[s < VPF ? s : 0];
+                    if (vearly && first) xs8[s] = ve[s];
+                    else if (s < VPF && first) xs8[s] = vpre[s < VPF ? s : 0];
                     else if (!GHIP_AH_TRIM || s * 32 < n_kv) xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
                     else xs8[s] = make_uint4(0, 0, 0, 0);  // past n_kv: never used (no load issued)
                 }

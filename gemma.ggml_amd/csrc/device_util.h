@@ -127,6 +127,9 @@ __device__ __forceinline__ double seq_sumsq_wave(int64_t n, Load8 load8) {
         float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         const int64_t i = base + (int64_t)lane * 8;
         if (i < n) load8(i, v);
+        // not unrolled: the rare path's code stays small (unrolled it added ~6 KB to every kernel
+        // holding a norm prologue, and the instruction fetch of the hot path paid for it)
+#pragma unroll 1
         for (int L = 0; L < 64; ++L) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {

@@ -1681,13 +1681,20 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
         if (gemma_engine_step(e, 1, nullptr, 1)) return -1.0;  // eager step + capture
         for (int i = 0; i < 2; ++i)
             if (hipGraphLaunch(e->graph_exec, e->stream) != hipSuccess) return -1.0;
-        if (hipEventRecord(t0, e->stream) != hipSuccess) return -1.0;
-        for (int i = 0; i < iters; ++i)
-            if (hipGraphLaunch(e->graph_exec, e->stream) != hipSuccess) return -1.0;
-        if (hipEventRecord(t1, e->stream) != hipSuccess || hipEventSynchronize(t1) != hipSuccess) return -1.0;
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, t0, t1);
-        return (double)ms * 1000.0 / iters;
+        // the minimum of three timed runs: one run's box noise (±1 %) exceeded the differences
+        // between neighbouring plans, so single samples picked plans by luck (round 5: the bench's
+        // logits plan varied run to run between 1, 2 and 8 row tiles per workgroup, ±2 µs)
+        double tmin = 1e30;
+        for (int rep = 0; rep < 3; ++rep) {
+            if (hipEventRecord(t0, e->stream) != hipSuccess) return -1.0;
+            for (int i = 0; i < iters; ++i)
+                if (hipGraphLaunch(e->graph_exec, e->stream) != hipSuccess) return -1.0;
+            if (hipEventRecord(t1, e->stream) != hipSuccess || hipEventSynchronize(t1) != hipSuccess) return -1.0;
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, t0, t1);
+            tmin = std::min(tmin, (double)ms * 1000.0 / iters);
+        }
+        return tmin;
     };
     const layer_dev &L0 = e->layers[0];
     const int64_t nbt[MC_N] = {L0.qkv.n_bt, L0.o.n_bt, L0.gate.n_bt, L0.down.n_bt, e->embd.n_bt};
@@ -1709,6 +1716,14 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
         if (splits && cls != MC_GU && pick_ks(wt, nbt[cls], KS_RR) == KS_RR) cands.push_back({KS_RR, 1, e->plan[cls].img});
         const launch_plan keep = e->plan[cls];
         launch_plan win = keep;
+        {  // the incumbent re-measured beside its challengers (not a sample from an earlier class)
+            const double t = trial();
+            if (t < 0) {
+                rc = -1;
+                break;
+            }
+            best = t;
+        }
         for (const launch_plan &p : cands) {
             if (p.ks == keep.ks && p.rpw == keep.rpw && p.img == keep.img) continue;
             e->plan[cls] = p;

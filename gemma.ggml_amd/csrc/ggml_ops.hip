@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(256) k_g_rms_norm(gt_desc a, gt_desc dst, floa
     }
     const double q = red[0] / (double)n;
     float mean = (float)q;
-    if (!rms_mean_certain(q, n))  // workgroup-uniform; rare: ggml's own order
+    if (__builtin_expect(!rms_mean_certain(q, n), 0))  // workgroup-uniform; rare: ggml's own order
         mean = (float)(seq_sumsq_wave(n, [&](int64_t i0, float v[8]) {
                            for (int j = 0; j < 8; ++j)
                                v[j] = i0 + j < n ? *(const float *)(src + (i0 + j) * a.nb[0]) : 0.0f;

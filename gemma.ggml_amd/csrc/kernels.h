@@ -283,6 +283,9 @@ struct attn_args {
     // per-head mode (k_attn_head): byte offset in LDS of the workgroup's V rows, copied there by
     // LDS-DMA at the start (positions < min(ctx, 256), row pitch ATT_VDMA_PITCH); 0 = no copy
     uint32_t v_lds = 0;
+    // per-head mode: 1 = head h's workgroups on XCD h % 8 (blocks b -> h = b % H, split b / H), so
+    // the heads' K / V reads spread over the XCDs' L2s; 0 = every workgroup of a kv head on one XCD
+    int spread = 0;
     int H, Hkv, hd, ctx;
     float q_scale;
     float *dbg_w = nullptr;      // optional debug taps: [H][ctx] scores, [H][ctx] fp16 P, [H] inv

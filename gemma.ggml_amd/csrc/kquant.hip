@@ -349,16 +349,16 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
         scale = kq_norm_scale(a, red[0], &q);
         }
     }
-    auto emit = [&](float sc) {
+    auto emit = [&](const kq_pro_regs<XJ> &rv, float sc) {
         float y[XJ][4];
 #pragma unroll
         for (int j = 0; j < XJ; ++j) {
-            y[j][0] = r.x[j].x; y[j][1] = r.x[j].y; y[j][2] = r.x[j].z; y[j][3] = r.x[j].w;
+            y[j][0] = rv.x[j].x; y[j][1] = rv.x[j].y; y[j][2] = rv.x[j].z; y[j][3] = rv.x[j].w;
             if (a.pro == KQP_NORM) {
-                y[j][0] = pin(y[j][0] * sc) * r.w[j].x;
-                y[j][1] = pin(y[j][1] * sc) * r.w[j].y;
-                y[j][2] = pin(y[j][2] * sc) * r.w[j].z;
-                y[j][3] = pin(y[j][3] * sc) * r.w[j].w;
+                y[j][0] = pin(y[j][0] * sc) * rv.w[j].x;
+                y[j][1] = pin(y[j][1] * sc) * rv.w[j].y;
+                y[j][2] = pin(y[j][2] * sc) * rv.w[j].z;
+                y[j][3] = pin(y[j][3] * sc) * rv.w[j].w;
             }
         }
         if (two) {
@@ -371,10 +371,13 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
             if (sb < a.nsb) q8K_store(y[j], lane, xs + (int64_t)sb * 292);  // wave-uniform
         }
     };
-    emit(scale);
-    // checked after the image is built (off the critical path); rare, workgroup-uniform: ggml's own
-    // order, image rebuilt
-    if (a.pro == KQP_NORM && !rms_mean_certain(q, (int64_t)a.nsb * 256)) emit(kq_seq_scale(a, col));
+    // the check before the one image build (a few integer ops); rare, workgroup-uniform: ggml's own
+    // order.  (A second, fallback image build after the first cost the Q4_K_M step 2.5 % — 1,034 vs
+    // 1,060 tok/s with the check compiled out — through ~6 KB more code per kernel.)
+#ifndef GHIP_KQ_NOCHK  // (A/B builds only: the check's cost)
+    if (__builtin_expect(a.pro == KQP_NORM && !rms_mean_certain(q, (int64_t)a.nsb * 256), 0)) scale = kq_seq_scale(a, col);
+#endif
+    emit(r, scale);
 }
 
 __device__ __forceinline__ double *kq_red(uint8_t *xs, int nsb) {
@@ -459,11 +462,16 @@ __device__ __forceinline__ double kq_tree(double part[8], int J, int lane, doubl
     return __shfl(v, 0);
 }
 
+// HO: the hand-off kind as a template constant (0 none, 1 KQO_QUANT, 2 KQO_NORM; -1 read from
+// a.q8_mode): the norm tail holds the whole column in registers (~200 VGPRs), so a kernel that
+// compiles it in runs at 2 waves per SIMD even when it only quantizes (111 VGPRs without it)
+template <int HO = -1>
 __device__ __forceinline__ void kq_handoff(const kq_args &a, int col, int64_t g, int lane, uint8_t *lds) {
+    if (HO == 0 || (HO < 0 && a.q8_mode == KQO_NONE)) return;
     if (a.q8_abl & 2) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int nsb_y = (int)(a.rows / 256);
-    const bool quant = a.q8_mode == KQO_QUANT;
+    const bool quant = HO == 1 || (HO < 0 && a.q8_mode == KQO_QUANT);
     const int idx = (int)(g / 32);
     unsigned *cnt = a.q8_cnt + (int64_t)col * (quant ? nsb_y : nsb_y + 1) * 32;
     if (!kq_count(cnt + idx * 32, 32u, lane)) return;
@@ -476,6 +484,7 @@ __device__ __forceinline__ void kq_handoff(const kq_args &a, int col, int64_t g,
         q8K_store(xv, lane, out + (int64_t)idx * 292);
         return;
     }
+    if (HO == 1) return;
     if (!kq_count(cnt + nsb_y * 32, (unsigned)nsb_y, lane)) return;
     // nsb_y <= 8 (launch_matvec_kq checks): the column in registers
     float4 xv[8], wv[8];
@@ -498,7 +507,7 @@ __device__ __forceinline__ void kq_handoff(const kq_args &a, int col, int64_t g,
     const double sum = kq_tree(part, nsb_y, lane, (double *)lds);
     const double q = sum / (double)a.rows;
     float mean = (float)q;
-    if (!rms_mean_certain(q, a.rows))  // rare: ggml's own order, from the same sc1 loads
+    if (__builtin_expect(!rms_mean_certain(q, a.rows), 0))  // rare: ggml's own order, from the same sc1 loads
         mean = (float)(seq_sumsq_wave(a.rows, [&](int64_t i0, float v[8]) {
                            const float4 u = kq_ld4_sc1(y + i0, a.q8_abl & 8), w = kq_ld4_sc1(y + i0 + 4, a.q8_abl & 8);
                            v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
@@ -555,8 +564,15 @@ __device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t r
     }
 }
 
-template <int WT, bool DUAL, int XJ, bool TL, int PF = KQ_PF>
-__global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
+#ifndef GHIP_KQ_WPE
+#define GHIP_KQ_WPE 0  // k_matvec_kq: minimum waves per SIMD the compiler must fit (0: its choice)
+#endif
+template <int WT, bool DUAL, int XJ, bool TL, int HO, int PF = KQ_PF>
+__global__ void __launch_bounds__(KQ_THREADS)
+#if GHIP_KQ_WPE
+__attribute__((amdgpu_waves_per_eu(GHIP_KQ_WPE)))
+#endif
+k_matvec_kq(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];  // the column's Q8_K blocks
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
     const int col = blockIdx.y;
@@ -616,7 +632,7 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
         }
         if (DUAL) kq_store_gu<WT>(a, col, row_raw, l, acc, accm, acc2, accm2);
         else kq_store<WT>(a, col, row_raw, l, acc, accm);
-        if (a.q8_mode != KQO_NONE) kq_handoff(a, col, g, lane, xs);
+        kq_handoff<HO>(a, col, g, lane, xs);
     }
 }
 
@@ -625,7 +641,7 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq(kq_args a) {
 // segment's weight loads issued before the prologue (one round trip, overlapping it).  Wave 2j+1
 // stashes its exact terms; after one barrier wave 2j continues its own chains through them in
 // super-block order — the identical fmaf sequences — then stores gelu(gate)*up (+ the D hand-off).
-template <int WT, int XJ, bool TL>
+template <int WT, int XJ, bool TL, int HO>
 __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq_gu2(kq_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
     constexpr int HS = 4;  // super-blocks per half (nsb <= 8)
@@ -698,7 +714,7 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq_gu2(kq_args a) {
         }
     }
     kq_store_gu<WT>(a, col, row_raw, l, acc, accm, acc2, accm2);
-    if (a.q8_mode != KQO_NONE) kq_handoff(a, col, g, lane, xs);
+    kq_handoff<HO>(a, col, g, lane, xs);
 }
 
 // T-column form (the batched prefill): NC columns per workgroup share every weight load, so the
@@ -823,7 +839,7 @@ __device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
         if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(st_m[s * 8 + rr], (float)st_p[s * 64 + lane], accm);
     }
     kq_store<WT>(a, col, row_raw, l, acc, accm);
-    if (a.q8_mode != KQO_NONE) kq_handoff(a, col, gx, lane, xs);  // waves 1.. are gone: LDS is free
+    kq_handoff(a, col, gx, lane, xs);  // waves 1.. are gone: LDS is free
 }
 
 template <int WT, int KS, int XJ, int PF, bool TL>
@@ -956,7 +972,7 @@ __global__ void __launch_bounds__(1024) k_norm_q8K(const float *x, int64_t ldx, 
     }
     const double q = red[0] / (double)E;
     float mean = (float)q;
-    if (!rms_mean_certain(q, E)) {  // workgroup-uniform; rare: ggml's own order
+    if (__builtin_expect(!rms_mean_certain(q, E), 0)) {  // workgroup-uniform; rare: ggml's own order
         const float *xr = x + (int64_t)r * ldx;
         mean = (float)(seq_sumsq_wave(E, [&](int64_t i0, float v[8]) {
                            const float4 u = *(const float4 *)(xr + i0), w4 = *(const float4 *)(xr + i0 + 4);
@@ -1298,13 +1314,21 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         const size_t lds2 = std::max(((img0 + 15) & ~(size_t)15) + (size_t)a.nsb * 64 * sizeof(double) +
                                          (size_t)2 * (2 * 4 * 64 * 2 * 4 + 2 * 4 * 8 * 2 * 4), img);
         const dim3 grid((unsigned)((groups + 1) / 2), a.ncols);
-        if (a.tiled) {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q4_K, 2, true>), grid, dim3(KQ_THREADS), lds2, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q6_K, 2, true>), grid, dim3(KQ_THREADS), lds2, s, a);
-        } else {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q4_K, 2, false>), grid, dim3(KQ_THREADS), lds2, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q6_K, 2, false>), grid, dim3(KQ_THREADS), lds2, s, a);
-        }
+        const int ho = a.q8_mode == KQO_NONE ? 0 : a.q8_mode == KQO_QUANT ? 1 : 2;
+#define GHIP_KQ_GU2(HO)                                                                                          \
+    do {                                                                                                         \
+        if (a.tiled) {                                                                                           \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q4_K, 2, true, HO>), grid, dim3(KQ_THREADS), lds2, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q6_K, 2, true, HO>), grid, dim3(KQ_THREADS), lds2, s, a);            \
+        } else {                                                                                                 \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q4_K, 2, false, HO>), grid, dim3(KQ_THREADS), lds2, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q6_K, 2, false, HO>), grid, dim3(KQ_THREADS), lds2, s, a);            \
+        }                                                                                                        \
+    } while (0)
+        if (ho == 0) GHIP_KQ_GU2(0);
+        else if (ho == 1) GHIP_KQ_GU2(1);
+        else GHIP_KQ_GU2(2);
+#undef GHIP_KQ_GU2
         GHIP_CHECK(hipGetLastError());
         return 0;
     }
@@ -1315,15 +1339,22 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         return -1;
     }
     const dim3 grid(grid_x, a.ncols);
-#define GHIP_KQ_LAUNCH(DUAL, XJ)                                                                              \
+    const int ho = a.q8_mode == KQO_NONE ? 0 : a.q8_mode == KQO_QUANT ? 1 : 2;
+#define GHIP_KQ_LAUNCH_HO(DUAL, XJ, HO)                                                                       \
     do {                                                                                                      \
         if (a.tiled) {                                                                                        \
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, true>), grid, dim3(KQ_THREADS), lds, s, a); \
-            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, true>), grid, dim3(KQ_THREADS), lds, s, a);            \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, true, HO>), grid, dim3(KQ_THREADS), lds, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, true, HO>), grid, dim3(KQ_THREADS), lds, s, a);            \
         } else {                                                                                              \
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, false>), grid, dim3(KQ_THREADS), lds, s, a); \
-            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, false>), grid, dim3(KQ_THREADS), lds, s, a);            \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, false, HO>), grid, dim3(KQ_THREADS), lds, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, false, HO>), grid, dim3(KQ_THREADS), lds, s, a);            \
         }                                                                                                     \
+    } while (0)
+#define GHIP_KQ_LAUNCH(DUAL, XJ)                 \
+    do {                                         \
+        if (ho == 0) GHIP_KQ_LAUNCH_HO(DUAL, XJ, 0); \
+        else if (ho == 1) GHIP_KQ_LAUNCH_HO(DUAL, XJ, 1); \
+        else GHIP_KQ_LAUNCH_HO(DUAL, XJ, 2);     \
     } while (0)
     const bool wide = a.pro != KQP_COPY && a.nsb > 8;  // more than 2 super-blocks per wave
     if (a.w2) {
@@ -1334,6 +1365,7 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         else GHIP_KQ_LAUNCH(false, 2);
     }
 #undef GHIP_KQ_LAUNCH
+#undef GHIP_KQ_LAUNCH_HO
     GHIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -363,7 +363,7 @@ __device__ __forceinline__ void finish_activation(const mv_args &a, int col, uin
     return;
 #endif
     const int64_t n = a.nb * 32;
-    if (rms_mean_certain(ns.q, n)) return;
+    if (__builtin_expect(rms_mean_certain(ns.q, n), 1)) return;  // the fallback placed out of line
     const act_src<WT, PRO, R, NSA, NTH> src(a, col, r);
     const float mean = (float)(seq_sumsq_wave(n, [&](int64_t i0, float v[8]) { load8<WT, PRO>(a, src.x, src.tok, i0, v); }) /
                                (double)n);

@@ -512,7 +512,12 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
 // the per-head form (k_attn_head) lives in attn_impl.h: the fused layer-front kernel runs it too
 __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int S = a.dsplit, G = a.H / a.Hkv, hs = blockIdx.x >> 3, h = hs / S, kvh = h / G;
+    const int S = a.dsplit, G = a.H / a.Hkv;
+    if (a.spread) {  // blocks round-robin over the XCDs: head h on XCD h % 8 (speed only)
+        attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false>(a, (int)blockIdx.x % a.H, smem, nullptr, (int)blockIdx.x / a.H);
+        return;
+    }
+    const int hs = blockIdx.x >> 3, h = hs / S, kvh = h / G;
     if ((int)(blockIdx.x & 7) != (kvh & 7)) return;  // the G*S workgroups of a kv head share an XCD (speed only)
     attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false>(a, h, smem, nullptr, hs % S);
 }
@@ -886,7 +891,9 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
         }
         if (lds > 64 * 1024)
             GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_head, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k_attn_head, dim3(8 * a.H * a.dsplit), dim3(AH_THREADS), lds, s, la);
+        const char *xcd_s = getenv("GHIP_ATT_XCD");  // 1: heads spread over the XCDs (attn_args::spread)
+        la.spread = xcd_s && atoi(xcd_s) == 1;
+        hipLaunchKernelGGL(k_attn_head, dim3((la.spread ? 1 : 8) * a.H * a.dsplit), dim3(AH_THREADS), lds, s, la);
         GHIP_CHECK(hipGetLastError());
         return 0;
     }

@@ -262,7 +262,7 @@ __device__ void norm_quant(bool aux, int atid, const float *xf, const norm_w<E> 
         for (int k = 0; k < TK_AUX; ++k) sum += red[k];
         const double qm = sum / (double)E;
         float mean = (float)qm;
-        if (!rms_mean_certain(qm, E))  // uniform over the aux waves; rare: ggml's own order
+        if (__builtin_expect(!rms_mean_certain(qm, E), 0))  // uniform over the aux waves; rare: ggml's own order
             mean = (float)(seq_sumsq_wave(E, [&](int64_t i0, float v[8]) {
                                const float4 u = *(const float4 *)(xf + i0), u4 = *(const float4 *)(xf + i0 + 4);
                                v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = u4.x; v[5] = u4.y; v[6] = u4.z; v[7] = u4.w;
