@@ -125,6 +125,7 @@ struct kq_args {  // y[c][r] = vec_dot_{q4_K,q6_K}_q8_K(row r of w, column c of 
     int q8_abl = 0;  // timing ablation only (wrong bytes): 1 no tail work, 2 no counting, 4 plain stores
     int tiled = 0;   // w (and w2) in the lane-contiguous layout of launch_kq_retile
     int gu2 = 0;     // DUAL, one column: the K-split-in-two gate/up kernel (k_matvec_kq_gu2)
+    unsigned long long *dbg_t = nullptr;  // stamps build: 16 s_memrealtime per workgroup (k_matvec_kq)
 };
 // ggml K-quant rows <-> the lane-contiguous device layout the matvec reads with one vector load per
 // lane (Q4_K any K % 256 == 0, Q6_K K % 2048 == 0); src != dst

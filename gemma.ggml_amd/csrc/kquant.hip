@@ -183,7 +183,8 @@ __device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *
 #endif
 constexpr int KQ_PF = GHIP_KQ_PF;
 #ifndef GHIP_KQ_EARLY
-#define GHIP_KQ_EARLY 1  // 1: first weight round issued before the Q8_K staging
+#define GHIP_KQ_EARLY 2  // 1: first weight round issued before the Q8_K staging; 2: after every wave's
+                         // activation loads (one s_barrier): Q4_K_M 1,066-1,067 vs 1,053-1,066 tok/s
 #endif
 #ifndef GHIP_KQ_NORM1
 #define GHIP_KQ_NORM1 1  // 1: the norm prologue's tree with one barrier (every wave runs the lane levels)
@@ -567,7 +568,7 @@ __device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t r
 #ifndef GHIP_KQ_WPE
 #define GHIP_KQ_WPE 0  // k_matvec_kq: minimum waves per SIMD the compiler must fit (0: its choice)
 #endif
-template <int WT, bool DUAL, int XJ, bool TL, int HO, int PF = KQ_PF>
+template <int WT, bool DUAL, int XJ, bool TL, int HO, int NSB = 0, int PF = KQ_PF>
 __global__ void __launch_bounds__(KQ_THREADS)
 #if GHIP_KQ_WPE
 __attribute__((amdgpu_waves_per_eu(GHIP_KQ_WPE)))
@@ -578,15 +579,30 @@ k_matvec_kq(kq_args a) {
     const int col = blockIdx.y;
     const int64_t n_groups = (a.rows + 7) / 8;
     const int64_t g0 = (int64_t)blockIdx.x * (KQ_THREADS / 64) + wave;
+#define KQ_STAMP(i)                                                                                              \
+    do {                                                                                                         \
+        if (GHIP_STAMPS && a.dbg_t && tid == 0)                                                                  \
+            a.dbg_t[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    KQ_STAMP(0);
     // the first round of weight loads goes out before the Q8_K staging, so its HBM round trip
     // overlaps the activation copy into LDS (the Q4_0 matvec's ring-before-prologue)
     // DUAL (ffn gate and up in one launch): the up matrix w2 (same type and shape) streams beside the
     // gate rows, each in its own ordered chain; the epilogue forms gelu(gate) * up in registers
     kq_pro_regs<XJ> pr;
     kq_pro_load<XJ>(a, col, wave, KQ_THREADS / 64, lane, pr);
-    kq_raw<WT> r[PF], r2[DUAL ? PF : 1];
+    // NSB > 0 (compile-time super-blocks per row, one row group per wave): the rounds of PF
+    // super-blocks are software-pipelined — round k + 1's loads go out before round k's arithmetic,
+    // into the other half of rb — instead of each round's load waiting behind the previous round's
+    // arithmetic (NSB / PF dependent round trips: 6 of the K-quant gate/up's 12 µs, stamps)
+    kq_raw<WT> rb[2][PF], rb2[2][DUAL ? PF : 1];
+    kq_raw<WT>(&r)[PF] = rb[0];
+    kq_raw<WT>(&r2)[DUAL ? PF : 1] = rb2[0];
 #if GHIP_KQ_EARLY
     {
+        // GHIP_KQ_EARLY 2: every wave's activation loads go out before ANY wave's weight loads (one
+        // s_barrier; no wait): a wave's x / w requests no longer queue behind its neighbours' weights
+        if (GHIP_KQ_EARLY == 2 && a.pro != KQP_COPY) __builtin_amdgcn_s_barrier();
         const int64_t row0 = g0 * 8 + rr < a.rows ? g0 * 8 + rr : a.rows - 1;
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
@@ -598,8 +614,56 @@ k_matvec_kq(kq_args a) {
 #else
     constexpr bool early = false;
 #endif
+    if (GHIP_STAMPS == 1 && a.dbg_t) {  // stamps: the activation loads have landed (the first weight
+        // round, issued after them, stays in flight: 2 loads per super-block and matrix, TL Q4_K)
+        if (DUAL && TL && WT == T_Q4_K && PF == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        KQ_STAMP(6);
+    }
     kq_pro_build<XJ>(a, xs, kq_red(xs, a.nsb), col, tid, KQ_THREADS, pr);
+    KQ_STAMP(1);
     __syncthreads();
+    KQ_STAMP(2);
+    if constexpr (NSB > 0 && GHIP_KQ_EARLY) {
+        static_assert(NSB % PF == 0, "whole rounds");
+        constexpr int NR = NSB / PF;
+        if (g0 < n_groups) {  // wave-uniform; the launch gives every row group its own wave
+            const int64_t row_raw = g0 * 8 + rr;
+            const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
+            const uint8_t *wrow = a.w + row * a.row_bytes;
+            const uint8_t *wrow2 = DUAL ? a.w2 + row * a.row_bytes : nullptr;
+            float acc = 0.0f, accm = 0.0f, acc2 = 0.0f, accm2 = 0.0f;
+#pragma unroll
+            for (int rd = 0; rd < NR; ++rd) {
+                if (rd + 1 < NR) {
+#pragma unroll
+                    for (int p = 0; p < PF; ++p) {
+                        rb[(rd + 1) & 1][p] = kq_load<WT, TL>(wrow, (rd + 1) * PF + p, l);
+                        if (DUAL) rb2[(rd + 1) & 1][p] = kq_load<WT, TL>(wrow2, (rd + 1) * PF + p, l);
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < PF; ++p) {
+                    const int sb = rd * PF + p;
+                    const kq_term t = kq_terms<WT>(rb[rd & 1][p], xs, sb, l);
+                    acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
+                    if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
+                    if (DUAL) {
+                        const kq_term u = kq_terms<WT>(rb2[rd & 1][p], xs, sb, l);
+                        acc2 = __builtin_fmaf(u.d, (float)u.sumi, acc2);
+                        if (WT == T_Q4_K && l < 4) accm2 = __builtin_fmaf(u.dmin, (float)u.prod, accm2);
+                    }
+                }
+            }
+            KQ_STAMP(3);
+            if (DUAL) kq_store_gu<WT>(a, col, row_raw, l, acc, accm, acc2, accm2);
+            else kq_store<WT>(a, col, row_raw, l, acc, accm);
+            KQ_STAMP(4);
+            kq_handoff<HO>(a, col, g0, lane, xs);
+        }
+        KQ_STAMP(5);
+        return;
+    }
     for (int64_t g = g0; g < n_groups; g += (int64_t)gridDim.x * (KQ_THREADS / 64)) {
         const int64_t row_raw = g * 8 + rr;
         const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;  // all lanes stay active for the folds
@@ -630,10 +694,14 @@ k_matvec_kq(kq_args a) {
                 }
             }
         }
+        KQ_STAMP(3);
         if (DUAL) kq_store_gu<WT>(a, col, row_raw, l, acc, accm, acc2, accm2);
         else kq_store<WT>(a, col, row_raw, l, acc, accm);
+        KQ_STAMP(4);
         kq_handoff<HO>(a, col, g, lane, xs);
     }
+    KQ_STAMP(5);
+#undef KQ_STAMP
 }
 
 // gate and up (DUAL) with K split in two (K = 512..2048): a 4-wave workgroup takes 2 row groups,
@@ -1340,24 +1408,34 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     }
     const dim3 grid(grid_x, a.ncols);
     const int ho = a.q8_mode == KQO_NONE ? 0 : a.q8_mode == KQO_QUANT ? 1 : 2;
-#define GHIP_KQ_LAUNCH_HO(DUAL, XJ, HO)                                                                       \
+#define GHIP_KQ_LAUNCH_HO(DUAL, XJ, HO, NSB)                                                                  \
     do {                                                                                                      \
         if (a.tiled) {                                                                                        \
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, true, HO>), grid, dim3(KQ_THREADS), lds, s, a); \
-            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, true, HO>), grid, dim3(KQ_THREADS), lds, s, a);            \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, true, HO, NSB>), grid, dim3(KQ_THREADS), lds, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, true, HO, NSB>), grid, dim3(KQ_THREADS), lds, s, a);            \
         } else {                                                                                              \
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, false, HO>), grid, dim3(KQ_THREADS), lds, s, a); \
-            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, false, HO>), grid, dim3(KQ_THREADS), lds, s, a);            \
+            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, DUAL, XJ, false, HO, NSB>), grid, dim3(KQ_THREADS), lds, s, a); \
+            else hipLaunchKernelGGL((k_matvec_kq<T_Q6_K, DUAL, XJ, false, HO, NSB>), grid, dim3(KQ_THREADS), lds, s, a);            \
         }                                                                                                     \
     } while (0)
 #define GHIP_KQ_LAUNCH(DUAL, XJ)                 \
     do {                                         \
-        if (ho == 0) GHIP_KQ_LAUNCH_HO(DUAL, XJ, 0); \
-        else if (ho == 1) GHIP_KQ_LAUNCH_HO(DUAL, XJ, 1); \
-        else GHIP_KQ_LAUNCH_HO(DUAL, XJ, 2);     \
+        if (ho == 0) GHIP_KQ_LAUNCH_HO(DUAL, XJ, 0, 0); \
+        else if (ho == 1) GHIP_KQ_LAUNCH_HO(DUAL, XJ, 1, 0); \
+        else GHIP_KQ_LAUNCH_HO(DUAL, XJ, 2, 0);  \
     } while (0)
     const bool wide = a.pro != KQP_COPY && a.nsb > 8;  // more than 2 super-blocks per wave
-    if (a.w2) {
+    // gate/up rows of 8 super-blocks (Gemma-2B): the software-pipelined rounds (NSB = 8); every row
+    // group gets its own wave when grid_x * 4 covers them (GHIP_KQ_PIPE=0: the round-trip loop)
+    // (measured: the dot phase 6.0 -> 1.9 µs in the stamps, but Q4_K_M 1,044-1,045 vs 1,044-1,054
+    // tok/s without it — the launch stays bandwidth / issue bound; off by default)
+    static const int kq_pipe = getenv("GHIP_KQ_PIPE") ? atoi(getenv("GHIP_KQ_PIPE")) : 0;
+    const bool pipe8 = kq_pipe && GHIP_KQ_EARLY && a.nsb == 8 && !wide && (int64_t)grid_x * (KQ_THREADS / 64) >= groups;
+    if (a.w2 && pipe8) {
+        if (ho == 0) GHIP_KQ_LAUNCH_HO(true, 2, 0, 8);
+        else if (ho == 1) GHIP_KQ_LAUNCH_HO(true, 2, 1, 8);
+        else GHIP_KQ_LAUNCH_HO(true, 2, 2, 8);
+    } else if (a.w2) {
         if (wide) GHIP_KQ_LAUNCH(true, 8);
         else GHIP_KQ_LAUNCH(true, 2);
     } else {
