@@ -67,6 +67,42 @@ __device__ __forceinline__ float wave_max(float v) {
     return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 
+// T / n for the norms' mean: an exact scaling by 2^-k when n = 2^k (no double division on the
+// prologue's critical path; the quotient is the same bits), else the IEEE division
+__device__ __forceinline__ double div_by_n(double T, int64_t n) {
+#ifdef GHIP_DIVN_OLD  // (A/B builds only)
+    return T / (double)n;
+#endif
+    if ((n & (n - 1)) == 0) {
+        const int k = __builtin_ctzll((unsigned long long)n);
+        return T * __builtin_bit_cast(double, (unsigned long long)(1023 - k) << 52);
+    }
+    return T / (double)n;
+}
+
+// a double's DPP move (two dword moves)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    return __builtin_bit_cast(double, ((unsigned long long)dpp_u<CTRL>((uint32_t)(b >> 32)) << 32) | dpp_u<CTRL>((uint32_t)b));
+}
+// the wave's sum of a double in every lane, by DPP within 16-lane rows and v_readlane across them
+// (no LDS round trips).  The ORDER is this butterfly's, not a sequential one: only for sums whose
+// use is order-proof (the rms_norm mean under rms_mean_certain)
+__device__ __forceinline__ double wave_sum_f64(double v) {
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    v += dpp_d<0x141>(v);
+    v += dpp_d<0x140>(v);
+    auto rl = [&](int L) {
+        const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, L);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), L);
+        return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+    };
+    return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
+
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
     // integer sum is exact in any order; reduce 32-bit halves with carries via 64-bit adds
     unsigned long long t;

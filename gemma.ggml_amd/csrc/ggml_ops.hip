@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(256) k_g_rms_norm(gt_desc a, gt_desc dst, floa
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    const double q = red[0] / (double)n;
+    const double q = div_by_n(red[0], n);
     float mean = (float)q;
     if (__builtin_expect(!rms_mean_certain(q, n), 0))  // workgroup-uniform; rare: ggml's own order
         mean = (float)(seq_sumsq_wave(n, [&](int64_t i0, float v[8]) {

@@ -187,7 +187,8 @@ constexpr int KQ_PF = GHIP_KQ_PF;
                          // activation loads (one s_barrier): Q4_K_M 1,066-1,067 vs 1,053-1,066 tok/s
 #endif
 #ifndef GHIP_KQ_NORM1
-#define GHIP_KQ_NORM1 1  // 1: the norm prologue's tree with one barrier (every wave runs the lane levels)
+#define GHIP_KQ_NORM1 2  // 2: DPP wave sums + one LDS word per wave (order-free under rms_mean_certain);
+                         // 1: the pairwise tree with one barrier (every wave runs the lane levels)
 #endif
 
 // the column's Q8_K image into LDS: 16-B loads, all of a thread's loads issued before the first
@@ -249,7 +250,7 @@ __device__ __forceinline__ void kq_pro_load(const kq_args &a, int col, int wave,
 // 1/sqrtf(mean + eps) of the column's rms_norm from the prologue's tree sum T (*q = T/n; the caller
 // checks it with rms_mean_certain after the image is built)
 __device__ __forceinline__ float kq_norm_scale(const kq_args &a, double T, double *q) {
-    *q = T / (double)((int64_t)a.nsb * 256);
+    *q = div_by_n(T, (int64_t)a.nsb * 256);
     return 1.0f / sqrtf((float)*q + a.eps);
 }
 // the same from ggml's sequential sum (every wave runs it itself: the rare slow path)
@@ -289,7 +290,22 @@ __device__ void kq_pro_build(const kq_args &a, uint8_t *xs, double *red, int col
         }
         int n = a.nsb * 64;
         const int R = two ? nw : a.nsb;  // rows of 64 partials in the tree
-        if (GHIP_KQ_NORM1 && (R == 2 || R == 4 || R == 8)) {
+        if (GHIP_KQ_NORM1 == 2) {
+            // any summation order is ggml's once rms_mean_certain holds: the wave's
+            // partials by DPP (wave_sum_f64), one LDS word per wave, one barrier — instead of the
+            // pairwise tree's six dependent ds_bpermute levels
+            double p = 0.0;
+#pragma unroll
+            for (int j = 0; j < XJ; ++j)
+                if (wave + nw * j < a.nsb) p += part[j];
+            p = wave_sum_f64(p);
+            if (lane == 0) red[wave] = p;
+            __syncthreads();
+            double T = 0.0;
+            for (int w = 0; w < nw; ++w) T += red[w];
+            scale = kq_norm_scale(a, T, &q);
+            n = 0;  // done
+        } else if (GHIP_KQ_NORM1 && (R == 2 || R == 4 || R == 8)) {
             // the same pairwise tree (h = n/2 per level over R rows of 64 partials, then the six lane
             // levels) with ONE barrier: every wave reads its lane's R partials and runs the row levels
             // in registers and the lane levels itself, so no wave waits for wave 0's tree
@@ -506,7 +522,7 @@ __device__ __forceinline__ void kq_handoff(const kq_args &a, int col, int64_t g,
         part[k] = p;
     }
     const double sum = kq_tree(part, nsb_y, lane, (double *)lds);
-    const double q = sum / (double)a.rows;
+    const double q = div_by_n(sum, a.rows);
     float mean = (float)q;
     if (__builtin_expect(!rms_mean_certain(q, a.rows), 0))  // rare: ggml's own order, from the same sc1 loads
         mean = (float)(seq_sumsq_wave(a.rows, [&](int64_t i0, float v[8]) {
@@ -1038,7 +1054,7 @@ __global__ void __launch_bounds__(1024) k_norm_q8K(const float *x, int64_t ldx, 
         __syncthreads();
         n = h;
     }
-    const double q = red[0] / (double)E;
+    const double q = div_by_n(red[0], E);
     float mean = (float)q;
     if (__builtin_expect(!rms_mean_certain(q, E), 0)) {  // workgroup-uniform; rare: ggml's own order
         const float *xr = x + (int64_t)r * ldx;

@@ -344,7 +344,7 @@ __device__ norm_state build_activation(const mv_args &a, int col, uint8_t *smem,
         __syncthreads();
         double sum = 0.0;
         for (int w = 0; w < nth / 64; ++w) sum += red[w];
-        ns.q = sum / (double)(nb * 32);
+        ns.q = div_by_n(sum, nb * 32);
         scale = 1.0f / sqrtf((float)ns.q + a.eps);
     }
     src.emit(smem, m, scale);

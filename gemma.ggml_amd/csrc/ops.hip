@@ -513,13 +513,19 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
 __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int S = a.dsplit, G = a.H / a.Hkv;
-    if (a.spread) {  // blocks round-robin over the XCDs: head h on XCD h % 8 (speed only)
-        attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false>(a, (int)blockIdx.x % a.H, smem, nullptr, (int)blockIdx.x / a.H);
-        return;
+    // one inlined copy of the body (a second call site, for the XCD-spread mapping, doubled the
+    // kernel's code: measured slower and removed); spread: block b -> head b % H
+    int h, sp;
+    if (a.spread) {
+        h = (int)blockIdx.x % a.H;
+        sp = (int)blockIdx.x / a.H;
+    } else {
+        const int hs = blockIdx.x >> 3;
+        h = hs / S;
+        sp = hs % S;
+        if ((int)(blockIdx.x & 7) != ((h / G) & 7)) return;  // the G*S workgroups of a kv head share an XCD (speed only)
     }
-    const int hs = blockIdx.x >> 3, h = hs / S, kvh = h / G;
-    if ((int)(blockIdx.x & 7) != (kvh & 7)) return;  // the G*S workgroups of a kv head share an XCD (speed only)
-    attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false>(a, h, smem, nullptr, hs % S);
+    attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false>(a, h, smem, nullptr, sp);
 }
 
 // ---- exact causal attention for T prompt rows (the reference's prefill graph) -----------------

@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(256) k_quant_rows(qrow_args a) {
         if ((tid & 63) == 0) red[tid >> 6] = part;
         __syncthreads();
         const double sum = red[0] + red[1] + red[2] + red[3];
-        const double q = sum / (double)K;
+        const double q = div_by_n(sum, K);
         float mean = (float)q;
         if (__builtin_expect(!rms_mean_certain(q, K), 0))  // workgroup-uniform; rare: ggml's own order
             mean = (float)(seq_sumsq_wave(K, [&](int64_t i0, float v[8]) { load(i0, v); }) / (double)K);

@@ -12,6 +12,12 @@
 #ifndef GHIP_Q8K_DPP
 #define GHIP_Q8K_DPP 1
 #endif
+#ifndef GHIP_Q8K_F32DIV
+#define GHIP_Q8K_F32DIV 1
+#endif
+#ifndef GHIP_Q8K_RL
+#define GHIP_Q8K_RL 1  // the cross-row levels of the (|x| max, index) reduction by v_readlane
+#endif
 
 namespace ghip {
 
@@ -19,6 +25,18 @@ namespace ghip {
 // 16 lanes (xor 1, xor 2 by quad permutes; the 4- and 8-lane steps by the half-row / row mirrors,
 // which pair each group with its neighbour), ds_bpermute across rows.  The reduction (max, ties to
 // the smaller index) is order-independent, so any pairing gives the same result in every lane.
+// ggml's float division a / b (quantize_row_q8_K: iscale = -127.f/max, d = 1/iscale), correctly
+// rounded: the f32 IEEE division (hipcc's default -fhip-fp32-correctly-rounded-divide-sqrt), which
+// equals the double quotient rounded to float for float operands (53 >= 2*24 + 2 bits) — the form
+// used before, at twice the latency
+__device__ __forceinline__ float q8k_div(float a, float b) {
+#if GHIP_Q8K_F32DIV
+    return a / b;
+#else
+    return (float)((double)a / (double)b);
+#endif
+}
+
 template <int OFF>
 __device__ __forceinline__ uint32_t q8k_partner(uint32_t v) {
     if constexpr (OFF == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
@@ -43,8 +61,30 @@ __device__ __forceinline__ void q8k_amax_reduce(float &amax, float &mx, int &idx
     q8k_amax_level<2>(amax, mx, idx);
     q8k_amax_level<4>(amax, mx, idx);
     q8k_amax_level<8>(amax, mx, idx);
+#if GHIP_Q8K_RL
+    // every lane of a 16-lane row now holds the row's best: the four rows by v_readlane (uniform
+    // values, no LDS round trip) instead of two ds_bpermute levels — the same winner
+    float ba = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amax), 0));
+    float bm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mx), 0));
+    int bi = __builtin_amdgcn_readlane(idx, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) {
+        const float ra = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amax), r));
+        const float rm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mx), r));
+        const int ri = __builtin_amdgcn_readlane(idx, r);
+        if (ra > ba || (ra == ba && ri < bi)) {
+            ba = ra;
+            bm = rm;
+            bi = ri;
+        }
+    }
+    amax = ba;
+    mx = bm;
+    idx = bi;
+#else
     q8k_amax_level<16>(amax, mx, idx);
     q8k_amax_level<32>(amax, mx, idx);
+#endif
 }
 
 __device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *blk) {
@@ -76,10 +116,10 @@ __device__ __forceinline__ void q8K_store(const float xv[4], int lane, uint8_t *
     int q[4] = {0, 0, 0, 0};
     float d = 0.0f;
     if (amax != 0.0f) {
-        const float iscale = (float)(-127.0 / (double)mx);
+        const float iscale = q8k_div(-127.0f, mx);
 #pragma unroll
         for (int j = 0; j < 4; ++j) q[j] = min(127, (int)__builtin_rintf(iscale * xv[j]));
-        d = (float)(1.0 / (double)iscale);
+        d = q8k_div(1.0f, iscale);
     }
     int bs = q[0] + q[1] + q[2] + q[3];
     bs += (int)q8k_partner<1>((uint32_t)bs);  // sums of 16 (4 lanes): exact integer adds
@@ -140,10 +180,10 @@ __device__ __forceinline__ void q8K_store_n(const float (&xv)[N][4], int lane, u
         int q[4] = {0, 0, 0, 0};
         float d = 0.0f;
         if (amax[k] != 0.0f) {
-            const float iscale = (float)(-127.0 / (double)mx[k]);
+            const float iscale = q8k_div(-127.0f, mx[k]);
 #pragma unroll
             for (int j = 0; j < 4; ++j) q[j] = min(127, (int)__builtin_rintf(iscale * xv[k][j]));
-            d = (float)(1.0 / (double)iscale);
+            d = q8k_div(1.0f, iscale);
         }
         bs[k] = q[0] + q[1] + q[2] + q[3];
         uint8_t *b = blk + k * stride;

@@ -260,7 +260,7 @@ __device__ void norm_quant(bool aux, int atid, const float *xf, const norm_w<E> 
     if (aux) {
         double sum = 0.0;
         for (int k = 0; k < TK_AUX; ++k) sum += red[k];
-        const double qm = sum / (double)E;
+        const double qm = div_by_n(sum, E);
         float mean = (float)qm;
         if (__builtin_expect(!rms_mean_certain(qm, E), 0))  // uniform over the aux waves; rare: ggml's own order
             mean = (float)(seq_sumsq_wave(E, [&](int64_t i0, float v[8]) {
