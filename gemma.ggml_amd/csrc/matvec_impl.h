@@ -213,6 +213,9 @@ __device__ __forceinline__ void prefetch_activation(const mv_args &a, int col, a
     }
 }
 
+#ifndef GHIP_MV_NORM_DPP
+#define GHIP_MV_NORM_DPP 1
+#endif
 // The rms_norm's tree sum and mean (PRO_NORM / PRO_EMBED), kept for finish_activation's check.
 struct norm_state {
     double q = 0.0;  // T/n: float(q) is the mean
@@ -338,8 +341,12 @@ __device__ norm_state build_activation(const mv_args &a, int col, uint8_t *smem,
             }
         }
         double *red = (double *)(smem + m.red);
+#if GHIP_MV_NORM_DPP
+        part = wave_sum_f64(part);  // DPP + v_readlane: no ds_bpermute round trips (any order: §3)
+#else
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);  // (once per launch)
+#endif
         if ((tid & 63) == 0) red[tid >> 6] = part;
         __syncthreads();
         double sum = 0.0;

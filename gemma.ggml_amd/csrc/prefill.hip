@@ -127,8 +127,7 @@ __global__ void __launch_bounds__(256) k_quant_rows(qrow_args a) {
             }
         }
         __shared__ double red[4];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+        part = wave_sum_f64(part);  // any order: the mean is certified
         if ((tid & 63) == 0) red[tid >> 6] = part;
         __syncthreads();
         const double sum = red[0] + red[1] + red[2] + red[3];
