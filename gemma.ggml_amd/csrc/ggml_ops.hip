@@ -118,14 +118,11 @@ __global__ void __launch_bounds__(256) k_g_rms_norm(gt_desc a, gt_desc dst, floa
         const float x = *(const float *)(src + k * a.nb[0]);
         part += (double)(x * x);
     }
-    __shared__ double red[256];
-    red[threadIdx.x] = part;
+    __shared__ double red[4];
+    part = wave_sum_f64(part);  // any order: the mean is certified below
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    const double q = div_by_n(red[0], n);
+    const double q = div_by_n((red[0] + red[1]) + (red[2] + red[3]), n);
     float mean = (float)q;
     if (__builtin_expect(!rms_mean_certain(q, n), 0))  // workgroup-uniform; rare: ggml's own order
         mean = (float)(seq_sumsq_wave(n, [&](int64_t i0, float v[8]) {

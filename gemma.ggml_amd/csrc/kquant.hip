@@ -1045,16 +1045,14 @@ __global__ void __launch_bounds__(1024) k_norm_q8K(const float *x, int64_t ldx, 
     double part = 0.0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) part += (double)(xv[j] * xv[j]);
-    red[tid] = part;
+    // any order (the mean is certified below): DPP wave sums, one word per wave, one
+    // barrier — instead of a pairwise tree with a barrier per level
+    part = wave_sum_f64(part);
+    if ((tid & 63) == 0) red[tid >> 6] = part;
     __syncthreads();
-    int n = nt;
-    while (n > 1) {  // pairwise tree over any thread count
-        const int h = (n + 1) >> 1;
-        if (tid + h < n) red[tid] += red[tid + h];
-        __syncthreads();
-        n = h;
-    }
-    const double q = div_by_n(red[0], E);
+    double tot = 0.0;
+    for (int w = 0; w < (nt >> 6); ++w) tot += red[w];
+    const double q = div_by_n(tot, E);
     float mean = (float)q;
     if (__builtin_expect(!rms_mean_certain(q, E), 0)) {  // workgroup-uniform; rare: ggml's own order
         const float *xr = x + (int64_t)r * ldx;
