@@ -1414,7 +1414,15 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         GHIP_CHECK(hipGetLastError());
         return 0;
     }
-    const unsigned grid_x = (unsigned)std::min<int64_t>((groups + 3) / 4, 4096);
+    // the output head (single matrix, precomputed image, 32,000 row groups): GHIP_KQ_OGRID=1 gives
+    // every row group its own wave instead of capping the grid at 4,096 workgroups
+    static const int kq_ogrid = getenv("GHIP_KQ_OGRID") ? atoi(getenv("GHIP_KQ_OGRID")) : 0;
+    // GHIP_KQ_PIPE bits (default 2): 1 the gate/up rounds pipelined (measured neutral), 2 the output
+    // head's (Q4_K_M 1,089-1,094 -> 1,103-1,109 tok/s; its grid uncapped alone: 1,091-1,094)
+    static const int kq_pipe = getenv("GHIP_KQ_PIPE") ? atoi(getenv("GHIP_KQ_PIPE")) : 2;
+    const bool single_out = !a.w2 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && a.ncols == 1;
+    const bool uncap = single_out && (kq_ogrid || (kq_pipe & 2));
+    const unsigned grid_x = (unsigned)std::min<int64_t>((groups + 3) / 4, uncap ? (int64_t)1 << 30 : 4096);
     const size_t lds = std::max(img, red);
     if (lds > 64 * 1024) {
         set_error("matvec_kq: row too long for the LDS image");
@@ -1443,15 +1451,17 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     // group gets its own wave when grid_x * 4 covers them (GHIP_KQ_PIPE=0: the round-trip loop)
     // (measured: the dot phase 6.0 -> 1.9 µs in the stamps, but Q4_K_M 1,044-1,045 vs 1,044-1,054
     // tok/s without it — the launch stays bandwidth / issue bound; off by default)
-    static const int kq_pipe = getenv("GHIP_KQ_PIPE") ? atoi(getenv("GHIP_KQ_PIPE")) : 0;
-    const bool pipe8 = kq_pipe && GHIP_KQ_EARLY && a.nsb == 8 && !wide && (int64_t)grid_x * (KQ_THREADS / 64) >= groups;
-    if (a.w2 && pipe8) {
+    // GHIP_KQ_PIPE bits: 1 the gate/up (dual), 2 the output head (single, its grid uncapped)
+    const bool pipe8 = GHIP_KQ_EARLY && a.nsb == 8 && !wide && (int64_t)grid_x * (KQ_THREADS / 64) >= groups;
+    if (a.w2 && pipe8 && (kq_pipe & 1)) {
         if (ho == 0) GHIP_KQ_LAUNCH_HO(true, 2, 0, 8);
         else if (ho == 1) GHIP_KQ_LAUNCH_HO(true, 2, 1, 8);
         else GHIP_KQ_LAUNCH_HO(true, 2, 2, 8);
     } else if (a.w2) {
         if (wide) GHIP_KQ_LAUNCH(true, 8);
         else GHIP_KQ_LAUNCH(true, 2);
+    } else if (single_out && pipe8 && (kq_pipe & 2)) {
+        GHIP_KQ_LAUNCH_HO(false, 2, 0, 8);
     } else {
         if (wide) GHIP_KQ_LAUNCH(false, 8);
         else GHIP_KQ_LAUNCH(false, 2);
