@@ -775,6 +775,9 @@ __device__ __forceinline__ float carry_chain(const void *st_s, const float *st_d
 #ifndef GHIP_UPRE
 #define GHIP_UPRE 4
 #endif
+#ifndef GHIP_MV_XFIRST
+#define GHIP_MV_XFIRST 1  // decode 1,527-1,529 -> 1,529-1,536 tok/s (4 interleaved reps)
+#endif
 #ifndef GHIP_SCL
 #define GHIP_SCL 1  // gate/up scales as one 1 KiB run per row tile and matrix (k_matvec SCL)
 #endif
@@ -829,6 +832,9 @@ __global__ void __launch_bounds__(512) k_matvec(mv_args a) {
         scl_g = ld_sc16(a.sc + rts * 1024 + lane * 16);
         scl_u = ld_sc16(a.sc2 + rts * 1024 + lane * 16);
     }
+    // GHIP_MV_XFIRST: every wave's activation loads go out before any wave's weight ring (one
+    // s_barrier, no wait) — the K-quant prologue's measured +0.5-1 % (kquant.hip GHIP_KQ_EARLY 2)
+    if (GHIP_MV_XFIRST && (PRO == PRO_NORM || PRO == PRO_EMBED)) __builtin_amdgcn_s_barrier();
 
     // 1) fill the register ring: the HBM round trip overlaps the prologue below.  Loads are
     //    never inside a runtime branch (hipcc would wait vmcnt(0) around them): past the last item
