@@ -182,6 +182,9 @@ __device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *
 #define GHIP_KQ_PF 2  // Q4_K_M decode, same box: 1 / 2 / 3 / 4 / 8 -> 1.170 / 1.132 / 1.140 / 1.155 / 1.315 ms/token
 #endif
 constexpr int KQ_PF = GHIP_KQ_PF;
+#ifndef GHIP_KQ_KSX
+#define GHIP_KQ_KSX 0
+#endif
 #ifndef GHIP_KQ_EARLY
 #define GHIP_KQ_EARLY 2  // 1: first weight round issued before the Q8_K staging; 2: after every wave's
                          // activation loads (one s_barrier): Q4_K_M 1,066-1,067 vs 1,053-1,066 tok/s
@@ -881,6 +884,8 @@ __device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
     kq_pro_load<XJ>(a, col, wave, KS, lane, pr);
     kq_raw<WT> r[PF];
 #if GHIP_KQ_EARLY
+    // (GHIP_KQ_KSX: the k_matvec_kq EARLY=2 barrier here too — every wave's activation loads first)
+    if (GHIP_KQ_KSX && GHIP_KQ_EARLY == 2 && a.pro != KQP_COPY) __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int p = 0; p < PF; ++p) r[p] = kq_load<WT, TL>(wrow, p < seg ? wave * seg + p : wave * seg, l);
     bool early = true;
