@@ -8,10 +8,13 @@ shapes, generated on the GPU; DESIGN.md §Synthetic weights) — no checkpoint i
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--profile-out PATH]
 
-N > 1: one process per GPU (torch.distributed.run).  The headline `value` runs one independent
-Gemma-2B decode stream per GPU (weak scaling: tokens over all ranks / max-over-ranks time); the
-`tp_decode` leg runs BASELINE config 4 — Gemma-7B decode with every weight matrix row-split across
-the N GPUs and RCCL all-gathers (strong scaling of one stream).  Rank 0 prints ONE JSON line.
+N > 1: one process per GPU (torch.distributed.run).  The headline `value` is ONE Gemma-2B Q4_0
+decode stream with every weight matrix row-split across the N GPUs and RCCL all-gathers inside the
+decode hipGraph (the north star's partition; strong scaling: the same stream at every N), timed in
+scripts/tp_leg.py children (one per rank, time-limited) with the bench's prompt, warmup and steps,
+every rank's logits checked against the unsplit engine first (a mismatch exits 3 and the line says
+so).  `replicas` keeps N independent streams (one per GPU, weak scaling); the `tp_decode` leg runs
+BASELINE config 4 — Gemma-7B, row-split the same way.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import ctypes as C
@@ -328,21 +331,26 @@ def load_traffic(kernel_id):
         return None
 
 
-def run_tp_leg(args, world, rank):
+def run_tp_leg(args, world, rank, model="7b", steps=None, warmup=4, prompt=16, port_offset=1009):
     """Every rank starts scripts/tp_leg.py as a child (its own gloo rendezvous on another port) and
     waits with a time limit: a hung RCCL collective costs the leg, never the bench line."""
     import subprocess
     env = dict(os.environ)
     if world > 1:
-        env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + 1009)
-    cmd = [sys.executable, os.path.join(ROOT, "scripts", "tp_leg.py"), str(args.tp_steps), args.wtype,
-           "0" if args.no_tune else "1"]
+        env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + port_offset)
+    cmd = [sys.executable, os.path.join(ROOT, "scripts", "tp_leg.py"), str(steps or args.tp_steps), args.wtype,
+           "0" if args.no_tune else "1", model, str(warmup), str(prompt)]
     try:
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.tp_timeout)
     except subprocess.TimeoutExpired:
         return {"error": f"timed out after {args.tp_timeout} s"}
     if r.returncode != 0:
-        return {"error": (r.stderr or r.stdout)[-300:]}
+        if r.returncode == 3 and rank == 0:  # parity mismatch: the leg's own error object
+            try:
+                return dict(json.loads(r.stdout.strip().splitlines()[-1]), exit=3)
+            except Exception:
+                pass
+        return {"error": (r.stderr or r.stdout)[-300:], "exit": r.returncode}
     if rank != 0:
         return None
     try:
@@ -388,6 +396,14 @@ def main():
         torch.cuda.synchronize(local_rank) if torch.cuda.is_available() else None
         if dist is not None:
             dist.barrier()
+
+    # N > 1: the headline stream, Gemma-2B row-split over the N GPUs (children, before this
+    # process's own engines take the GPUs' time)
+    tp2 = None
+    if world > 1:
+        log(f'row-split Gemma-2B stream over {world} GPUs')
+        tp2 = run_tp_leg(args, world, rank, model="2b", steps=args.steps, warmup=args.warmup, prompt=args.prompt,
+                         port_offset=1013)
 
     log('engine: Gemma-2B decode')
     eng = G.Engine(GEMMA_2B, n_ctx=args.ctx, wtype=wtype, device=local_rank)
@@ -625,6 +641,7 @@ def main():
 
     if rank == 0:
         n_tok = args.steps * world
+        rep_tok_s = n_tok / dt  # N independent streams (at N = 1: the headline itself)
         line = {
             "metric": METRIC,
             "value": round(n_tok / dt, 2),
@@ -676,6 +693,29 @@ def main():
         line["token_hbm_frac"] = round(line["token_weight_bytes"] * line["value"] / world / 1e9 / HBM_PEAK_GBS, 4)
         line["token_hbm_frac_of_measured"] = (round(line["token_weight_bytes"] * line["value"] / world / 1e9 / hbm_measured, 4)
                                               if hbm_measured > 0 else None)
+        if world > 1:
+            line["replicas"] = {"value": round(rep_tok_s, 2), "unit": "tok/s", "scaling": "weak",
+                                "ms_per_step": round(dt / args.steps * 1e3, 4),
+                                "what": f"{world} independent Gemma-2B Q4_0 streams, one per GPU (tokens over all "
+                                        f"ranks / max-over-ranks time)", "roofline": line["roofline"]}
+            if tp2 and "tok_s" in tp2:
+                line["value"] = line["decode_tok_s"] = tp2["tok_s"]
+                line["ms_per_step"] = tp2["ms_per_token"]
+                line["scaling"] = "strong"
+                line["config"]["parallelism"] = f"row-split tp{world} (RCCL all-gather x4/layer)"
+                line["config"]["workload"] = (f"ONE Gemma-2B {args.wtype.upper()} greedy decode stream, batch 1, every "
+                                              f"weight matrix row-split over {world} GPUs, after a {args.prompt}-token "
+                                              f"prompt (BASELINE config 2 partitioned as the north star asks)")
+                line["row_split"] = tp2
+                if tp2.get("roofline"):
+                    line["roofline"] = dict(tp2["roofline"], traffic=None)
+                # each token reads the weights once, spread over the N GPUs: against the N GPUs' combined peak
+                line["token_hbm_frac"] = round(line["token_weight_bytes"] * line["value"] / world / 1e9 / HBM_PEAK_GBS, 4)
+                line["token_hbm_frac_of_measured"] = (round(line["token_weight_bytes"] * line["value"] / world / 1e9 / hbm_measured, 4)
+                                                      if hbm_measured > 0 else None)
+            else:  # the row-split stream failed: the line says so and reports the replicas
+                line["row_split"] = tp2
+                line["config"]["parallelism"] = f"replicas x{world} (row-split stream failed, see row_split)"
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -308,7 +308,9 @@ __device__ __forceinline__ void attn_vdma(const attn_args &a, int kvh, int d_lo,
 // shared through the XCD's L2) and the KQV of output dims [sp*hd/S, (sp+1)*hd/S) — each output
 // is still one vec_dot_f16 in ggml's order, so the split changes no bits, only how much of V
 // each CU streams.
-template <int NTH, bool SC1, int KPF = AH_KPF, int VPF = AH_VPF, bool PRE = false>
+// SC1O: the output's Q8_0 image stored write-through (sc1) for a consumer inside the same launch
+// (k_attn_o, layer_front.hip); defaults to SC1 (the inputs were handed off in-launch too)
+template <int NTH, bool SC1, int KPF = AH_KPF, int VPF = AH_VPF, bool PRE = false, bool SC1O = SC1>
 __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, const attn_pre<KPF, VPF> *pre = nullptr,
                               const int sp = 0, const int tid_in = -1) {
     // tid_in: the caller's (opaque) thread index, so that a persistent caller's loop does not keep
@@ -625,7 +627,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = o[j];
-            if (SC1) image_put_quad_sc1(a.out_act, a.out_da, (int64_t)h * (hd / 32) + b, tid & 3, v);
+            if (SC1O) image_put_quad_sc1(a.out_act, a.out_da, (int64_t)h * (hd / 32) + b, tid & 3, v);
             else image_put_quad(a.out_act, nullptr, a.out_da, (int64_t)h * (hd / 32) + b, tid & 3, v);
         }
     }

@@ -254,6 +254,11 @@ struct gemma_engine {
                          // launch boundaries they replace; DESIGN.md perf log) — kept as an option
     unsigned *front_cnt = nullptr;
     int *front_err = nullptr;
+    // attention + attn-out in one launch (layer_front.hip k_attn_o): on / off, its per-layer hand-off
+    // counters (8 replicas + done, 128 B apart; the launch leaves them zero) and sticky error words
+    int att_o = 0;
+    unsigned *ao_cnt = nullptr;
+    int *ao_err = nullptr;
     uint32_t *att_act = nullptr, *h_act = nullptr;
     float *att_da = nullptr, *h_da = nullptr;
     unsigned long long *key = nullptr;
@@ -262,6 +267,8 @@ struct gemma_engine {
     int host_pos = 0;  // mirror of *pos (steps are deterministic)
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
+    // flow control of gemma_engine_step: an event every FC_EVERY graph launches, FC_SLOTS of them
+    hipEvent_t fc_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // launch geometry: one plan per matrix class (defaults below; gemma_engine_tune measures)
     int ks_small = KS_RR, ks_down = KS_RR;  // round-pipelined form where the shape allows (pick_ks falls back)
     int grid_big = 2048;
@@ -449,6 +456,22 @@ static int persist_report(gemma_engine *e, const int *w) {
     return 1;
 }
 
+// After a stream sync that covers k_attn_o launches: a hand-off poll that timed out leaves the sticky
+// word set and the step's numbers wrong.  Report it, clear it and run the two launches from then on.
+static int att_o_check(gemma_engine *e) {
+    if (!e->att_o || !e->ao_err) return 0;
+    int w[5] = {0, 0, 0, 0, 0};
+    if (hipMemcpy(w, e->ao_err, 20, hipMemcpyDeviceToHost) != hipSuccess || !w[0]) return 0;
+    (void)hipMemset(e->ao_err, 0, 64);
+    (void)hipMemset(e->ao_cnt, 0, (size_t)e->cfg.n_layer * 16 * 32 * 4);
+    e->att_o = 0;
+    drop_graph(e);
+    set_error("attention + attn-out launch: hand-off timeout (counter " + std::to_string(w[2]) + " of " +
+              std::to_string(w[3]) + "): the step's logits and KV rows are invalid; the engine now runs the two "
+              "launches");
+    return 1;
+}
+
 static int persist_check(gemma_engine *e) {
     if (!persist_on(e) || !e->tok_err) return 0;
     int w[3] = {0, 0, 0};
@@ -558,6 +581,26 @@ static int enqueue_step(gemma_engine *e) {
             if (launch_mall_warm(ptrs, bytes, 6, e->warm_grid, e->side)) return -1;
         }
         if (t.mode == ATTN_PER_HEAD) t.dsplit = e->att_dsplit;
+        // attention + attn-out in one launch (k_attn_o): the attention's idle workgroups run attn-out
+        if (e->att_o && att_img && e->n_virtual == 1 && e->ao_cnt && !e->warm && e->plan[MC_O].ks == KS_RR) {
+            const layer_dev &L = layer_of(e, il, 0);
+            const size_t r0 = (size_t)rank_of(e, 0) * e->sh_e;
+            attn_o_args f;
+            f.t = t;
+            f.o.qs = L.o.qs; f.o.sc = L.o.sc; f.o.rows = L.o.rows; f.o.n_rt = L.o.n_rt; f.o.n_bt = L.o.n_bt; f.o.nb = L.o.nb;
+            f.o.x = e->att_act; f.o.x_da = e->att_da; f.o.y = e->sa + r0; f.o.resid = e->x + r0;
+            f.cnt = e->ao_cnt + (size_t)il * 16 * 32;
+            f.err = e->ao_err;
+            if (attn_o_supported(wt, f.t, f.o)) {
+                if (launch_attn_o(wt, f, s)) return -1;
+                const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
+                if (e->dbg) GHIP_CHECK(hipMemcpyAsync(e->dbg + tap, e->qkv, (size_t)e->qkv_rows * 4, hipMemcpyDeviceToDevice, s));
+                if (e->dbg)
+                    GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows, e->attn, (size_t)e->qw * 4, hipMemcpyDeviceToDevice, s));
+                if (tp_gather(e, e->sa, e->sh_e)) return -1;
+                goto ffn;
+            }
+        }
         if (launch_attn_decode(t, s)) return -1;
         const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
         if (e->dbg) GHIP_CHECK(hipMemcpyAsync(e->dbg + tap, e->qkv, (size_t)e->qkv_rows * 4, hipMemcpyDeviceToDevice, s));
@@ -1113,6 +1156,10 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         GHIP_FATAL(hipMemset(e->front_cnt, 0, (size_t)c.n_layer * 16 * 32 * 4));
         GHIP_FATAL(hipMemset(e->front_err, 0, 64));
         if (const char *v = getenv("GHIP_FUSE_FRONT")) e->fuse_front = atoi(v);
+        GHIP_FATAL(hipMalloc(&e->ao_cnt, (size_t)c.n_layer * 16 * 32 * 4));
+        GHIP_FATAL(hipMalloc(&e->ao_err, 64));
+        GHIP_FATAL(hipMemset(e->ao_cnt, 0, (size_t)c.n_layer * 16 * 32 * 4));
+        GHIP_FATAL(hipMemset(e->ao_err, 0, 64));
     }
     if (e->sh_ff % 128 == 0) {  // every rank's shard is whole 4-block groups
         GHIP_FATAL(hipMalloc(&e->h_act, (size_t)c.n_ff));
@@ -1359,7 +1406,7 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
             (void)hipFree(L.ffn_norm);
         }
     }
-    void *bufs[] = {e->tok_gran, e->epoch, e->tok_err, e->tok_dev, e->tok_tab, e->front_cnt, e->front_err, e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
+    void *bufs[] = {e->tok_gran, e->epoch, e->tok_err, e->tok_dev, e->tok_tab, e->front_cnt, e->front_err, e->ao_cnt, e->ao_err, e->att_act, e->att_da, e->h_act, e->h_da, e->rope_cur, e->att_sbuf, e->att_sync, e->out_norm, e->kc, e->vc, e->exp_tab, e->gelu_tab, e->rope_cos, e->rope_sin, e->x, e->qkv,
                     e->attn, e->sa, e->h, e->logits, e->key, e->pos, e->token, e->hist, e->nfix, e->pf.X, e->pf.SA, e->pf.QKV, e->pf.ATT, e->pf.G, e->pf.U,
                     e->pf.LG, e->pf.DA, e->pf.Q16, e->pf.XQ, e->pf.XH, e->pf.XM, e->pf.keys};
     for (void *p : bufs)
@@ -1373,6 +1420,8 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     if (e->kq_cnt) (void)hipFree(e->kq_cnt);
     for (hipEvent_t ev : e->ev_fork) (void)hipEventDestroy(ev);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    for (hipEvent_t &ev : e->fc_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (e->side) (void)hipStreamDestroy(e->side);
     if (e->xq8k) (void)hipFree(e->xq8k);
     (void)hipStreamDestroy(e->stream);
@@ -1448,7 +1497,20 @@ extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_
         n -= 1;
         if (ensure_graph(e)) return -1;
     }
+    // Flow control: at most FC_EVERY * FC_SLOTS decode graphs (x 92 kernels) queued ahead of the GPU.
+    // Before the bound, a long step queued every launch at once (a 176-step call: ~16,000 dispatch
+    // packets); rocprofv3 --kernel-trace crashed inside the HIP runtime's graph-launch path on exactly
+    // such calls (175 and 191 queued graphs) and completed on calls of <= 127.  Waiting
+    // on the event of the launch FC_EVERY * FC_SLOTS back never drains the queue, so the GPU never
+    // idles: the host only stops running ahead.
+    constexpr int FC_EVERY = 16, FC_SLOTS = 4;
     for (int i = 0; i < n; ++i) {
+        if (use_graph && !logits && i % FC_EVERY == 0) {
+            hipEvent_t &ev = e->fc_ev[(i / FC_EVERY) % FC_SLOTS];
+            if (!ev) GHIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            if (i >= FC_EVERY * FC_SLOTS) GHIP_CHECK(hipEventSynchronize(ev));
+            GHIP_CHECK(hipEventRecord(ev, e->stream));
+        }
         if (use_graph) GHIP_CHECK(hipGraphLaunch(e->graph_exec, e->stream));
         else if (enqueue_step(e)) return -1;
         if (logits) {
@@ -1461,6 +1523,7 @@ extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_
     }
     GHIP_CHECK(hipStreamSynchronize(e->stream));
     if (persist_check(e)) return -1;  // the sequence must be restarted (gemma_engine_begin)
+    if (att_o_check(e)) return -1;
     return 0;
 }
 
@@ -1843,6 +1906,15 @@ extern "C" int gemma_engine_persist_err(gemma_engine *e, int *out3, int reset) {
     if (out3) memcpy(out3, w, 12);
     if (reset && e->tok_err) GHIP_CHECK(hipMemset(e->tok_err, 0, 64));
     return w[0];
+}
+
+// attention + attn-out in one launch on (1) / off (0) / unchanged (-1); returns the setting
+extern "C" int gemma_engine_set_att_o(gemma_engine *e, int on) {
+    if (on >= 0 && (on != 0) != (e->att_o != 0)) {
+        e->att_o = on != 0 && e->ao_cnt;
+        drop_graph(e);
+    }
+    return e->att_o;
 }
 
 // fused layer front on/off (tests, A/B); returns the sticky hand-off timeout word (0 = none seen)

@@ -317,6 +317,18 @@ struct front_args {
 };
 bool layer_front_supported(int wtype, const mv_args &q, const attn_args &t, const mv_args &o);
 int launch_layer_front(int wtype, const front_args &f, hipStream_t s);
+// the decode attention (per-head form) and attn-out (+ residual) in ONE launch (layer_front.hip
+// k_attn_o): the attention launch's idle workgroups run attn-out's row tiles, weights in flight
+// before the in-launch hand-off of the attention's Q8_0 image
+struct attn_o_args {
+    attn_args t;              // per-head attention, out_act / out_da set (the handed-off image)
+    mv_args o;                // attn-out: PRO_IMG from t.out_act / t.out_da, EPI_ADD
+    unsigned *cnt = nullptr;  // this layer's counters: 8 replicas + the consumers' done count, 128 B apart;
+                              // zero before the launch, and the launch leaves them zero
+    int *err = nullptr;       // sticky: a hand-off poll timed out (err[0]; err[1..4] diagnostics)
+};
+bool attn_o_supported(int wtype, const attn_args &t, const mv_args &o);
+int launch_attn_o(int wtype, const attn_o_args &f, hipStream_t s);
 
 // ---- the whole decode token's layers as ONE persistent launch (token.hip) ----------
 // per layer: device pointers of the tiled matrices, norms and KV caches (a table in device memory,

@@ -214,6 +214,51 @@ __global__ void __launch_bounds__(LF_NTH) k_layer_front(front_args f) {
 #undef LF_STAMP
 }
 
+// ---- attention + attn-out in ONE launch (the decode step's K2 + K3; src/gemma_model.cpp:454-497,
+// :723) ------------------------------------------------------------------------------------------
+// The per-head attention launch has 8*H*S workgroups of which only one in eight works: the G*S
+// workgroups of a kv head share one XCD (its L2 serves their K / V rows), the other seven of every
+// octet return at once.  Here those seven run attn-out's row tiles (rr_tiles: weights issued first,
+// then the wait, then the attention's Q8_0 image by sc1 loads, rr rounds, + residual), so attn-out's
+// weight stream and launch ramp overlap the attention instead of following it, and one kernel
+// boundary per layer disappears.  Same operands, same fmaf chains: bit-identical to the two launches.
+// Hand-off (MI355X_MICROARCH sc1 table row 1): each attention workgroup stores its image blocks sc1,
+// drains vmcnt, barriers, then adds 1 to each of the 8 counter replicas; consumer c polls replica
+// c % 8 for H*S.  Reset without a memset node: every consumer adds 1 to `done` after its poll, and
+// the one that completes it subtracts the targets (order-free: a replica increment still in flight
+// nets to zero; nobody polls any more).  Dispatch: the attention workgroups of a kv head have the
+// lowest block index of their XCD's share and never wait, so the waiters cannot starve them; the
+// launcher caps the grid at one workgroup per CU.
+constexpr int AO_DONE = LF_NREP;  // counter slot of the consumers' done count
+template <int WT>
+__global__ void __launch_bounds__(LF_NTH) k_attn_o(attn_o_args f) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int b = blockIdx.x, S = f.t.dsplit, H = f.t.H, G = H / f.t.Hkv;
+    const int hs = b >> 3, h = hs / S, sp = hs % S, att = (h / G) & 7, j = b & 7;
+    if (j == att) {  // the attention of (head h, dims split sp), exactly k_attn_head's body
+        attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false, true>(f.t, h, smem, nullptr, sp);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's image stores have landed
+        __syncthreads();
+        if (threadIdx.x < LF_NREP) add_cnt(f.cnt + threadIdx.x * LF_CS);
+        return;
+    }
+    const int nc = (int)(gridDim.x >> 3) * 7;        // consumers (launcher: nc <= n_rt <= 2 nc)
+    const int c = hs * 7 + (j < att ? j : j - 1);   // this consumer's index
+    const int no = (int)f.o.n_rt, P = H * S;
+    rr_tiles<WT, PRO_IMG, EPI_ADD, true>(f.o, c, c + nc < no ? c + nc : -1, smem, f.cnt + (c & (LF_NREP - 1)) * LF_CS,
+                                         (unsigned)P, f.err);
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add((gu32_t *)(f.cnt + AO_DONE * LF_CS), 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        if (old == (unsigned)nc - 1) {  // every consumer is past its poll: return the counters to zero
+            for (int r = 0; r < LF_NREP; ++r)
+                __hip_atomic_fetch_sub((gu32_t *)(f.cnt + r * LF_CS), (unsigned)P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_sub((gu32_t *)(f.cnt + AO_DONE * LF_CS), (unsigned)nc, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 }  // namespace
 
 static int cu_count() {
@@ -263,6 +308,46 @@ int launch_layer_front(int wtype, const front_args &f, hipStream_t s) {
     front_args la = f;
     void *args[] = {(void *)&la};
     GHIP_CHECK(hipLaunchKernel(fn, dim3(grid), dim3(LF_NTH), args, lds, s));
+    return 0;
+}
+
+}  // namespace ghip
+
+namespace ghip {
+
+bool attn_o_supported(int wtype, const attn_args &t, const mv_args &o) {
+    if (wtype != T_Q4_0 && wtype != T_Q8_0) return false;
+    const int64_t nbt = wtype == T_Q4_0 ? 8 : 4;
+    // rr_tiles: one round per row tile (K = 8 block tiles), the image within 2 items per thread
+    if (o.n_bt != 8 || o.nb != 8 * nbt || o.nb % 4 || o.nb * 2 + o.nb / 4 > 2 * LF_NTH) return false;
+    if (t.mode != ATTN_PER_HEAD || t.spread || t.v_lds || !t.out_act || !t.out_da || !t.rope_cur || t.out_q8k) return false;
+    if (t.hd % 32 || t.hd > 256 || t.ctx % 32 || t.H % t.Hkv || t.dsplit < 1 || t.hd % (32 * t.dsplit) ||
+        4 * (t.hd / t.dsplit) > AH_THREADS)
+        return false;
+    // one workgroup per CU for the whole grid (nobody waits for a CU), every consumer 1 or 2 tiles
+    const int64_t grid = 8LL * t.H * t.dsplit, nc = grid / 8 * 7;
+    return grid <= cu_count() && o.n_rt >= nc && o.n_rt <= 2 * nc;
+}
+
+int launch_attn_o(int wtype, const attn_o_args &f, hipStream_t s) {
+    if (!attn_o_supported(wtype, f.t, f.o) || !f.cnt || !f.err) {
+        set_error("attn_o: unsupported shape");
+        return -1;
+    }
+    const size_t lds_mv = wtype == T_Q4_0
+                              ? ((make_lds_map<T_Q4_0, true>(1, 8, 8, 0).total + 15) & ~(size_t)15) + 2 * rr_geom<T_Q4_0>::SLOT
+                              : ((make_lds_map<T_Q8_0, true>(1, 8, 8, 0).total + 15) & ~(size_t)15) + 2 * rr_geom<T_Q8_0>::SLOT;
+    const size_t lds_att = ((2 * (size_t)f.t.hd * 2 + 15) & ~(size_t)15) + (size_t)f.t.ctx * 6 + 16;
+    const size_t lds = lds_mv > lds_att ? lds_mv : lds_att;
+    if (lds > 160 * 1024) {
+        set_error("attn_o: context too long for the LDS image");
+        return -1;
+    }
+    const void *fn = wtype == T_Q4_0 ? (const void *)k_attn_o<T_Q4_0> : (const void *)k_attn_o<T_Q8_0>;
+    if (lds > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attn_o_args la = f;
+    void *args[] = {(void *)&la};
+    GHIP_CHECK(hipLaunchKernel(fn, dim3(8 * f.t.H * f.t.dsplit), dim3(LF_NTH), args, lds, s));
     return 0;
 }
 

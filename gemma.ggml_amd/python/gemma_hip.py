@@ -10,8 +10,14 @@ import subprocess
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# GHIP_LIB: an alternative build of the same library (A/B timing of two builds on one box)
-LIB_PATH = os.environ.get("GHIP_LIB") or os.path.join(PKG_DIR, "lib", "libgemma_hip.so")
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libgemma_hip.so")
+# GHIP_LIB: an alternative build of the same library, for A/B timing of two builds on one box
+# (scripts/lib_ab.sh).  Honoured only with GHIP_ALLOW_ALT_LIB=1, so a stray variable can never make
+# a test, smoke() or bench.py load anything but the in-tree build.
+if os.environ.get("GHIP_LIB"):
+    if os.environ.get("GHIP_ALLOW_ALT_LIB") != "1":
+        raise RuntimeError("GHIP_LIB is set but GHIP_ALLOW_ALT_LIB=1 is not: refusing to load a non-tree library")
+    LIB_PATH = os.environ["GHIP_LIB"]
 
 GGML_TYPE_F32, GGML_TYPE_F16, GGML_TYPE_Q4_0, GGML_TYPE_Q8_0 = 0, 1, 2, 8
 GGML_TYPE_Q4_K, GGML_TYPE_Q6_K, GGML_TYPE_Q8_K = 12, 14, 15
@@ -23,7 +29,7 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact", "gemma_kq_time", "hpc_graph_compute",
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
-           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs",
+           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_att_o", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs",
            "gemma_tp_unique_id", "gemma_engine_create_tp", "gemma_engine_tp_info", "gemma_engine_set_persist_timeout",
            "gguf_init_from_file", "gguf_free", "gguf_get_n_kv", "gguf_get_key", "gguf_get_kv_type",
            "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
@@ -111,6 +117,7 @@ def lib():
     L.gemma_engine_plan.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     L.gemma_engine_set_plan.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     L.gemma_engine_set_fuse.argtypes = [vp, C.c_int]
+    L.gemma_engine_set_att_o.argtypes = [vp, C.c_int]
     L.gemma_engine_set_persist.argtypes = [vp, C.c_int]
     L.gemma_engine_persist_err.argtypes = [vp, vp, C.c_int]
     L.gemma_engine_set_persist_timeout.argtypes = [vp, C.c_uint]
@@ -246,6 +253,10 @@ class Engine:
         self._chk(self.L.gemma_engine_step(self.h, n, _p(lg) if want_logits else None, 1 if use_graph else 0), "step")
         return lg
 
+    def sync(self):
+        """wait for the engine's stream"""
+        self._chk(self.L.gemma_engine_sync(self.h), "sync")
+
     def tokens(self):
         out = np.zeros(self.cfg.n_ctx + 1, dtype=np.int32)
         n = self.L.gemma_engine_tokens(self.h, _p(out), len(out))
@@ -307,6 +318,10 @@ class Engine:
         """fused layer front on (1) / off (0) / unchanged (-1); returns the sticky hand-off timeout
         word (0 = every in-launch hand-off completed in time)"""
         return self.L.gemma_engine_set_fuse(self.h, front)
+
+    def set_att_o(self, on=-1):
+        """decode attention + attn-out in one launch per layer: on 1 / off 0 / keep -1; returns the setting"""
+        return self.L.gemma_engine_set_att_o(self.h, on) == 1
 
     def set_persist(self, on=-1):
         """The decode step's layers as one persistent launch (token.hip): on 1/0, -1 keep; returns

@@ -119,6 +119,11 @@ int gemma_engine_tune(gemma_engine *e, int iters);
 int gemma_engine_plan(gemma_engine *e, int *out, int cap);
 int gemma_engine_set_plan(gemma_engine *e, const int *in, int n);
 int gemma_engine_set_fuse(gemma_engine *e, int fuse_front); /* fused layer front on/off (-1 = keep); returns the hand-off timeout word */
+/* the decode attention and attn-out (+ residual) in ONE launch per layer (k_attn_o: the attention
+   launch's idle workgroups run attn-out's row tiles after an in-launch hand-off; same bits): on 1 /
+   off 0 / keep -1; returns the setting.  A hand-off timeout is reported by gemma_engine_step (-1) and
+   turns it off. */
+int gemma_engine_set_att_o(gemma_engine *e, int on);
 int gemma_engine_graph_kernels(gemma_engine *e);            /* kernel launches per decode token (captured graph) */
 /* the decode step's layers as ONE persistent launch (opt-in: off by default, GHIP_PERSIST=1 or this
  * call; -1 = keep): returns 1 when it runs this engine's steps, 0 when not (hpc_last_error says why:

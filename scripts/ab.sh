@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # Same-box A/B of two builds of libgemma_hip.so (ab_libs/libA.so vs libB.so): alternating bench
 # runs, decode step time + kernel times.  Usage: bash scripts/ab.sh [extra bench args]
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # attention prefetch-depth experiment: stamps of layer 9 and bench step time for each build
 set -o pipefail
 mkdir -p gpurun_out/ab

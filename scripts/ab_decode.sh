@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # Same-box A/B of decode builds ab_libs/lib<v>.so: alternating bench runs (no CPU/prefill/TP legs),
 # decode tok/s + per-kernel µs.  usage: bash scripts/ab_decode.sh v1 v2 ... [-- extra bench args]
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # Same-box A/B of exact-prefill builds: ab_libs/lib<v>.so for each v given; per-pass prefill ms.
 # usage: bash scripts/ab_prefill.sh v1 v2 ...
 set -o pipefail

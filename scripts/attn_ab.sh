@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # decode step time per build (bench decode leg only), 2 interleaved reps: attention variants differ
 # by 18 x their attention time.  usage: bash scripts/attn_ab.sh <tag> <variant...>
 # ("new" = in-tree, else ab_libs/lib<v>.so)

@@ -13,6 +13,10 @@ rocprofv3 kernel trace of graph replays once crashed inside the runtime (DESIGN.
 import os
 import sys
 
+if os.environ.get("TORCH_FIRST", "0") == "1":
+    # torch's bundled HIP runtime (libamdhip64.so.7 of torch/lib, the one bench.py and the tests run on,
+    # since they import torch first) instead of /opt/rocm's: the dynamic linker reuses the loaded soname
+    import torch  # noqa: F401
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gemma.ggml_amd", "python"))
 sys.path.insert(0, ROOT)
@@ -26,8 +30,13 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     graph = os.environ.get("GHIP_PROF_GRAPH", "0") == "1"
     e = G.Engine(GEMMA_2B, n_ctx=512, device=0)
+    if os.environ.get("PROF_MAPS"):  # the process's mappings (symbolizes a native crash exactly)
+        with open("/proc/self/maps") as f, open(os.environ["PROF_MAPS"], "w") as g:
+            g.write(f.read())
     v = [int(t) for t in os.environ.get("PLAN", BENCH_R04_PLAN).split(",")]
     e.set_plan({k: (v[3 * i], v[3 * i + 1], v[3 * i + 2]) for i, k in enumerate(e.PLAN_CLASSES)})
+    if os.environ.get("ATT_O"):
+        e.set_att_o(int(os.environ["ATT_O"]))
     prompt = make_prompt(128, GEMMA_2B["n_vocab"])
     e.begin(prompt)
     e.step(len(prompt) + steps, use_graph=graph)

@@ -1,25 +1,44 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, attention phase stamps, bench line, rocprofv3 kernel stats.
-# usage (from the repo root, on the GPU box): bash scripts/gpu_check.sh [tag] [what]
-# (stamp / steps need the stamps build first, here: bash scripts/build_variant.sh stamps \
-#  matvec_ks1.hip,matvec_ks2.hip,matvec_ks4.hip,matvec_ks8.hip,ops.hip,engine.cpp -DGHIP_STAMPS=1)
-#   what: any of "tests stamp bench prof" (default: all)
+# One GPU-box pass, in modes (run from the repo root on the GPU box; every GPU step under its own
+# time limit, the script stops at the first failure):
+#   bash scripts/gpu_check.sh TAG "MODE ..."
+#   tests      pytest -m gpu (thread timeouts, so a hang names its test)
+#   bench      python bench.py (the driver's line)
+#   prof       the bench under rocprofv3 --kernel-trace --stats (csv kernel stats)
+#   profgraph  the fixed-plan decode (scripts/decode_prof.py) as hipGraph replays under rocprofv3
+#              --kernel-trace --stats -> decode_kernels_graph.md (per-class table of the benched path)
+#   pmcprefill the exact T = 2048 prefill under two SQ --pmc passes -> pmc_prefill_q4_0.json
+#   pmc        FETCH_SIZE / WRITE_SIZE passes over scripts/pmc_probe.py (decode matvec traffic)
+#   stamp / steps  attention / step phase stamps (needs the stamps build in ab_libs/, which
+#              .gpurunignore leaves out by default: remove that line for such a run)
 set -o pipefail
 TAG=${1:-run}
-WHAT=${2:-"tests stamp bench prof"}
+WHAT=${2:-"tests bench prof"}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+PLAN=${PLAN:-"9,1,0,9,1,0,1,1,0,9,1,1,1,8,0"}
 for w in $WHAT; do
+  echo "== $w $(date +%T)"
   case $w in
-    tests) timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; } ; tail -2 $OUT/pytest_gpu.log ;;
-    stamp) GHIP_LIB=ab_libs/libstamps.so timeout -k 10 120 python tests/stamp_attn.py 0 > $OUT/stamp.log 2>&1 && GHIP_LIB=ab_libs/libstamps.so timeout -k 10 120 python tests/stamp_attn.py 1 >> $OUT/stamp.log 2>&1 || { cat $OUT/stamp.log; exit 1; } ; cat $OUT/stamp.log ;;
-    steps) GHIP_LIB=ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 9 > $OUT/stamp_step.log 2>&1 && GHIP_LIB=ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 17 >> $OUT/stamp_step.log 2>&1 || { cat $OUT/stamp_step.log; exit 1; } ; cat $OUT/stamp_step.log ;;
-    bench) timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
-    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu --steps 32 > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; } ;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; } ; tail -2 $OUT/pytest_gpu.log ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; } ; cat $OUT/smoke.log ;;
+    bench) timeout -k 10 500 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
+    prof) timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu --steps 32 > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; } ;
           find $OUT/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/kernel_stats.csv ; head -12 $OUT/kernel_stats.csv | cut -c1-200 ;;
+    profgraph) TORCH_FIRST=${TORCH_FIRST:-1} PROF_MAPS=$OUT/maps_profg.txt GHIP_PROF_GRAPH=1 PLAN=$PLAN timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profg -o run -- python3 scripts/decode_prof.py 48 > $OUT/profg.log 2>&1 || { tail -40 $OUT/profg.log; exit 1; } ;
+          python3 scripts/decode_classes.py $(find $OUT/profg -name "run_kernel_trace.csv" | head -1) 128 48 "$PLAN (hipGraph replay)" > $OUT/decode_kernels_graph.md && cat $OUT/decode_kernels_graph.md ;;
+    pmcprefill) bash scripts/pmc_prefill.sh $TAG/pmcp 2048 q4_0 > $OUT/pmcp.log 2>&1 || { tail -20 $OUT/pmcp.log; exit 1; } ; tail -20 $OUT/pmcp.log ;;
     pmc) timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_size -o run -- python3 scripts/pmc_probe.py > $OUT/pmc1.log 2>&1 || { tail -20 $OUT/pmc1.log; exit 1; } ;
          timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_size -o run -- python3 scripts/pmc_probe.py > $OUT/pmc2.log 2>&1 || { tail -20 $OUT/pmc2.log; exit 1; } ;
          ls -R $OUT/pmc_fetch_size | head -20 ;;
+    stamp) export GHIP_ALLOW_ALT_LIB=1; GHIP_LIB=ab_libs/libstamps.so timeout -k 10 120 python tests/stamp_attn.py 0 > $OUT/stamp.log 2>&1 && GHIP_LIB=ab_libs/libstamps.so timeout -k 10 120 python tests/stamp_attn.py 1 >> $OUT/stamp.log 2>&1 || { cat $OUT/stamp.log; exit 1; } ; cat $OUT/stamp.log ;;
+    steps) export GHIP_ALLOW_ALT_LIB=1; GHIP_LIB=ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 9 > $OUT/stamp_step.log 2>&1 && GHIP_LIB=ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 17 >> $OUT/stamp_step.log 2>&1 || { cat $OUT/stamp_step.log; exit 1; } ; cat $OUT/stamp_step.log ;;
+    attoab) timeout -k 10 300 python scripts/att_o_ab.py 3 64 > $OUT/att_o_ab.log 2>&1 || { tail -20 $OUT/att_o_ab.log; exit 1; } ; cat $OUT/att_o_ab.log ;;
+    gputest) timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_sel.log 2>&1 || { tail -40 $OUT/pytest_sel.log; exit 1; } ; tail -15 $OUT/pytest_sel.log ;;
+    # the graph-replay trace on /opt/rocm's HIP runtime (no torch): the configuration that crashed in
+    # rounds 4-6; its mappings are kept so the frames resolve exactly.  LAST in a call: a crash ends it.
+    crashrepro) TORCH_FIRST=0 PROF_MAPS=$OUT/maps_crash.txt GHIP_PROF_GRAPH=1 PLAN=$PLAN timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc -o run -- python3 scripts/decode_prof.py 48 > $OUT/profc.log 2>&1; echo "crashrepro rc=$?"; tail -40 $OUT/profc.log; exit 0 ;;
+    *) echo "unknown mode $w"; exit 2 ;;
   esac
 done

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # Q8_K quantizer with DPP reductions (ab_libs/libdpp.so) vs the in-tree build: K-quant parity tests
 # under the variant, then Q4_K_M decode interleaved
 set -o pipefail

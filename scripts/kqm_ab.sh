@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # Q4_K_M decode A/B over (library, env) variants, interleaved (scripts/run_kqm.py at the bench's
 # positions): VARS="name=lib[:ENV=V,ENV2=V2] ..." (lib "new" = in-tree), REPS rounds
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # A/B of two builds on one box: ab_libs/libbase.so (GHIP_LIB) vs the in-tree library, decode bench
 # legs, interleaved; optional parity tests of the in-tree build first (TESTS="-k ...")
 set -o pipefail

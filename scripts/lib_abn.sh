@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # A/B/... of several builds on one box: LIBS="base nochk new" (ab_libs/lib<name>.so via GHIP_LIB;
 # "new" = the in-tree library), decode bench legs, interleaved, REPS rounds; per-class µs printed
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # T = 2048 exact prefill time per build (timing only, no parity: for ablation builds).
 # usage: bash scripts/pf_time_ab.sh <tag> <variant...>   ("new" = in-tree, else ab_libs/lib<v>.so)
 set -o pipefail

@@ -1,6 +1,6 @@
 """Phase stamps of the persistent token launch (token.hip), one decode step after a 128-token prompt.
 
-    GHIP_LIB=ab_libs/libstamps.so python scripts/token_stamps.py [layers-to-print]
+    GHIP_ALLOW_ALT_LIB=1 GHIP_LIB=ab_libs/libstamps.so python scripts/token_stamps.py [layers-to-print]
 (build: bash scripts/build_variant.sh stamps token.hip,engine.cpp -DGHIP_STAMPS=1)
 
 Stamp i of layer l (s_memrealtime, 100 MHz = 10 ns) per workgroup: 0 layer start, 1 x gathered,

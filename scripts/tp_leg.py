@@ -1,154 +1,107 @@
-"""Gemma-7B row-split decode leg of bench.py (BASELINE config 4): one process per GPU, weights
-row-split across WORLD_SIZE GPUs, RCCL all-gathers.  bench.py runs it as a child
-process of every rank with a time limit, so a collective that never completes cannot stall the
-bench line.  Rank 0 prints one JSON line.  usage: tp_leg.py <steps> <wtype q4_0|q8_0> <tune 0|1>
+"""Row-split decode leg of bench.py: one process per GPU, every weight matrix row-split
+across WORLD_SIZE GPUs, RCCL all-gathers inside the decode hipGraph.  bench.py runs it as a child
+process of every rank with a time limit, so a collective that never completes cannot stall the bench
+line.  Rank 0 prints one JSON line; a parity mismatch on any rank prints an error object and every
+rank exits 3.
 
-Synthetic Gemma-7B weights with the token_embd / output matrix at 0.25x its default std, so the
-greedy tokens follow the input instead of settling on one id.  SURVEY §8(d) suggests x4 for peaked
-logits, but the output is TIED to the embedding: the current token's own row rides the residual
-stream to the final norm and x4 turns the model into a copy model (every prompt row's argmax is its
-input token, the greedy sequence repeats the last prompt token; x1 settles on one id with a 1.2e-5
-margin).  Measured with scripts/out_gain_scan.py 7b: x4 / x1 / x0.5 / x0.25 / x0.125 give 1 / 1 / 5
-/ 10 / 10 distinct tokens in 16 greedy steps, margins 0.40 / 1.2e-5 / 3.3e-3 / 1.9e-3 / 1.2e-3.  The unsplit 1-GPU reference engine and the split engine under test get the same launch-plan
-treatment (both tuned, or both on the default plan), so at N = 1 the efficiency reads ~1.00."""
+usage: tp_leg.py <steps> <wtype q4_0|q8_0> <tune 0|1> [model 2b|7b] [warmup] [prompt]
+
+  2b  Gemma-2B (BASELINE config 2 row-split over N GPUs: the headline of `bench.py --gpus N`, N > 1),
+      the bench's synthetic weights and prompt
+  7b  Gemma-7B (BASELINE config 4), synthetic weights with the token_embd / output matrix at 0.25x
+      its default std, so the greedy tokens follow the input instead of settling on one id.  SURVEY
+      §8(d) suggests x4 for peaked logits, but the output is TIED to the embedding: the current
+      token's own row rides the residual stream to the final norm and x4 turns the model into a copy
+      model (every prompt row's argmax is its input token; x1 settles on one id with a 1.2e-5
+      margin).  Measured with scripts/out_gain_scan.py 7b: x4 / x1 / x0.5 / x0.25 / x0.125 give 1 /
+      1 / 5 / 10 / 10 distinct tokens in 16 greedy steps, margins 0.40 / 1.2e-5 / 3.3e-3 / 1.9e-3 /
+      1.2e-3.
+
+The control flow (RCCL id broadcast, lockstep tuning with rank 0's plan broadcast, the unsplit-engine
+hash check, max-over-ranks timing) is gemma_tp.run_stream; tests/test_tp_control.py drives it with a
+stub engine over gloo.  The unsplit 1-GPU engine and the split engine get the same launch-plan
+treatment (both tuned, or both on the default plan), so at N = 1 the ratio reads ~1.00."""
 import json
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gemma.ggml_amd", "python"))
 sys.path.insert(0, ROOT)
 
+# per class: kernel id of gemma_engine_time -> name, launches per token
+KERNELS = {0: ("ffn gate/up matvec (+norm, +gelu*mul)", "n_layer"), 1: ("ffn down matvec (+resid)", "n_layer"),
+           2: ("qkv matvec (+norm)", "n_layer"), 3: ("attn-out matvec (+resid)", "n_layer"),
+           4: ("logits matvec (+argmax)", 1)}
 
-def main():
-    steps, wtype_s, tune = int(sys.argv[1]), sys.argv[2], sys.argv[3] == "1"
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
 
-    import gemma_hip as G
-    from bench import GEMMA_7B, make_prompt
-    wtype = G.GGML_TYPE_Q4_0 if wtype_s == "q4_0" else G.GGML_TYPE_Q8_0
-    if world > 1:
-        dist.init_process_group(backend="gloo", init_method="env://")
+def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None):
+    argv = sys.argv[1:] if argv is None else argv
+    steps, wtype_s, tune = int(argv[0]), argv[1], argv[2] == "1"
+    model = argv[3] if len(argv) > 3 else "7b"
+    warmup = int(argv[4]) if len(argv) > 4 else 4
+    n_prompt = int(argv[5]) if len(argv) > 5 else 16
+    import gemma_tp as T
+    from bench import GEMMA_2B, GEMMA_7B, HBM_PEAK_GBS, make_prompt
+    shape = GEMMA_2B if model == "2b" else GEMMA_7B
+    out_gain = 0.0 if model == "2b" else 0.25
+    comm = comm or T.Comm.from_env("gloo")
+    if make_engine is None:  # the product: the HIP engine on this rank's GPU
+        import torch
 
-    def new_id():
-        """A fresh RCCL unique id for ONE communicator (an id serves a single ncclCommInitRank round:
-        its bootstrap root leaves once every rank has joined, so a second init on it fails with
-        "remote process exited").  N > 1: rank 0 makes it and broadcasts it over gloo."""
-        if world == 1:
-            return G.tp_unique_id()
-        idt = torch.zeros(256, dtype=torch.uint8)
-        if rank == 0:
-            raw = G.tp_unique_id()
-            idt[: len(raw)] = torch.tensor(list(raw), dtype=torch.uint8)
-        dist.broadcast(idt, 0)
-        return bytes(idt.numpy())
+        import gemma_hip as G
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        wtype = G.GGML_TYPE_Q4_0 if wtype_s == "q4_0" else G.GGML_TYPE_Q8_0
+        n_ctx = ((n_prompt + warmup + steps + 64) // 32 + 1) * 32
 
-    def sync():
-        torch.cuda.synchronize(local_rank)
-        if world > 1:
-            dist.barrier()
-
-    import hashlib
-
-    import numpy as np
-    n_check, prompt = 20, make_prompt(16, GEMMA_7B["n_vocab"])
-    OUT_GAIN = 0.25
-
-    def row_hashes(lg):
-        return np.frombuffer(b"".join(hashlib.sha1(r.tobytes()).digest()[:8] for r in lg), dtype=np.uint8).copy()
-
-    # reference (rank 0): the UNSPLIT engine on one GPU, same synthetic weights and prompt; the first
-    # 16 rows are the prompt positions (teacher-forced, so they vary with the input tokens), then 4
-    # greedy steps.  Its logits hashes are broadcast; every rank compares its own gathered logits.
-    # At N = 1 the split under test is 8 virtual ranks on one GPU (the same shards and key merge).
-    ref = torch.zeros(n_check * 8, dtype=torch.uint8)
-    tok_s_1 = None
-    margin = None
-    if rank == 0:
-        re_ = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, out_gain=OUT_GAIN)
-        re_.begin(prompt)
-        lg = re_.step(n_check, want_logits=True, use_graph=True)
-        ref = torch.from_numpy(row_hashes(lg))
-        top2 = np.sort(lg, axis=1)[:, -2:]
-        margin = float(np.min((top2[:, 1] - top2[:, 0]) / np.maximum(np.abs(top2[:, 1]), 1e-30)))
-        ref_tokens = [int(t) for t in re_.tokens()[16:24]]
-        plan_1 = re_.tune(6) if tune else re_.plan()
-        re_.begin(prompt)
-        re_.step(16 + 4, use_graph=True)
-        re_.L.gemma_engine_sync(re_.h)
-        t1 = time.perf_counter()
-        re_.step(steps, use_graph=True)
-        re_.L.gemma_engine_sync(re_.h)
-        tok_s_1 = steps / (time.perf_counter() - t1)
-        re_.close()
-    if world > 1:
-        dist.broadcast(ref, 0)
-    # checked: the RCCL ranks (N > 1) or, at N = 1, 8 virtual ranks AND a 1-rank RCCL engine (so the
-    # timed engine below runs the transport); every communicator gets its own id
-    splits = [(world, rank, "rccl")] if world > 1 else [(8, 0, None), (1, 0, "rccl")]
-    nbad = 0
-    for split in splits:
-        if split[2] == "rccl":
-            split = (split[0], split[1], new_id())
-        ce = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=split, out_gain=OUT_GAIN)
-        ce.begin(prompt)
-        got = row_hashes(ce.step(n_check, want_logits=True, use_graph=True))
-        ce.close()
-        nbad += int(np.sum(got.reshape(n_check, 8) != ref.numpy().reshape(n_check, 8), axis=1).astype(bool).sum())
-    bad = torch.tensor([nbad])
-    if world > 1:
-        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
-    if int(bad.item()) != 0:
-        if rank == 0:
-            print(json.dumps({"error": f"row-split logits differ from the unsplit engine: {int(bad.item())} rows over all ranks"}), flush=True)
-        sys.exit(3)
-
-    te = G.Engine(GEMMA_7B, n_ctx=256, wtype=wtype, device=local_rank, tp=(world, rank, new_id()), out_gain=OUT_GAIN)
-    plan = te.tune(6) if tune else te.plan()
-    te.begin(prompt)
-    te.step(16 + 4, use_graph=True)
-    sync()
-    t0 = time.perf_counter()
-    te.step(steps, use_graph=True)
-    te.L.gemma_engine_sync(te.h)
-    sync()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    toks = list(te.tokens())
-    te.close()
-    if rank == 0:
-        tok_s = steps / dt
-        print(json.dumps({"model": "Gemma-7B " + wtype_s.upper(), "ranks": world, "tok_s": round(tok_s, 2),
-                          "ms_per_token": round(dt / steps * 1e3, 4), "steps": steps,
-                          "parallelism": f"row-split tp{world} (RCCL all-gather x4/layer)" if world > 1
-                          else "1 GPU, 1-rank RCCL communicator (every gather through ncclAllGather in the hipGraph)",
-                          "tok_s_unsplit_1gpu": round(tok_s_1, 2),
-                          # scaling fields only where ranks > 1; at N = 1 the ratio is the 1-rank RCCL
-                          # communicator's overhead against the unsplit engine
-                          "speedup_vs_1gpu": round(tok_s / tok_s_1, 3) if world > 1 else None,
-                          "strong_scaling_efficiency": round(tok_s / tok_s_1 / world, 3) if world > 1 else None,
-                          "rccl_overhead_vs_unsplit": round(tok_s / tok_s_1, 3) if world == 1 else None,
-                          "parity_check": {"rows": n_check, "mismatched_rows_all_ranks": 0,
-                                           "reference": "unsplit 1-GPU engine (rank 0), logits sha1 per row",
-                                           "split_checked": f"{world} RCCL ranks" if world > 1
-                                           else "8 virtual ranks + the 1-rank RCCL engine",
-                                           "min_top1_top2_rel_margin": round(margin, 6)},
-                          "tokens_head": [int(t) for t in toks[16:24]], "tokens_head_unsplit": ref_tokens,
-                          "distinct_tokens_head": len(set(int(t) for t in toks[16:24])),
-                          "synthetic_output_gain": OUT_GAIN, "launch_plan": plan, "launch_plan_unsplit": plan_1,
-                          "plans": "both tuned" if tune else "both default"}), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        def make_engine(tp):
+            return G.Engine(shape, n_ctx=max(256, n_ctx), wtype=wtype, device=local_rank, tp=tp, out_gain=out_gain)
+        make_id = G.tp_unique_id
+        device_sync = lambda: torch.cuda.synchronize(local_rank)  # noqa: E731
+    prompt = make_prompt(n_prompt, shape["n_vocab"])
+    try:
+        r = T.run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=tune,
+                         check_prompt=make_prompt(16, shape["n_vocab"]), device_sync=device_sync or (lambda: None),
+                         kernel_iters=30 if model == "2b" else 0)
+    except T.ParityError as ex:
+        if comm.rank == 0:
+            print(json.dumps({"error": str(ex)}), flush=True)
+        comm.close()
+        return T.EXIT_PARITY
+    if comm.rank == 0:
+        world, tok_s, tok_s_1 = comm.world, r["tok_s"], r["tok_s_unsplit_1gpu"]
+        toks = r["tokens"][n_prompt:n_prompt + 8]
+        line = {"model": f"Gemma-{model.upper()} {wtype_s.upper()}", "ranks": world, "tok_s": round(tok_s, 2),
+                "ms_per_token": round(r["ms_per_token"], 4), "steps": steps, "warmup": warmup, "prompt": n_prompt,
+                "timed_s": round(r["timed_s"], 6),
+                "parallelism": f"row-split tp{world} (RCCL all-gather x4/layer)" if world > 1
+                else "1 GPU, 1-rank RCCL communicator (every gather through ncclAllGather in the hipGraph)",
+                "tok_s_unsplit_1gpu": round(tok_s_1, 2) if tok_s_1 else None,
+                # scaling fields only where ranks > 1; at N = 1 the ratio is the 1-rank RCCL
+                # communicator's overhead against the unsplit engine
+                "speedup_vs_1gpu": round(tok_s / tok_s_1, 3) if world > 1 and tok_s_1 else None,
+                "strong_scaling_efficiency": round(tok_s / tok_s_1 / world, 3) if world > 1 and tok_s_1 else None,
+                "rccl_overhead_vs_unsplit": round(tok_s / tok_s_1, 3) if world == 1 and tok_s_1 else None,
+                "parity_check": r["parity_check"], "tokens_head": toks,
+                "distinct_tokens_head": len(set(toks)), "synthetic_output_gain": out_gain or None,
+                "launch_plan": r["launch_plan"], "launch_plan_unsplit": r["launch_plan_unsplit"],
+                "plans": ("both tuned; every rank runs rank 0's plan" if tune else "both default")}
+        if r["kernels"]:  # per-N roofline: rank 0's shard kernels timed alone (hipEvents)
+            cls = {}
+            for k, (us, algo) in r["kernels"].items():
+                name, calls = KERNELS[k]
+                gbs = algo / (us * 1e-6) / 1e9
+                cls[name] = {"avg_us": round(us, 3), "algo_bytes": int(algo), "GB/s": round(gbs, 1),
+                             "frac": round(gbs / HBM_PEAK_GBS, 4),
+                             "launches_per_token": shape["n_layer"] if calls == "n_layer" else calls}
+            dom = max(cls, key=lambda n: cls[n]["avg_us"] * cls[n]["launches_per_token"])
+            line["roofline"] = dict(bound="hbm", kernel=dom, achieved=cls[dom]["GB/s"], peak=HBM_PEAK_GBS, unit="GB/s",
+                                    frac=cls[dom]["frac"], avg_us=cls[dom]["avg_us"], algo_bytes=cls[dom]["algo_bytes"],
+                                    per="rank 0's row shard (1/N of every matrix's rows)", classes=cls)
+        print(json.dumps(line), flush=True)
+    comm.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # decode bench: in-tree build vs ab_libs/lib<v>.so variants, interleaved (usage: bash scripts/var_ab.sh v1 v2 ...)
 set -o pipefail
 mkdir -p gpurun_out/varab

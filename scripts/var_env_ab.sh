@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # Interleaved decode-bench A/B over (library, env) variants: VARS="name=lib[:ENV=V,ENV2=V2] ..."
 # (lib "new" = the in-tree build, else ab_libs/lib<lib>.so); REPS rounds; per-class µs printed
 set -o pipefail

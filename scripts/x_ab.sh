@@ -1,4 +1,5 @@
 #!/bin/bash
+export GHIP_ALLOW_ALT_LIB=1  # the A/B libraries are loaded on purpose (gemma_hip.py refuses GHIP_LIB otherwise)
 # exact Q4_0 prefill GEMM tile variants: parity (exact prefill tests) and T = 2048 prefill time per
 # build.  usage: bash scripts/x_ab.sh <tag> <variant...>   (variant "new" = the in-tree library,
 # others ab_libs/lib<variant>.so from scripts/build_variant.sh)

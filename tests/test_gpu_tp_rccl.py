@@ -112,3 +112,24 @@ def test_bench_tp_leg_runs_at_one_gpu():
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert "error" not in line, line
     assert line["parity_check"]["mismatched_rows_all_ranks"] == 0 and line["tok_s"] > 0
+
+
+@gpu
+def test_bench_tp_leg_2b_headline_at_one_gpu():
+    """The N > 1 headline leg (Gemma-2B row-split, scripts/tp_leg.py 2b) end to end at N = 1 with the
+    bench's prompt length: parity vs the unsplit engine (8 virtual ranks + a 1-rank RCCL engine),
+    rank 0's tuned plan installed, the timed 1-rank RCCL stream and its per-shard roofline."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "tp_leg.py"), "8", "q4_0", "1", "2b", "2", "128"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "error" not in line, line
+    assert line["parity_check"]["mismatched_rows_all_ranks"] == 0 and line["tok_s"] > 0
+    assert line["steps"] == 8 and line["warmup"] == 2 and line["prompt"] == 128
+    assert line["roofline"]["classes"] and line["roofline"]["avg_us"] > 0
