@@ -53,7 +53,6 @@ constexpr int ATT_QUADS = ATT_THREADS / 4;  // one KQ (position, head) or KQV (d
 constexpr int ATT_VW = 256;                 // V positions staged in LDS per dimension row (n_kv <= 256)
 constexpr int ATT_STG = 2;                  // staging uint4 per thread for each of K and V
 constexpr int ATT_MAXWG = 256;              // co-resident workgroups (in-kernel hand-off)
-constexpr int ATT_VDMA_PITCH = 576;         // bytes per V row in the per-head form's LDS copy
 
 // ggml_vec_dot_f16 with accumulator row j = t4 held by lane t4 of a quad: fold the
 // quad exactly as sum0+=sum2, sum1+=sum3, sum0+=sum1 (xor-2 then xor-1), then halves and hadds.
@@ -201,21 +200,11 @@ constexpr int AH_THREADS = 1024;  // per-head form: 256 quads = 256 KQ positions
 constexpr int AH_KPF = GHIP_AH_KPF;  // K steps (of 32 elements) prefetched per lane: hd <= 256
 constexpr int AH_VPF = GHIP_AH_VPF;  // V steps (of 32 positions) prefetched per lane: n_kv <= 256
 
-#ifndef GHIP_AH_TRIM
-#define GHIP_AH_TRIM 0  // 1: no dead V load instructions (wave-uniform skips) — measured 0.3 % slower
-#endif
 #ifndef GHIP_AH_SPOS
 #define GHIP_AH_SPOS 1  // the position by a scalar load, the wave index uniform (readfirstlane)
 #endif
-#ifndef GHIP_AH_RW
-#define GHIP_AH_RW 0  // 1: the last wave does the RoPE, its prefetch after it (measured ~1 % slower)
-#endif
-#ifndef GHIP_AH_VEARLY
-#define GHIP_AH_VEARLY 0  // 1 (with VPF 0): V loads after the K dots (spills at 1024 threads: slower)
-#endif
-#ifndef GHIP_AH_KTRIM
-#define GHIP_AH_KTRIM 0
-#endif
+// (measured slower and removed, DESIGN.md §10: dead-load trims of the V / K prefetch, the RoPE on the
+// last wave with its prefetch after it, V loads issued after the K dots)
 #ifndef GHIP_AH_ABL
 #define GHIP_AH_ABL 0  // timing ablations only (wrong results): 1 every K load reads row 0, 2 no KQ dots,
                        // 4 no KQ phase at all, 8 no KQV dots, 16 KQ dots over 4 of 8 steps
@@ -262,43 +251,16 @@ __device__ __forceinline__ void attn_prefetch(const attn_args &a, const int h, a
 #else
     p.pos_v = ((const int *)a.rope_cur)[hd];
 #endif
-    // GHIP_AH_KTRIM: the position by a scalar load first (its own counter: the RoPE loads already
-    // in flight are not waited for), then K rows only for the waves whose positions lie below n_kv
-    bool kload = true;
-    if (GHIP_AH_KTRIM) {
-        const int ps = *((const __attribute__((address_space(4))) int *)a.rope_cur + hd);
-        const int nk = 32 * (ps / 32 + 1);
-        kload = (quad & ~15) < (nk < a.ctx ? nk : a.ctx);
-    }
-    if (kload) {
+    {
         const int j = (GHIP_AH_ABL & 1) ? 0 : quad < a.ctx ? quad : 0;  // no dependency on pos: rows >= pos are masked
         const uint16_t *krow = a.kc + (int64_t)j * kvw + (int64_t)kvh * hd + t4 * 8;
 #pragma unroll
         for (int s = 0; s < KPF; ++s) p.k[s] = *(const uint4 *)(krow + (s * 32 < hd ? s * 32 : 0));
     }
-    if (a.v_lds) return;  // the V rows come by LDS-DMA (attn_vdma)
-    // only the waves whose quads own output dims load V (wave-uniform: quad & ~15 = 16 * wave);
-    // the others' loads were dead, and each costs the CU's load path its cycles
-    if (GHIP_AH_TRIM && d_lo + (quad & ~15) >= (hd < d_hi ? hd : d_hi)) return;
     const int d0 = d_lo + quad < (hd < d_hi ? hd : d_hi) ? d_lo + quad : d_lo;
     const uint16_t *vrow0 = a.vc + ((int64_t)kvh * hd + d0) * a.ctx;
 #pragma unroll
     for (int s = 0; s < VPF; ++s) p.v[s] = *(const uint4 *)(vrow0 + (s * 32 < a.ctx ? s * 32 : 0) + t4 * 8);
-}
-
-// The workgroup's V rows [d_lo, d_hi) x positions [0, min(ctx, 256)) into LDS by LDS-DMA (no
-// registers, no round trip at the KQV): row r at smem + a.v_lds + r * ATT_VDMA_PITCH, one wave
-// instruction per row (16 B per lane = 8 positions).  The pitch (512 + 64 B) puts the 16 quads of a
-// KQV read on distinct banks (quad q at dword 16q + 4 t4 mod 64).  Completion: each wave waits for
-// its own DMAs (vmcnt) before the barrier ahead of the KQV.
-__device__ __forceinline__ void attn_vdma(const attn_args &a, int kvh, int d_lo, int dsz, uint8_t *smem, int wave, int nwave,
-                                          int lane) {
-    const int np = a.ctx < 256 ? a.ctx : 256;  // positions copied (n_kv <= np on the KQV's fast branch)
-    for (int r = wave; r < dsz; r += nwave) {
-        const uint16_t *src = a.vc + ((int64_t)kvh * a.hd + d_lo + r) * a.ctx + lane * 8;
-        auto *dst = (__attribute__((address_space(3))) void *)(smem + a.v_lds + (uint32_t)r * ATT_VDMA_PITCH);
-        if (lane * 8 < np) __builtin_amdgcn_global_load_lds((const void *)src, dst, 16, 0, 0);
-    }
 }
 
 // One token's attention for query head h by one NTH-thread workgroup (SURVEY A.4/A.6 order).
@@ -329,23 +291,17 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     const float *cs = a.rope_cur, *sn = a.rope_cur + half;
     // ---- early loads (issue order = wait order): RoPE inputs + pos, then K rows, then V rows
     // RoPE inputs: only the RoPE wave loads them (every load instruction costs the CU's load path
-    // ~16 clk whatever its addresses; a wave-uniform branch skips the others).  GHIP_AH_RW: the
-    // RoPE wave is the LAST wave and it issues its own K / V prefetch only after the RoPE: the
-    // RoPE's wait for its inputs sits after a branch, where the compiler can only drain every load
-    // (s_waitcnt vmcnt(0)), so a RoPE wave that had issued its prefetch first waited for all of it
-    // before the workgroup barrier (stamps build 4: RoPE done 1.2-1.5 µs, the prefetch's landing)
-    constexpr int RW = GHIP_AH_RW ? NTH / 64 - 1 : 0;  // the RoPE wave (hd <= 512: 64 lanes suffice)
-    const int rl = tid - RW * 64;
+    // ~16 clk whatever its addresses; a wave-uniform branch skips the others)
+    const int rl = tid;  // the RoPE lanes: wave 0 (hd <= 512: 64 lanes suffice)
     const int n4 = half / 4, i4 = (rl >= 0 && rl < n4 ? rl : 0) * 4;
     float4 qa{}, qb{}, ka{}, kb{}, ca{}, sa{};
-    if (GHIP_AH_RW ? wave == RW : wave * 64 < n4) {
+    if (wave * 64 < n4) {
         qa = ld4<SC1>(qh + i4); qb = ld4<SC1>(qh + i4 + half);
         ka = ld4<SC1>(kh + i4); kb = ld4<SC1>(kh + i4 + half);
         ca = *(const float4 *)(cs + i4); sa = *(const float4 *)(sn + i4);
     }
     attn_pre<KPF, VPF> own;
-    if (!PRE && (!GHIP_AH_RW || wave != RW)) attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi, tid);
-    if (a.v_lds) attn_vdma(a, kvh, d_lo, dsz, smem, wave, nwave, lane);
+    if (!PRE) attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi, tid);
     const attn_pre<KPF, VPF> &P = PRE ? *pre : own;
     const uint4 *kpre = P.k, *vpre = P.v;
     const int d0 = d_lo + quad < d_hi ? d_lo + quad : d_lo;
@@ -385,10 +341,6 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
     if (rl == 0) {  // (the RoPE wave: its loads are drained here; another wave could wait on them)
         *mx_key = 0u;  // below the key of every float, -inf included
         *e_sum = 0ull;
-    }
-    if (GHIP_AH_RW && !PRE && wave == RW) {
-        asm volatile("" ::: "memory");  // (issued after the RoPE, not hoisted above it)
-        attn_prefetch<NTH, KPF, VPF>(a, h, own, d_lo, d_hi, tid);
     }
     const int pos = __builtin_amdgcn_readfirstlane(P.pos_v);
     const int n_total = pos + 1;
@@ -475,16 +427,6 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         }
     }
     // the row max, partial per wave (DPP) then one LDS max per wave, in the same barrier as S
-    // GHIP_AH_VEARLY: the V rows of this quad's first KQV dim issued here, after the K dots (their
-    // registers are free again), so they land during the softmax; only the waves owning dims load
-    // (a scalar branch on the uniform wave index), only steps below n_kv
-    uint4 ve[8];
-    const bool vearly = GHIP_AH_VEARLY && VPF == 0 && !a.v_lds && n_kv <= 256 && d_lo + wave * 16 < d_hi;
-    if (vearly) {
-        const uint16_t *vr0 = a.vc + ((int64_t)kvh * hd + d0) * a.ctx + t4 * 8;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) ve[s] = s * 32 < n_kv ? *(const uint4 *)(vr0 + s * 32) : make_uint4(0, 0, 0, 0);
-    }
     lmax = wave_max(lmax);
     if (lane == 0) {
         const uint32_t b = __builtin_bit_cast(uint32_t, lmax);
@@ -523,7 +465,6 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             if (a.dbg_p) a.dbg_p[(int64_t)h * a.ctx + j] = P16[j];
         }
     }
-    if (a.v_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V DMAs have landed
     attn_barrier();
     AH_STAMP(3);
     // ---- KQV: out[d] = vec_dot_f16(n_kv, V[kvh][d][0..n_kv), P16); lane t4 runs accumulator j = t4
@@ -553,24 +494,15 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
             // for every dimension) read into registers once
             uint4 xs8[8], pr8[8];
             const bool first = d == d0;
-            if (a.v_lds) {
-                const uint8_t *vl = smem + a.v_lds + (uint32_t)(d - d_lo) * ATT_VDMA_PITCH + t4 * 16;
 #pragma unroll
-                for (int s = 0; s < 8; ++s) xs8[s] = *(const uint4 *)(vl + (s * 32 < n_kv ? s * 64 : 0));
-            } else {
-#pragma unroll
-                for (int s = 0; s < 8; ++s) {
-                    const int e0 = s * 32 + t4 * 8;
-                    if (vearly && first) xs8[s] = ve[s];
-                    else if (s < VPF && first) xs8[s] = vpre[s < VPF ? s : 0];
-                    else if (!GHIP_AH_TRIM || s * 32 < n_kv) xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
-                    else xs8[s] = make_uint4(0, 0, 0, 0);  // past n_kv: never used (no load issued)
-                }
+            for (int s = 0; s < 8; ++s) {
+                const int e0 = s * 32 + t4 * 8;
+                if (s < VPF && first) xs8[s] = vpre[s < VPF ? s : 0];
+                else xs8[s] = *(const uint4 *)(vr + (s * 32 < n_kv ? e0 : t4 * 8));
             }
 #pragma unroll
             for (int s = 0; s < 8; ++s)
-                pr8[s] = (!GHIP_AH_TRIM || s * 32 < n_kv) ? *(const uint4 *)(P16 + (s * 32 < n_kv ? s * 32 : 0) + t4 * 8)
-                                                          : make_uint4(0, 0, 0, 0);
+                pr8[s] = *(const uint4 *)(P16 + (s * 32 < n_kv ? s * 32 : 0) + t4 * 8);
             if (GHIP_STAMPS == 2 && d == d_lo + quad) {  // operands in registers (stamps build 2)
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                 AH_STAMP(5);
@@ -587,7 +519,7 @@ __device__ void attn_head_dev(const attn_args &a, const int h, uint8_t *smem, co
         for (int st = 0, s = 0; st < n_kv; st += 32, ++s) {
             const int e0 = st + t4 * 8;
             uint4 xv;
-            if (!a.v_lds && d == d0 && s < VPF) {  // (with the LDS copy no V was loaded early)
+            if (d == d0 && s < VPF) {
                 xv = vpre[0];  // statically-indexed pick from the early loads
 #pragma unroll
                 for (int k = 1; k < VPF; ++k)

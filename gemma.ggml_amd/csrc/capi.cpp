@@ -453,8 +453,8 @@ extern "C" double gemma_kq_time(int type, int64_t rows, int64_t K, int iters, do
     (void)hipStreamCreate(&s);
     kq_args a;
     a.row_bytes = rb; a.rows = rows; a.nsb = (int)nsb; a.x = x; a.x_col_stride = nsb * 292; a.y = y; a.y_col_stride = rows;
-    // the engine's lane-contiguous layout unless GHIP_KQ_TILE=0 (the bytes are arbitrary either way)
-    a.tiled = (!getenv("GHIP_KQ_TILE") || atoi(getenv("GHIP_KQ_TILE"))) && (type == T_Q4_K || K % 2048 == 0);
+    // the engine's lane-contiguous layout (the bytes are arbitrary either way)
+    a.tiled = type == T_Q4_K || K % 2048 == 0;
     int r = 0;
     for (int i = 0; i < 3 && !r; ++i) { a.w = w + (size_t)(i % copies) * wbytes; r = launch_matvec_kq(type, a, s); }
     hipEvent_t e0, e1;

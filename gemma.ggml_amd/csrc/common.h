@@ -60,6 +60,7 @@ struct tiled_mat {
 
 // error state (thread-local last error, exposed by hpc_last_error)
 void set_error(const std::string &msg);
+int ghip_debug_level();  // GHIP_GGML_DEBUG (ggml_api.cpp): 0 quiet, 1 fast-path reasons, 2 + host timings
 const std::string &last_error();
 
 #define GHIP_CHECK(expr)                                                                        \

@@ -177,12 +177,6 @@ struct gemma_engine {
     gemma_hip_config cfg{};
     int device = 0;
     hipStream_t stream = nullptr;
-    // MALL warm-up (GHIP_WARM): while a layer's attention runs on a few CUs, a side-stream kernel
-    // reads that layer's attn-out and gate/up weights so their matvecs stream from the Infinity Cache
-    int warm = 0, warm_grid = 512;
-    hipStream_t side = nullptr;
-    std::vector<hipEvent_t> ev_fork;
-    hipEvent_t ev_join = nullptr;
     int qw = 0, kvw = 0, qkv_rows = 0;
     tiled_mat embd;
     // token_embd / tied output in Q6_K (llama.cpp's Q4_0 / Q8_0 Gemma files): raw ggml rows, the
@@ -232,12 +226,16 @@ struct gemma_engine {
     // hand-off counters [n_layer][16] zeroed once per token (memset node), sticky timeout word
     // K-quant layers: kq_fuse = the plan for where ggml's Q8_K INIT runs (enqueue_step_kq, 0..6);
     // kq_dual: gate+up in one launch
-    int kq_fuse = 5, kq_dual = 1, kq_pair = 1, kq_gu2 = 0;  // kq_gu2: GHIP_KQ_GU2 (k_matvec_kq_gu2)  // kq_pair: q|k and v in one launch (GHIP_KQ_PAIR)
+    // K-quant step options (gemma_engine_set_option): the Q8_K INIT plan, gate+up in one launch, q|k
+    // and v in one launch
+    int kq_fuse = 5, kq_dual = 1, kq_pair = 1;
     // per-head decode attention: workgroups per head (each the KQ/softmax, 1/att_dsplit of the KQV
-    // dims; GHIP_ATT_DSPLIT). Same box, decode tok/s: 1 / 2 / 4 -> 1,443 / 1,458 / 1,458; after the
+    // dims; option "att_dsplit"). Same box, decode tok/s: 1 / 2 / 4 -> 1,443 / 1,458 / 1,458; after the
     // batched K/V step loads 2 / 4 / 8 -> 1,470-1,482 / 1,491 / 1,355-1,369 (scripts/env_ab.sh)
     int att_dsplit = 4;
-    int kq_abl = 0;  // GHIP_KQ_ABL: hand-off timing ablation (kq_args::q8_abl; wrong results)
+    int kq_abl = 0;  // option "kq_abl": hand-off timing ablation (kq_args::q8_abl; wrong results)
+    int att_mx = 1;  // option "att_mx": exact prefill attention on the f32 matrix cores (0: the row form)
+    int time_hot = 0, ablate = 0;  // gemma_engine_time diagnostics: one layer's matrix repeated; ablations
     // the whole token's layers as ONE persistent launch (token.hip) when the shapes
     // allow it (GHIP_PERSIST=1 or gemma_engine_set_persist(e, 1)); off by default until it beats
     // the per-layer launches on the bench
@@ -272,6 +270,7 @@ struct gemma_engine {
     // launch geometry: one plan per matrix class (defaults below; gemma_engine_tune measures)
     int ks_small = KS_RR, ks_down = KS_RR;  // round-pipelined form where the shape allows (pick_ks falls back)
     int grid_big = 2048;
+    int grid_big_cap = 2048;  // workgroups the argmax key buffer holds
     launch_plan plan[MC_N];
     // prefill scratch (lazily allocated)
     // prefill buffers (lazily sized for the prompt length)
@@ -359,13 +358,11 @@ static inline uint16_t *vc_of(const gemma_engine *e, int il) {
 
 static inline int wfmt_scale(int wt) { return wt == T_Q4_0 ? 16 : 8; }  // scale bytes per row and tile
 
-// join the warm-up side stream back into the engine stream (one join per step / capture)
-// ggml K-quant rows -> the lane-contiguous layout, in place (through a scratch copy); GHIP_KQ_TILE=0
-// keeps ggml rows.  Q6_K needs K % 2048 == 0 (else the rows stay as they are).
+// ggml K-quant rows -> the lane-contiguous layout, in place (through a scratch copy).  Q6_K needs
+// K % 2048 == 0 (else the rows stay as they are).
 static int kq_retile_inplace(uint8_t *w, int type, int64_t rows, int64_t K, hipStream_t s, bool *tiled) {
-    static const bool on = !getenv("GHIP_KQ_TILE") || atoi(getenv("GHIP_KQ_TILE"));
     *tiled = false;
-    if (!on || (type == T_Q6_K && K % 2048)) return 0;
+    if (type == T_Q6_K && K % 2048) return 0;
     const size_t bytes = (size_t)(K / 256 * (type == T_Q4_K ? 144 : 210) * rows);
     uint8_t *tmp = nullptr;
     GHIP_CHECK(hipMalloc(&tmp, bytes));
@@ -374,13 +371,6 @@ static int kq_retile_inplace(uint8_t *w, int type, int64_t rows, int64_t K, hipS
     GHIP_CHECK(hipStreamSynchronize(s));
     GHIP_CHECK(hipFree(tmp));
     *tiled = true;
-    return 0;
-}
-
-static int warm_join(gemma_engine *e) {
-    if (!e->warm || !e->side) return 0;
-    GHIP_CHECK(hipEventRecord(e->ev_join, e->side));
-    GHIP_CHECK(hipStreamWaitEvent(e->stream, e->ev_join, 0));
     return 0;
 }
 
@@ -435,7 +425,7 @@ static int tok_prepare(gemma_engine *e) {
     return 0;
 }
 static bool persist_on(const gemma_engine *e) {
-    return e->persist && e->persist_why.empty() && !e->dbg && !e->stamp && e->att_mode == ATTN_PER_HEAD && !e->warm &&
+    return e->persist && e->persist_why.empty() && !e->dbg && !e->stamp && e->att_mode == ATTN_PER_HEAD &&
            !e->fuse_front;
 }
 
@@ -498,7 +488,7 @@ static int enqueue_step(gemma_engine *e) {
         goto logits;
     }
     {
-    const bool front_ok = e->front_cnt && e->fuse_front && e->tp_n == 1 && !e->comm && e->n_virtual == 1 && !e->warm &&
+    const bool front_ok = e->front_cnt && e->fuse_front && e->tp_n == 1 && !e->comm && e->n_virtual == 1 &&
                           e->att_mode == ATTN_PER_HEAD && e->att_act && e->plan[MC_QKV].ks == KS_RR &&
                           e->plan[MC_O].ks == KS_RR && e->plan[MC_O].img;
     if (front_ok) GHIP_CHECK(hipMemsetAsync(e->front_cnt, 0, (size_t)c.n_layer * 16 * 32 * 4, s));
@@ -570,19 +560,9 @@ static int enqueue_step(gemma_engine *e) {
         t.mode = e->att_mode;
         t.nwg = e->ag.nwg; t.sbuf = e->att_sbuf; t.sync = e->att_sync; t.err = e->att_sync + e->ag.sync_ints;
         t.dbg_t = stamp_region(e, il, 1);
-        if (e->warm && e->side) {  // fork: warm attn-out + gate/up while attention runs
-            const layer_dev &W = layer_of(e, il, 0);
-            const void *ptrs[6] = {W.o.qs, W.o.sc, W.gate.qs, W.gate.sc, W.up.qs, W.up.sc};
-            const int64_t bytes[6] = {W.o.n_rt * W.o.n_bt * 1024, W.o.n_rt * W.o.n_bt * 8 * wfmt_scale(wt),
-                                      W.gate.n_rt * W.gate.n_bt * 1024, W.gate.n_rt * W.gate.n_bt * 8 * wfmt_scale(wt),
-                                      W.up.n_rt * W.up.n_bt * 1024, W.up.n_rt * W.up.n_bt * 8 * wfmt_scale(wt)};
-            GHIP_CHECK(hipEventRecord(e->ev_fork[il], s));
-            GHIP_CHECK(hipStreamWaitEvent(e->side, e->ev_fork[il], 0));
-            if (launch_mall_warm(ptrs, bytes, 6, e->warm_grid, e->side)) return -1;
-        }
         if (t.mode == ATTN_PER_HEAD) t.dsplit = e->att_dsplit;
         // attention + attn-out in one launch (k_attn_o): the attention's idle workgroups run attn-out
-        if (e->att_o && att_img && e->n_virtual == 1 && e->ao_cnt && !e->warm && e->plan[MC_O].ks == KS_RR) {
+        if (e->att_o && att_img && e->n_virtual == 1 && e->ao_cnt && e->plan[MC_O].ks == KS_RR) {
             const layer_dev &L = layer_of(e, il, 0);
             const size_t r0 = (size_t)rank_of(e, 0) * e->sh_e;
             attn_o_args f;
@@ -680,7 +660,7 @@ logits:
         if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
         if (launch_row_argmax(e->logits, c.n_vocab, e->key, 256, s)) return -1;
         if (launch_advance(e->key, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s)) return -1;
-        return warm_join(e);
+        return 0;
     }
     int lg_grid = 0;
     for (int vr = 0; vr < e->n_virtual; ++vr) {
@@ -699,7 +679,7 @@ logits:
     }
     if (!e->tp_n_keys) {
         if (launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s)) return -1;
-        return warm_join(e);
+        return 0;
     }
     if (e->comm) {
         const ncclResult_t nr = ncclAllGather(e->rank_keys + e->tp_rank, e->rank_keys, 1, ncclUint64, e->comm, s);
@@ -773,8 +753,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
             k.q8_abl = e->kq_abl;
         }
         if (up) k.w2 = up->w;
-        k.gu2 = e->kq_gu2;
-        return k;
+                return k;
     };
     auto mv = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in, const img &in, const out &o,
                   const kq_mat *up) { return launch_matvec_kq(W.type, args(W, y, resid, gate_in, in, o, up), s); };
@@ -868,7 +847,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
     if (launch_matvec_kq(T_Q6_K, k, s)) return -1;
     if (launch_row_argmax(e->logits, c.n_vocab, e->key, 256, s)) return -1;
     if (launch_advance(e->key, 256, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s)) return -1;
-    return warm_join(e);
+    return 0;
 }
 
 // real weights in ggml row-major layout (a GGUF file's tensors, src/gemma_model.cpp:145-182)
@@ -920,7 +899,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         set_error("gemma_engine_create: hipSetDevice failed");
         return nullptr;
     }
-    static const bool cprof = getenv("GHIP_CREATE_PROF") != nullptr;
+    constexpr bool cprof = false;  // engine-creation phase timings to stderr (diagnostics build: set true)
     auto cnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double ct0 = cprof ? cnow() : 0.0;
     auto *e = new gemma_engine();
@@ -943,18 +922,6 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     e->sh_e = c.n_embd / tp_n;
     e->sh_ff = c.n_ff / tp_n;
     e->sh_v = c.n_vocab / tp_n;
-    if (const char *v = getenv("GHIP_KS_SMALL")) e->ks_small = atoi(v);
-    if (const char *v = getenv("GHIP_KS_DOWN")) e->ks_down = atoi(v);
-    if (const char *v = getenv("GHIP_GRID_BIG")) e->grid_big = atoi(v);
-    if (const char *v = getenv("GHIP_WARM")) e->warm = atoi(v);
-    if (const char *v = getenv("GHIP_WARM_GRID")) e->warm_grid = atoi(v);
-    if (tp_n > 1 || nccl_id) e->warm = 0;  // single-GPU decode only
-    if (e->warm) {
-        GHIP_FATAL(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
-        e->ev_fork.resize(c.n_layer);
-        for (hipEvent_t &ev : e->ev_fork) GHIP_FATAL(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        GHIP_FATAL(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
-    }
     const int wt = c.wtype;
     const uint64_t seed = c.seed;
     hipStream_t s = e->stream;
@@ -1114,7 +1081,6 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     build_rope(c.n_ctx, c.head_dim, c.rope_base, rc, rs);
     // attention form: one workgroup per head up to 2048 positions, the position-split form beyond
     e->att_mode = (c.head_dim <= 256 && c.n_ctx <= 2048) ? ATTN_PER_HEAD : ATTN_SPLIT;
-    if (const char *v = getenv("GHIP_ATTN")) e->att_mode = strcmp(v, "split") == 0 ? ATTN_SPLIT : ATTN_PER_HEAD;
     e->ag = attn_geometry(c.n_head, c.n_head_kv, c.head_dim, c.n_ctx);
     if (e->att_mode == ATTN_SPLIT && !e->ag.nwg) {
         set_error("gemma_engine_create: unsupported attention geometry");
@@ -1138,12 +1104,6 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     GHIP_FATAL(hipMalloc(&e->attn, (size_t)e->qw * 4));
     GHIP_FATAL(hipMalloc(&e->sa, (size_t)c.n_embd * 4));
     GHIP_FATAL(hipMalloc(&e->h, (size_t)c.n_ff * 4));
-    if (const char *v = getenv("GHIP_KQ_FUSE")) e->kq_fuse = atoi(v);
-    if (const char *v = getenv("GHIP_KQ_DUAL")) e->kq_dual = atoi(v);
-    if (const char *v = getenv("GHIP_KQ_ABL")) e->kq_abl = atoi(v);
-    if (const char *v = getenv("GHIP_KQ_PAIR")) e->kq_pair = atoi(v);
-    if (const char *v = getenv("GHIP_KQ_GU2")) e->kq_gu2 = atoi(v);
-    if (const char *v = getenv("GHIP_ATT_DSPLIT")) e->att_dsplit = atoi(v);
     // launch_attn_decode needs head_dim % (32 * dsplit) == 0: the largest of 4 / 2 / 1 that divides
     // (head_dim 32 / 64 / 96 / 160 / ... take fewer workgroups per head, never a failing step)
     if (e->att_dsplit < 1) e->att_dsplit = 1;
@@ -1155,7 +1115,6 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         GHIP_FATAL(hipMalloc(&e->front_err, 64));
         GHIP_FATAL(hipMemset(e->front_cnt, 0, (size_t)c.n_layer * 16 * 32 * 4));
         GHIP_FATAL(hipMemset(e->front_err, 0, 64));
-        if (const char *v = getenv("GHIP_FUSE_FRONT")) e->fuse_front = atoi(v);
         GHIP_FATAL(hipMalloc(&e->ao_cnt, (size_t)c.n_layer * 16 * 32 * 4));
         GHIP_FATAL(hipMalloc(&e->ao_err, 64));
         GHIP_FATAL(hipMemset(e->ao_cnt, 0, (size_t)c.n_layer * 16 * 32 * 4));
@@ -1193,7 +1152,6 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         GHIP_FATAL(hipMemset(e->tok_err, 0, 64));
         GHIP_FATAL(hipMalloc(&e->tok_dev, sizeof(tok_args)));
         GHIP_FATAL(hipMalloc(&e->tok_tab, (size_t)c.n_layer * sizeof(tok_layer)));
-        if (const char *v = getenv("GHIP_PERSIST")) e->persist = atoi(v);
     }
     GHIP_FATAL(hipMalloc(&e->key, (size_t)e->grid_big * 8));  // per-workgroup argmax keys
     GHIP_FATAL(hipMalloc(&e->pos, 4));
@@ -1418,11 +1376,8 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     if (e->kq_x) (void)hipFree(e->kq_x);
     if (e->kq_g) (void)hipFree(e->kq_g);
     if (e->kq_cnt) (void)hipFree(e->kq_cnt);
-    for (hipEvent_t ev : e->ev_fork) (void)hipEventDestroy(ev);
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     for (hipEvent_t &ev : e->fc_ev)
         if (ev) (void)hipEventDestroy(ev);
-    if (e->side) (void)hipStreamDestroy(e->side);
     if (e->xq8k) (void)hipFree(e->xq8k);
     (void)hipStreamDestroy(e->stream);
     delete e;
@@ -1674,8 +1629,8 @@ extern "C" double gemma_engine_time(gemma_engine *e, int which, int iters, doubl
     }
     setup(e->layers[0]);
     (void)act_q8;
-    const bool hot = getenv("GHIP_TIME_HOT") != nullptr;
-    if (const char *v = getenv("GHIP_ABLATE")) a.ablate = atoi(v);
+    const bool hot = e->time_hot != 0;
+    a.ablate = e->ablate;
     hipEvent_t t0, t1;
     GHIP_FATAL(hipEventCreate(&t0));
     GHIP_FATAL(hipEventCreate(&t1));
@@ -1908,6 +1863,38 @@ extern "C" int gemma_engine_persist_err(gemma_engine *e, int *out3, int reset) {
     return w[0];
 }
 
+// Engine options (tests, A/B): the measured variants that stay selectable, set through the API so a
+// stray environment variable on a box can never change the benched kernels.  Returns 0, or -1 for an
+// unknown name.  The decode graph is dropped (re-captured at the next step).
+extern "C" int gemma_engine_set_option(gemma_engine *e, const char *name, int value) {
+    set_error("");
+    const std::string n = name ? name : "";
+    int *f = n == "kq_fuse" ? &e->kq_fuse : n == "kq_dual" ? &e->kq_dual : n == "kq_pair" ? &e->kq_pair
+           : n == "kq_abl" ? &e->kq_abl : n == "att_mx" ? &e->att_mx : n == "time_hot" ? &e->time_hot
+           : n == "ablate" ? &e->ablate : n == "ks_small" ? &e->ks_small : n == "ks_down" ? &e->ks_down : nullptr;
+    if (n == "att_dsplit") {
+        if (value < 1 || value > 8 || (value & (value - 1)) || e->cfg.head_dim % (32 * value)) {
+            set_error("gemma_engine_set_option: att_dsplit must be 1, 2, 4 or 8 and divide head_dim / 32");
+            return -1;
+        }
+        f = &e->att_dsplit;
+    }
+    if (n == "grid_big") {
+        if (value < 1 || value > e->grid_big_cap) {
+            set_error("gemma_engine_set_option: grid_big out of range (1 .. the argmax key buffer)");
+            return -1;
+        }
+        f = &e->grid_big;
+    }
+    if (!f) {
+        set_error("gemma_engine_set_option: unknown option '" + n + "'");
+        return -1;
+    }
+    *f = value;
+    drop_graph(e);
+    return 0;
+}
+
 // attention + attn-out in one launch on (1) / off (0) / unchanged (-1); returns the setting
 extern "C" int gemma_engine_set_att_o(gemma_engine *e, int on) {
     if (on >= 0 && (on != 0) != (e->att_o != 0)) {
@@ -1925,20 +1912,6 @@ extern "C" int gemma_engine_set_fuse(gemma_engine *e, int fuse_front) {
     }
     int err = 0;
     if (e->front_err) (void)hipMemcpy(&err, e->front_err, 4, hipMemcpyDeviceToHost);
-    if (getenv("GHIP_FRONT_DUMP") && e->front_err) {
-        int w[8];
-        (void)hipMemcpy(w, e->front_err, 32, hipMemcpyDeviceToHost);
-        fprintf(stderr, "front_err: flag %d site %d value %d target %d max_polls %d\n", w[0], w[1], w[2], w[3], w[4]);
-    }
-    if (getenv("GHIP_FRONT_DUMP") && e->front_cnt) {  // diagnostics: the hand-off counters
-        std::vector<unsigned> v((size_t)e->cfg.n_layer * 16 * 32);
-        (void)hipMemcpy(v.data(), e->front_cnt, v.size() * 4, hipMemcpyDeviceToHost);
-        for (int il = 0; il < e->cfg.n_layer; ++il) {
-            fprintf(stderr, "front_cnt[%d]:", il);
-            for (int k = 0; k < 16; ++k) fprintf(stderr, " %u", v[((size_t)il * 16 + k) * 32]);
-            fprintf(stderr, "\n");
-        }
-    }
     return err;
 }
 
@@ -2013,12 +1986,11 @@ static int kq_expand(gemma_engine *e, const uint8_t *x, int64_t ld, int64_t K, i
 
 // The exact prefill attention: on the f32 matrix cores where the shapes allow it (attn_mx.hip:
 // v_mfma_f32_16x16x4_f32 is an fmaf chain over K, so vec_dot_f16's chains ride it bit for bit),
-// else per row with v_fma_mix (k_attn_rows).  GHIP_ATT_MX=0 forces the row form (tests, A/B).
-// The form is resolved once per prefill (att_mx_form): the env switch and the shape check do not
+// else per row with v_fma_mix (k_attn_rows).  Option "att_mx" 0 forces the row form (tests, A/B).
+// The form is resolved once per prefill (att_mx_form): the option and the shape check do not
 // change between its layers.
-static bool att_mx_form(const attnp_args &at) {
-    const char *env = getenv("GHIP_ATT_MX");
-    return (!env || atoi(env) != 0) && !attn_mx_unsupported(at);
+static bool att_mx_form(const gemma_engine *e, const attnp_args &at) {
+    return e->att_mx && !attn_mx_unsupported(at);
 }
 static int launch_attn_exact(const attnp_args &at, bool mx, hipStream_t s) {
     return mx ? launch_attn_mx(at, s) : launch_attn_rows(at, s);
@@ -2073,7 +2045,7 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
         attnp_args at;
         at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
         at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
-        if (mx_form < 0) mx_form = att_mx_form(at);
+        if (mx_form < 0) mx_form = att_mx_form(e, at);
         if (exact ? launch_attn_exact(at, mx_form == 1, s) : launch_attn_prefill(at, s)) return -1;
         if (quant(QR_F32, p.ATT, nullptr, e->qw, nullptr)) return -1;
         if (gemm(L.o, EPI_ADD, p.X, p.SA, E)) return -1;
@@ -2181,7 +2153,7 @@ static int enqueue_prefill_kq(gemma_engine *e, int T) {
         attnp_args at;
         at.q16 = p.Q16; at.kc = r.kc; at.vc = r.vc; at.out = p.ATT; at.ldo = e->qw;
         at.T = T; at.H = c.n_head; at.Hkv = c.n_head_kv; at.hd = c.head_dim; at.ctx = c.n_ctx; at.n_kv = n_kv;
-        if (mx_form < 0) mx_form = att_mx_form(at);
+        if (mx_form < 0) mx_form = att_mx_form(e, at);
         if (launch_attn_exact(at, mx_form == 1, s)) return -1;
         if (launch_quant_q8_K(p.ATT, e->qw, e->qw, T, img, ldk, s) || expand(e->qw)) return -1;
         if (mv(K.o, p.SA, E, p.X, nullptr, nullptr)) return -1;  // + inpL
@@ -2537,7 +2509,7 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
         set_error("gemma_engine_ext_decode: token or position out of range");
         return -1;
     }
-    static const bool prof = getenv("GHIP_GGML_FAST_PROF") != nullptr;
+    const bool prof = ghip_debug_level() >= 2;  // GHIP_GGML_DEBUG=2: per-step host phases to stderr
     auto us = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t0 = prof ? us() : 0.0;
     (void)hipSetDevice(e->device);
@@ -2553,19 +2525,14 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
     // logits through a pinned staging row (a pageable device-to-host copy stages through the driver);
     // with the persistent launch its sticky timeout word rides along, so ONE sync covers both
     const size_t lb = (size_t)c.n_vocab * 4;
-    static const int direct = getenv("GHIP_EXT_DIRECT") ? atoi(getenv("GHIP_EXT_DIRECT")) : 0;
     const bool pchk = persist_on(e) && e->tok_err;
     auto copy_out = [&]() -> int {
         if (pchk) {
             if (!e->ext_err) GHIP_CHECK(hipHostMalloc((void **)&e->ext_err, 16, hipHostMallocDefault));
             GHIP_CHECK(hipMemcpyAsync(e->ext_err, e->tok_err, 12, hipMemcpyDeviceToHost, e->stream));
         }
-        if (direct) {  // A/B: straight into the (pageable) graph tensor
-            GHIP_CHECK(hipMemcpyAsync(logits, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
-        } else {
-            if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, lb, hipHostMallocDefault));
-            GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
-        }
+        if (!e->ext_stage) GHIP_CHECK(hipHostMalloc((void **)&e->ext_stage, lb, hipHostMallocDefault));
+        GHIP_CHECK(hipMemcpyAsync(e->ext_stage, e->logits, lb, hipMemcpyDeviceToHost, e->stream));
         GHIP_CHECK(hipStreamSynchronize(e->stream));
         return 0;
     };
@@ -2577,7 +2544,7 @@ int gemma_engine_ext_decode(gemma_engine *e, int token, int pos, float *logits) 
         if (copy_out()) return -1;
     }
     const double t2 = prof ? us() : 0.0;
-    if (!direct) memcpy(logits, e->ext_stage, lb);
+    memcpy(logits, e->ext_stage, lb);
     if (prof) fprintf(stderr, "[gemma_hip] ext_decode: launch+run %.1f us, copy %.1f us, host copy %.1f us\n", t1 - t0, t2 - t1, us() - t2);
     e->host_pos = pos + 1;
     return 0;

@@ -40,6 +40,18 @@
 
 using namespace ghip;
 
+namespace ghip {
+// GHIP_GGML_DEBUG (operational knob): the ggml executor's diagnostics on stderr — 1: why the fast
+// path was not taken or failed; 2: also the per-step host phase timings
+int ghip_debug_level() {
+    static const int level = [] {
+        const char *v = getenv("GHIP_GGML_DEBUG");
+        return v ? atoi(v) : 0;
+    }();
+    return level;
+}
+}  // namespace ghip
+
 namespace ggml_impl {
 
 constexpr size_t kArenaAlign = 32;
@@ -805,14 +817,15 @@ double now_us() {
 }
 
 int try_fast(ggml_cgraph *g) {
+    // GHIP_GGML_FAST=0: every graph node by node (operational knob: the executor's generic path)
     static const bool on = !getenv("GHIP_GGML_FAST") || atoi(getenv("GHIP_GGML_FAST"));
-    static const bool prof = getenv("GHIP_GGML_FAST_PROF") != nullptr;
+    const bool prof = ghip_debug_level() >= 2;
     if (!on || g->n_nodes < 8) return 0;
     const double t0 = prof ? now_us() : 0.0;
     gemma_match m;
     std::string why;
     if (!match_gemma(g, m, why)) {
-        if (getenv("GHIP_GGML_FAST_WHY")) fprintf(stderr, "[gemma_hip] ggml fast path not taken: %s\n", why.c_str());
+        if (ghip_debug_level() >= 1) fprintf(stderr, "[gemma_hip] ggml fast path not taken: %s\n", why.c_str());
         return 0;
     }
     const double tm = prof ? now_us() : 0.0;
@@ -859,7 +872,7 @@ int try_fast(ggml_cgraph *g) {
     const int rc = m.T == 1 ? gemma_engine_ext_decode(f.e, m.tokens[0], m.pos0, (float *)last->data)
                             : gemma_engine_ext_prefill(f.e, m.tokens.data(), m.T, (float *)last->data);
     if (rc) {  // the engine could not serve this graph: node by node instead (same results)
-        if (getenv("GHIP_GGML_FAST_WHY")) fprintf(stderr, "[gemma_hip] ggml fast path failed: %s\n", last_error().c_str());
+        if (ghip_debug_level() >= 1) fprintf(stderr, "[gemma_hip] ggml fast path failed: %s\n", last_error().c_str());
         set_error("");
         return 0;
     }

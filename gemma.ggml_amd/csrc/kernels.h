@@ -124,7 +124,6 @@ struct kq_args {  // y[c][r] = vec_dot_{q4_K,q6_K}_q8_K(row r of w, column c of 
     const float *q8_norm = nullptr;
     int q8_abl = 0;  // timing ablation only (wrong bytes): 1 no tail work, 2 no counting, 4 plain stores
     int tiled = 0;   // w (and w2) in the lane-contiguous layout of launch_kq_retile
-    int gu2 = 0;     // DUAL, one column: the K-split-in-two gate/up kernel (k_matvec_kq_gu2)
     unsigned long long *dbg_t = nullptr;  // stamps build: 16 s_memrealtime per workgroup (k_matvec_kq)
 };
 // ggml K-quant rows <-> the lane-contiguous device layout the matvec reads with one vector load per
@@ -281,12 +280,6 @@ struct attn_args {
     float *out_da = nullptr;
     uint8_t *out_q8k = nullptr;   // per-head mode, hd == 256: out's Q8_K image (one super-block per head)
     int dsplit = 1;               // per-head mode: workgroups per head, each the KQV of hd/dsplit dims
-    // per-head mode (k_attn_head): byte offset in LDS of the workgroup's V rows, copied there by
-    // LDS-DMA at the start (positions < min(ctx, 256), row pitch ATT_VDMA_PITCH); 0 = no copy
-    uint32_t v_lds = 0;
-    // per-head mode: 1 = head h's workgroups on XCD h % 8 (blocks b -> h = b % H, split b / H), so
-    // the heads' K / V reads spread over the XCDs' L2s; 0 = every workgroup of a kv head on one XCD
-    int spread = 0;
     int H, Hkv, hd, ctx;
     float q_scale;
     float *dbg_w = nullptr;      // optional debug taps: [H][ctx] scores, [H][ctx] fp16 P, [H] inv

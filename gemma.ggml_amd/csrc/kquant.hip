@@ -182,9 +182,6 @@ __device__ __forceinline__ kq_term kq_block(const uint8_t *wrow, const uint8_t *
 #define GHIP_KQ_PF 2  // Q4_K_M decode, same box: 1 / 2 / 3 / 4 / 8 -> 1.170 / 1.132 / 1.140 / 1.155 / 1.315 ms/token
 #endif
 constexpr int KQ_PF = GHIP_KQ_PF;
-#ifndef GHIP_KQ_KSX
-#define GHIP_KQ_KSX 0
-#endif
 #ifndef GHIP_KQ_EARLY
 #define GHIP_KQ_EARLY 2  // 1: first weight round issued before the Q8_K staging; 2: after every wave's
                          // activation loads (one s_barrier): Q4_K_M 1,066-1,067 vs 1,053-1,066 tok/s
@@ -723,87 +720,6 @@ k_matvec_kq(kq_args a) {
 #undef KQ_STAMP
 }
 
-// gate and up (DUAL) with K split in two (K = 512..2048): a 4-wave workgroup takes 2 row groups,
-// wave 2j+h runs group j's super-blocks [h*nsb/2, (h+1)*nsb/2) of both matrices, its whole
-// segment's weight loads issued before the prologue (one round trip, overlapping it).  Wave 2j+1
-// stashes its exact terms; after one barrier wave 2j continues its own chains through them in
-// super-block order — the identical fmaf sequences — then stores gelu(gate)*up (+ the D hand-off).
-template <int WT, int XJ, bool TL, int HO>
-__global__ void __launch_bounds__(KQ_THREADS) k_matvec_kq_gu2(kq_args a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
-    constexpr int HS = 4;  // super-blocks per half (nsb <= 8)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
-    const int col = blockIdx.y, nsb = a.nsb, half = wave & 1, pair = wave >> 1, hs = nsb >> 1;
-    const int64_t g = (int64_t)blockIdx.x * 2 + pair;
-    const int64_t n_groups = (a.rows + 7) / 8;
-    const int64_t gg = g < n_groups ? g : n_groups - 1;
-    const int64_t row_raw = gg * 8 + rr;
-    const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
-    const uint8_t *w1 = a.w + row * a.row_bytes, *w2 = a.w2 + row * a.row_bytes;
-    // stash after the image + norm scratch: [pair][mat][HS][64] sumi, prod; [pair][mat][HS][8] d, dmin
-    const size_t base = (((size_t)nsb * 292 + 15) & ~(size_t)15) + (size_t)nsb * 64 * sizeof(double);
-    int *st_i = (int *)(xs + base) + pair * (2 * HS * 64 * 2);
-    int *st_p = st_i + 2 * HS * 64;
-    float *st_d = (float *)(xs + base) + 2 * (2 * HS * 64 * 2) + pair * (2 * HS * 8 * 2);
-    float *st_m = st_d + 2 * HS * 8;
-    kq_pro_regs<XJ> pr;
-    kq_pro_load<XJ>(a, col, wave, KQ_THREADS / 64, lane, pr);
-    kq_raw<WT> r1[HS], r2[HS];
-#pragma unroll
-    for (int p = 0; p < HS; ++p) {
-        const int sb = half * hs + (p < hs ? p : 0);
-        r1[p] = kq_load<WT, TL>(w1, sb, l);
-        r2[p] = kq_load<WT, TL>(w2, sb, l);
-    }
-    kq_pro_build<XJ>(a, xs, kq_red(xs, nsb), col, tid, KQ_THREADS, pr);
-    __syncthreads();
-    float acc = 0.0f, accm = 0.0f, acc2 = 0.0f, accm2 = 0.0f;
-#pragma unroll
-    for (int p = 0; p < HS; ++p) {
-        if (p >= hs) break;
-        const int sb = half * hs + p;
-        const kq_term t = kq_terms<WT>(r1[p], xs, sb, l);
-        const kq_term u = kq_terms<WT>(r2[p], xs, sb, l);
-        if (half == 0) {
-            acc = __builtin_fmaf(t.d, (float)t.sumi, acc);
-            acc2 = __builtin_fmaf(u.d, (float)u.sumi, acc2);
-            if (WT == T_Q4_K && l < 4) {
-                accm = __builtin_fmaf(t.dmin, (float)t.prod, accm);
-                accm2 = __builtin_fmaf(u.dmin, (float)u.prod, accm2);
-            }
-        } else {
-            st_i[p * 64 + lane] = t.sumi;
-            st_i[(HS + p) * 64 + lane] = u.sumi;
-            if (l == 0) {
-                st_d[p * 8 + rr] = t.d;
-                st_d[(HS + p) * 8 + rr] = u.d;
-            }
-            if (WT == T_Q4_K) {
-                st_p[p * 64 + lane] = t.prod;
-                st_p[(HS + p) * 64 + lane] = u.prod;
-                if (l == 0) {
-                    st_m[p * 8 + rr] = t.dmin;
-                    st_m[(HS + p) * 8 + rr] = u.dmin;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    if (half != 0 || g >= n_groups) return;
-#pragma unroll
-    for (int p = 0; p < HS; ++p) {
-        if (p >= hs) break;
-        acc = __builtin_fmaf(st_d[p * 8 + rr], (float)st_i[p * 64 + lane], acc);
-        acc2 = __builtin_fmaf(st_d[(HS + p) * 8 + rr], (float)st_i[(HS + p) * 64 + lane], acc2);
-        if (WT == T_Q4_K && l < 4) {
-            accm = __builtin_fmaf(st_m[p * 8 + rr], (float)st_p[p * 64 + lane], accm);
-            accm2 = __builtin_fmaf(st_m[(HS + p) * 8 + rr], (float)st_p[(HS + p) * 64 + lane], accm2);
-        }
-    }
-    kq_store_gu<WT>(a, col, row_raw, l, acc, accm, acc2, accm2);
-    kq_handoff<HO>(a, col, g, lane, xs);
-}
-
 // T-column form (the batched prefill): NC columns per workgroup share every weight load, so the
 // weights leave L2 / HBM once per NC prompt rows instead of once per row; each (row, column) is
 // still the decode dot in ggml's lane order (one fmaf chain per lane and column), so the result is
@@ -884,8 +800,8 @@ __device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
     kq_pro_load<XJ>(a, col, wave, KS, lane, pr);
     kq_raw<WT> r[PF];
 #if GHIP_KQ_EARLY
-    // (GHIP_KQ_KSX: the k_matvec_kq EARLY=2 barrier here too — every wave's activation loads first)
-    if (GHIP_KQ_KSX && GHIP_KQ_EARLY == 2 && a.pro != KQP_COPY) __builtin_amdgcn_s_barrier();
+    // (the k_matvec_kq EARLY=2 barrier here too — every wave's activation loads first: measured
+    // slower, 1,094-1,099 vs 1,104-1,108 tok/s, removed)
 #pragma unroll
     for (int p = 0; p < PF; ++p) r[p] = kq_load<WT, TL>(wrow, p < seg ? wave * seg + p : wave * seg, l);
     bool early = true;
@@ -1326,12 +1242,11 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     const size_t red = a.pro == KQP_NORM ? ((img0 + 15) & ~(size_t)15) + (size_t)a.nsb * 64 * sizeof(double) : 0;
     // few row groups and a long K: split K over 8 waves (the ordered carry keeps the fmaf chain)
     const size_t lds_ks = std::max(std::max((size_t)a.nsb * (292 + 64 * 4 * 2 + 8 * 4 * 2), red), img);
-    // (min super-blocks per row for the split: GHIP_KQ_KSMIN, default 8 — the small q|k / v / o
-    // shapes then fill 256+ workgroups instead of rows/32)
-    static const int ks_min = getenv("GHIP_KQ_KSMIN") ? atoi(getenv("GHIP_KQ_KSMIN")) : 8;
+    // (min super-blocks per row for the split: 8 — the small q|k / v / o shapes then fill 256+
+    // workgroups instead of rows/32)
+    constexpr int ks_min = 8;
     // many columns (the batched prefill): NC = 4 columns per workgroup share the weight loads
-    static const int kq_nc = getenv("GHIP_KQ_NC") ? atoi(getenv("GHIP_KQ_NC")) : 4;
-    if (kq_nc == 4 && a.ncols >= 4 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && 4 * img0 <= 160 * 1024) {
+    if (a.ncols >= 4 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && 4 * img0 <= 160 * 1024) {
         const size_t lds4 = 4 * img0;
         const unsigned gx = (unsigned)std::min<int64_t>((groups + 3) / 4, 4096);
         const dim3 grid(gx, (unsigned)((a.ncols + 3) / 4));
@@ -1349,31 +1264,22 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         if (a.tiled) return d ? go((const void *)k_matmul_kq<T_Q6_K, true, 4, true>) : go((const void *)k_matmul_kq<T_Q6_K, false, 4, true>);
         return d ? go((const void *)k_matmul_kq<T_Q6_K, true, 4, false>) : go((const void *)k_matmul_kq<T_Q6_K, false, 4, false>);
     }
-    // the down shape (64 super-blocks per row, precomputed column, engine layout): round-pipelined
-    // (GHIP_KQ_RR=0: the K-split form below; GHIP_KQ_RRD: rounds in flight per loader, 4 or 8;
-    // Q4_K_M decode, same box: K-split 1,013-1,015 tok/s; rounds 2 / 3 / 4 / 6 / 8 in flight:
-    // 1,032-1,038 / 1,042-1,047 / 1,052 / 1,041-1,044 / 1,017-1,020)
-    static const int kq_rr = getenv("GHIP_KQ_RR") ? atoi(getenv("GHIP_KQ_RR")) : 1;
-    static const int kq_rrd = getenv("GHIP_KQ_RRD") ? atoi(getenv("GHIP_KQ_RRD")) : 4;
-    if (kq_rr && !a.w2 && a.tiled && a.nsb == 64 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && a.x_col_stride % 16 == 0 &&
+    // the down shape (64 super-blocks per row, precomputed column, engine layout): round-pipelined,
+    // 4 rounds in flight per loader (Q4_K_M decode, same box: the K-split form 1,013-1,015 tok/s;
+    // rounds 2 / 3 / 4 / 6 / 8 in flight: 1,032-1,038 / 1,042-1,047 / 1,052 / 1,041-1,044 / 1,017-1,020)
+    if (!a.w2 && a.tiled && a.nsb == 64 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && a.x_col_stride % 16 == 0 &&
         ((uintptr_t)a.x & 15) == 0) {
         const size_t lds_rr = (((size_t)64 * 292 + 15) & ~(size_t)15) + 2 * (1024 + 128) * 4;
         const dim3 grid((unsigned)groups, a.ncols);
-        if (kq_rrd == 8) {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_rr<T_Q4_K, 8, 8>), grid, dim3(KR_NTH), lds_rr, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_rr<T_Q6_K, 8, 8>), grid, dim3(KR_NTH), lds_rr, s, a);
-        } else {
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_rr<T_Q4_K, 8, 4>), grid, dim3(KR_NTH), lds_rr, s, a);
-            else hipLaunchKernelGGL((k_matvec_kq_rr<T_Q6_K, 8, 4>), grid, dim3(KR_NTH), lds_rr, s, a);
-        }
+        if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_rr<T_Q4_K, 8, 4>), grid, dim3(KR_NTH), lds_rr, s, a);
+        else hipLaunchKernelGGL((k_matvec_kq_rr<T_Q6_K, 8, 4>), grid, dim3(KR_NTH), lds_rr, s, a);
         GHIP_CHECK(hipGetLastError());
         return 0;
     }
     if (!a.w2 && groups < 2048 && a.nsb % 8 == 0 && a.nsb >= ks_min && a.nsb <= 64 && lds_ks <= 64 * 1024) {
         const dim3 grid((unsigned)groups, a.ncols);
-        // prefetch depth of a wave's segment (Q4_K_M decode, same box: 2 / 4 / 8 -> 1.158 / 1.174 /
+        // prefetch depth of a wave's segment: 2 (Q4_K_M decode, same box: 2 / 4 / 8 -> 1.158 / 1.174 /
         // 1.214 ms/token; 8 super-blocks of Q6_K raw rows exceed the 63 outstanding loads vmcnt counts)
-        static const int ks_pf = getenv("GHIP_KQ_KSPF") ? atoi(getenv("GHIP_KQ_KSPF")) : 2;
 #define GHIP_KQ_KS(XJ, PF)                                                                                  \
     do {                                                                                                    \
         if (a.tiled) {                                                                                      \
@@ -1385,7 +1291,6 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         }                                                                                                   \
     } while (0)
         if (a.nsb <= 16) GHIP_KQ_KS(2, 2);
-        else if (ks_pf == 4) GHIP_KQ_KS(8, 4);
         else GHIP_KQ_KS(8, 2);
 #undef GHIP_KQ_KS
         GHIP_CHECK(hipGetLastError());
@@ -1395,38 +1300,11 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         set_error("matvec_kq: fused Q8_K prologue takes at most 32 super-blocks per row on this shape");
         return -1;
     }
-    // gate/up (DUAL) with K split in two: 2 row groups per 4-wave workgroup (kq_args::gu2; measured
-    // 1,000 vs 1,010 tok/s for the one-wave-per-group form, so off by default)
-    if (a.w2 && a.gu2 && a.nsb % 2 == 0 && a.nsb >= 2 && a.nsb <= 8 && a.rows % 8 == 0) {
-        const size_t lds2 = std::max(((img0 + 15) & ~(size_t)15) + (size_t)a.nsb * 64 * sizeof(double) +
-                                         (size_t)2 * (2 * 4 * 64 * 2 * 4 + 2 * 4 * 8 * 2 * 4), img);
-        const dim3 grid((unsigned)((groups + 1) / 2), a.ncols);
-        const int ho = a.q8_mode == KQO_NONE ? 0 : a.q8_mode == KQO_QUANT ? 1 : 2;
-#define GHIP_KQ_GU2(HO)                                                                                          \
-    do {                                                                                                         \
-        if (a.tiled) {                                                                                           \
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q4_K, 2, true, HO>), grid, dim3(KQ_THREADS), lds2, s, a); \
-            else hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q6_K, 2, true, HO>), grid, dim3(KQ_THREADS), lds2, s, a);            \
-        } else {                                                                                                 \
-            if (wtype == T_Q4_K) hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q4_K, 2, false, HO>), grid, dim3(KQ_THREADS), lds2, s, a); \
-            else hipLaunchKernelGGL((k_matvec_kq_gu2<T_Q6_K, 2, false, HO>), grid, dim3(KQ_THREADS), lds2, s, a);            \
-        }                                                                                                        \
-    } while (0)
-        if (ho == 0) GHIP_KQ_GU2(0);
-        else if (ho == 1) GHIP_KQ_GU2(1);
-        else GHIP_KQ_GU2(2);
-#undef GHIP_KQ_GU2
-        GHIP_CHECK(hipGetLastError());
-        return 0;
-    }
-    // the output head (single matrix, precomputed image, 32,000 row groups): GHIP_KQ_OGRID=1 gives
-    // every row group its own wave instead of capping the grid at 4,096 workgroups
-    static const int kq_ogrid = getenv("GHIP_KQ_OGRID") ? atoi(getenv("GHIP_KQ_OGRID")) : 0;
-    // GHIP_KQ_PIPE bits (default 2): 1 the gate/up rounds pipelined (measured neutral), 2 the output
-    // head's (Q4_K_M 1,089-1,094 -> 1,103-1,109 tok/s; its grid uncapped alone: 1,091-1,094)
-    static const int kq_pipe = getenv("GHIP_KQ_PIPE") ? atoi(getenv("GHIP_KQ_PIPE")) : 2;
+    // the output head (single matrix, precomputed image, 32,000 row groups): every row group its own
+    // wave (the grid uncapped) and its rounds software-pipelined (Q4_K_M 1,089-1,094 -> 1,103-1,109
+    // tok/s; the uncapped grid alone: 1,091-1,094; the gate/up rounds pipelined too: neutral, removed)
     const bool single_out = !a.w2 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && a.ncols == 1;
-    const bool uncap = single_out && (kq_ogrid || (kq_pipe & 2));
+    const bool uncap = single_out;
     const unsigned grid_x = (unsigned)std::min<int64_t>((groups + 3) / 4, uncap ? (int64_t)1 << 30 : 4096);
     const size_t lds = std::max(img, red);
     if (lds > 64 * 1024) {
@@ -1452,20 +1330,14 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         else GHIP_KQ_LAUNCH_HO(DUAL, XJ, 2, 0);  \
     } while (0)
     const bool wide = a.pro != KQP_COPY && a.nsb > 8;  // more than 2 super-blocks per wave
-    // gate/up rows of 8 super-blocks (Gemma-2B): the software-pipelined rounds (NSB = 8); every row
-    // group gets its own wave when grid_x * 4 covers them (GHIP_KQ_PIPE=0: the round-trip loop)
-    // (measured: the dot phase 6.0 -> 1.9 µs in the stamps, but Q4_K_M 1,044-1,045 vs 1,044-1,054
-    // tok/s without it — the launch stays bandwidth / issue bound; off by default)
-    // GHIP_KQ_PIPE bits: 1 the gate/up (dual), 2 the output head (single, its grid uncapped)
+    // the output head's rows of 8 super-blocks: the software-pipelined rounds (NSB = 8) when every row
+    // group has its own wave (the gate/up in that form measured 1,044-1,045 vs 1,044-1,054 tok/s
+    // without it: dropped)
     const bool pipe8 = GHIP_KQ_EARLY && a.nsb == 8 && !wide && (int64_t)grid_x * (KQ_THREADS / 64) >= groups;
-    if (a.w2 && pipe8 && (kq_pipe & 1)) {
-        if (ho == 0) GHIP_KQ_LAUNCH_HO(true, 2, 0, 8);
-        else if (ho == 1) GHIP_KQ_LAUNCH_HO(true, 2, 1, 8);
-        else GHIP_KQ_LAUNCH_HO(true, 2, 2, 8);
-    } else if (a.w2) {
+    if (a.w2) {
         if (wide) GHIP_KQ_LAUNCH(true, 8);
         else GHIP_KQ_LAUNCH(true, 2);
-    } else if (single_out && pipe8 && (kq_pipe & 2)) {
+    } else if (single_out && pipe8) {
         GHIP_KQ_LAUNCH_HO(false, 2, 0, 8);
     } else {
         if (wide) GHIP_KQ_LAUNCH(false, 8);

@@ -320,7 +320,7 @@ bool attn_o_supported(int wtype, const attn_args &t, const mv_args &o) {
     const int64_t nbt = wtype == T_Q4_0 ? 8 : 4;
     // rr_tiles: one round per row tile (K = 8 block tiles), the image within 2 items per thread
     if (o.n_bt != 8 || o.nb != 8 * nbt || o.nb % 4 || o.nb * 2 + o.nb / 4 > 2 * LF_NTH) return false;
-    if (t.mode != ATTN_PER_HEAD || t.spread || t.v_lds || !t.out_act || !t.out_da || !t.rope_cur || t.out_q8k) return false;
+    if (t.mode != ATTN_PER_HEAD || !t.out_act || !t.out_da || !t.rope_cur || t.out_q8k) return false;
     if (t.hd % 32 || t.hd > 256 || t.ctx % 32 || t.H % t.Hkv || t.dsplit < 1 || t.hd % (32 * t.dsplit) ||
         4 * (t.hd / t.dsplit) > AH_THREADS)
         return false;

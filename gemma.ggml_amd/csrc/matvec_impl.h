@@ -1239,8 +1239,7 @@ int launch_t(const mv_args &a, int grid_x, hipStream_t s) {
     la.ygroups = ygroups;
     // gate/up (KS 1): ONE_SHOT selects the SCL scale-run form (k_matvec) when every wave has at most
     // one row tile and a row tile's scales are one 1 KiB run per matrix; + 2 KiB of LDS per wave
-    static const int scl_env = getenv("GHIP_SCL") ? atoi(getenv("GHIP_SCL")) : GHIP_SCL;  // A/B switch
-    const bool scl = KS == 1 && EPI == EPI_GELU_MUL && scl_env && a.n_bt * 8 * wfmt<WT>::SCALE_BYTES == 1024 &&
+    const bool scl = KS == 1 && EPI == EPI_GELU_MUL && GHIP_SCL && a.n_bt * 8 * wfmt<WT>::SCALE_BYTES == 1024 &&
                      waves_x >= a.n_rt;
     const bool os = one_shot || scl;
     const size_t lds = m.total + (scl ? (size_t)(threads / 64) * 2048 : 0);

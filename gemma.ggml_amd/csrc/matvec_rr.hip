@@ -20,7 +20,7 @@
 namespace ghip {
 namespace {
 
-template <int WT, int PRO, int EPI, int NR, int R, int DD, int PRE = 0, bool EW = false>
+template <int WT, int PRO, int EPI, int NR, int R, int DD>
 __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using G = rr_geom<WT>;
@@ -52,30 +52,17 @@ __global__ void __launch_bounds__(RR_NTH) k_matvec_rr(mv_args a) {
             sb[r % D] = make_uint4(v.x, v.y, 0, 0);
         }
     };
-    // PRE rounds of weights before the activation (every wave: outside any branch, so the counted
-    // waits stay exact; the carrier's copies of loader 0's tiles are L2 hits, never used)
-    constexpr int P = PRE < D ? PRE : D;
-#pragma unroll
-    for (int r = 0; r < P; ++r) issue(r);
+    // (weight rounds issued before the activation, or right behind its loads, measured slower: DESIGN.md §10)
     act_regs<R> ar;
     prefetch_activation<WT, PRO, R, RR_NTH>(a, col, ar);
-    // EW: the ring goes out right behind the activation loads instead of after the image is built —
-    // the activation loads keep the front of the fabric queue (they were issued first), and the
-    // weights' round trip overlaps the image build instead of following it.  Every wave issues
-    // (the carrier's copies of loader 0's tiles are L2 hits, never used), so the build's waits on
-    // the older activation loads stay exact counted waits (no load inside a branch)
-    if (EW) {
-#pragma unroll
-        for (int r = P; r < D; ++r) issue(r);
-    }
     norm_state ns;
     if (!(a.ablate & 1)) ns = build_activation<WT, PRO, R, NSA, RR_NTH>(a, col, smem, m, ar);  // timing ablations only
     if (GHIP_STAMPS && stp && tid == 0) stp[10] = __builtin_amdgcn_s_memrealtime();
     // 1) the rest of the ring (loader w, round r -> block tile w + 8r; D rounds in flight per wave),
     //    issued after the image is used, so these loads may sit in a loader-only branch
-    if (!EW && loader) {
+    if (loader) {
 #pragma unroll
-        for (int r = P; r < D; ++r) issue(r);
+        for (int r = 0; r < D; ++r) issue(r);
     }
     // the norm's check (PRO_NORM / PRO_EMBED) with the weights already in flight: off the path to
     // the first weight load (measured: +0.35-0.45 us on qkv with the check in front of the issue);
@@ -141,26 +128,13 @@ int launch_rr_t(const mv_args &a, hipStream_t s) {
         set_error("matvec(rr): PRO_IMG needs K % 128 == 0");
         return -1;
     }
-    // ring depth (rounds in flight per loader wave; GHIP_RR_D overrides for timing experiments):
-    // measured on the down shape (NR 8), rounds issued after the image: all 8 at once 8.2 us, 6 8.1,
-    // 4 7.9, 2 8.2 — four keep the CU's memory queue full without stalling the first round's issue
-    static const int dd_env = getenv("GHIP_RR_D") ? atoi(getenv("GHIP_RR_D")) : 4;
-    const int dd = (PRO == PRO_IMG || PRO == PRO_F32) && EPI == EPI_ADD && NR >= 8 && dd_env ? dd_env : 64;
-    // (PRE > 0, rounds of weights issued before the image, measured slower: 8.4 / 8.5 vs 7.95 us)
-    // GHIP_RR_EW (round 5): 1 = the ring issued right behind the activation loads (EW), 0 = after
-    // the image is built
-    // (measured: EW 1,449-1,456 vs 1,513-1,517 tok/s — down 8.2 -> 9.2-10.2 us, attn-out 3.57 -> 3.34-3.53:
-    // off by default; GHIP_RR_EW=2 takes it for the one-round EPI_ADD shape (attn-out) only)
-    static const int ew_env = getenv("GHIP_RR_EW") ? atoi(getenv("GHIP_RR_EW")) : 0;
-    const bool ew = ew_env == 1 || (ew_env == 2 && NR == 1 && EPI == EPI_ADD);
-    const void *fn = ew ? (dd == 2 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 2, 0, true>
-                           : dd == 4 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 4, 0, true>
-                           : dd == 6 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 6, 0, true>
-                                     : (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 64, 0, true>)
-                        : (dd == 2 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 2>
-                           : dd == 4 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 4>
-                           : dd == 6 ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 6>
-                                     : (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 64>);
+    // ring depth (rounds in flight per loader wave), measured on the down shape (NR 8), rounds issued
+    // after the image: all 8 at once 8.2 us, 6 8.1, 4 7.9, 2 8.2 — four keep the CU's memory queue
+    // full without stalling the first round's issue.  (Rounds issued before the image: 8.4 / 8.5 vs
+    // 7.95 us; the ring right behind the activation loads: decode 1,449-1,456 vs 1,513-1,517 tok/s —
+    // both removed.)
+    constexpr bool deep = (PRO == PRO_IMG || PRO == PRO_F32) && EPI == EPI_ADD && NR >= 8;
+    const void *fn = deep ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 4> : (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 64>;
     if (lds > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     mv_args la = a;
     void *args[] = {(void *)&la};

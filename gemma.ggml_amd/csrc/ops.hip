@@ -513,18 +513,10 @@ __global__ void __launch_bounds__(ATT_THREADS) k_attn_decode(attn_args a) {
 __global__ void __launch_bounds__(AH_THREADS) k_attn_head(attn_args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int S = a.dsplit, G = a.H / a.Hkv;
-    // one inlined copy of the body (a second call site, for the XCD-spread mapping, doubled the
-    // kernel's code: measured slower and removed); spread: block b -> head b % H
-    int h, sp;
-    if (a.spread) {
-        h = (int)blockIdx.x % a.H;
-        sp = (int)blockIdx.x / a.H;
-    } else {
-        const int hs = blockIdx.x >> 3;
-        h = hs / S;
-        sp = hs % S;
-        if ((int)(blockIdx.x & 7) != ((h / G) & 7)) return;  // the G*S workgroups of a kv head share an XCD (speed only)
-    }
+    // one inlined copy of the body (a second call site doubled the kernel's code: measured slower,
+    // DESIGN.md §10)
+    const int hs = blockIdx.x >> 3, h = hs / S, sp = hs % S;
+    if ((int)(blockIdx.x & 7) != ((h / G) & 7)) return;  // the G*S workgroups of a kv head share an XCD (speed only)
     attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false>(a, h, smem, nullptr, sp);
 }
 
@@ -885,21 +877,11 @@ int launch_attn_decode(const attn_args &a, hipStream_t s) {
             set_error("attn_decode: context too long for the LDS image");
             return -1;
         }
-        // the workgroup's V rows by LDS-DMA when they fit beside the scores (GHIP_ATT_VDMA=1; off by
-        // default: measured neutral to -0.5 % per decode step)
-        const char *vdma_s = getenv("GHIP_ATT_VDMA");  // read per launch (graphs bake it in at capture)
-        const bool vdma_env = vdma_s && atoi(vdma_s) != 0;
-        attn_args la = a;
-        const size_t v_off = (lds + 15) & ~(size_t)15, v_bytes = (size_t)(a.hd / a.dsplit) * ATT_VDMA_PITCH;
-        if (vdma_env && v_off + v_bytes <= 160 * 1024) {
-            la.v_lds = (uint32_t)v_off;
-            lds = v_off + v_bytes;
-        }
+        // (V rows by LDS-DMA, and the heads spread over the XCDs, measured neutral / slower: removed,
+        // DESIGN.md §10)
         if (lds > 64 * 1024)
             GHIP_CHECK(hipFuncSetAttribute((const void *)k_attn_head, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        const char *xcd_s = getenv("GHIP_ATT_XCD");  // 1: heads spread over the XCDs (attn_args::spread)
-        la.spread = xcd_s && atoi(xcd_s) == 1;
-        hipLaunchKernelGGL(k_attn_head, dim3((la.spread ? 1 : 8) * a.H * a.dsplit), dim3(AH_THREADS), lds, s, la);
+        hipLaunchKernelGGL(k_attn_head, dim3(8 * a.H * a.dsplit), dim3(AH_THREADS), lds, s, a);
         GHIP_CHECK(hipGetLastError());
         return 0;
     }

@@ -932,15 +932,10 @@ int launch_quant_rows(int mode, const qrow_args &a, int T, hipStream_t s) {
         case QR_NORM: hipLaunchKernelGGL(k_quant_rows<QR_NORM>, dim3(T), dim3(256), 0, s, a); break;
         case QR_EMBED_NORM: hipLaunchKernelGGL(k_quant_rows<QR_EMBED_NORM>, dim3(T), dim3(256), 0, s, a); break;
         case QR_GELU: {
-            // the LDS-table form (default; GHIP_QR_GELU_LDS=0: the per-row form).  T = 2048 exact
-            // prefill 78.4 -> 77.5 ms (this kernel 109 -> ~57 us per layer)
-            const char *env = getenv("GHIP_QR_GELU_LDS");
-            if (!env || atoi(env)) {
-                if (allow_full_lds((const void *)k_quant_gelu_lds, LDS_SLOT_GELU_LDS)) return -1;
-                hipLaunchKernelGGL(k_quant_gelu_lds, dim3((unsigned)std::min(T, 256)), dim3(QG_THREADS), 65536 * 2, s, a, T);
-            } else {
-                hipLaunchKernelGGL(k_quant_rows<QR_GELU>, dim3(T), dim3(256), 0, s, a);
-            }
+            // the LDS-table form (the per-row form k_quant_rows<QR_GELU>: T = 2048 exact prefill
+            // 78.4 vs 77.5 ms; this kernel 109 -> ~57 us per layer)
+            if (allow_full_lds((const void *)k_quant_gelu_lds, LDS_SLOT_GELU_LDS)) return -1;
+            hipLaunchKernelGGL(k_quant_gelu_lds, dim3((unsigned)std::min(T, 256)), dim3(QG_THREADS), 65536 * 2, s, a, T);
             break;
         }
         default: set_error("quant_rows: bad mode"); return -1;

@@ -438,10 +438,7 @@ static std::atomic<int> g_kq_gemm_min{-1};
 int kq_gemm_min() {
     const int v = g_kq_gemm_min.load();
     if (v >= 0) return v;
-    static const int env = getenv("GHIP_KQ_MFMA") && !atoi(getenv("GHIP_KQ_MFMA"))
-                               ? INT_MAX
-                               : (getenv("GHIP_KQ_MFMA_MIN") ? atoi(getenv("GHIP_KQ_MFMA_MIN")) : 8);
-    return env;
+    return 8;  // default: the MFMA GEMM from 8 columns (hpc_set_kq_gemm_min moves it)
 }
 void set_kq_gemm_min(int v) { g_kq_gemm_min.store(v); }
 

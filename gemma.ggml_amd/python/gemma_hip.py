@@ -29,7 +29,7 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact", "gemma_kq_time", "hpc_graph_compute",
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
-           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_att_o", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs",
+           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_att_o", "gemma_engine_set_option", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs",
            "gemma_tp_unique_id", "gemma_engine_create_tp", "gemma_engine_tp_info", "gemma_engine_set_persist_timeout",
            "gguf_init_from_file", "gguf_free", "gguf_get_n_kv", "gguf_get_key", "gguf_get_kv_type",
            "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
@@ -118,6 +118,8 @@ def lib():
     L.gemma_engine_set_plan.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     L.gemma_engine_set_fuse.argtypes = [vp, C.c_int]
     L.gemma_engine_set_att_o.argtypes = [vp, C.c_int]
+    L.gemma_engine_set_option.restype = C.c_int
+    L.gemma_engine_set_option.argtypes = [vp, C.c_char_p, C.c_int]
     L.gemma_engine_set_persist.argtypes = [vp, C.c_int]
     L.gemma_engine_persist_err.argtypes = [vp, vp, C.c_int]
     L.gemma_engine_set_persist_timeout.argtypes = [vp, C.c_uint]
@@ -318,6 +320,10 @@ class Engine:
         """fused layer front on (1) / off (0) / unchanged (-1); returns the sticky hand-off timeout
         word (0 = every in-launch hand-off completed in time)"""
         return self.L.gemma_engine_set_fuse(self.h, front)
+
+    def set_option(self, name, value):
+        """a selectable variant (include/gemma_hpc.h gemma_engine_set_option); drops the decode graph"""
+        self._chk(self.L.gemma_engine_set_option(self.h, name.encode(), int(value)), f"set_option({name})")
 
     def set_att_o(self, on=-1):
         """decode attention + attn-out in one launch per layer: on 1 / off 0 / keep -1; returns the setting"""

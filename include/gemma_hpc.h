@@ -124,6 +124,13 @@ int gemma_engine_set_fuse(gemma_engine *e, int fuse_front); /* fused layer front
    off 0 / keep -1; returns the setting.  A hand-off timeout is reported by gemma_engine_step (-1) and
    turns it off. */
 int gemma_engine_set_att_o(gemma_engine *e, int on);
+/* The measured variants that stay selectable (tests, A/B), set through the API rather than the
+   environment: "kq_fuse" (K-quant Q8_K INIT plan 0..6), "kq_dual" (gate+up one launch), "kq_pair"
+   (q|k and v one launch), "kq_abl" (timing ablation, wrong results), "att_mx" (exact prefill attention
+   on the f32 matrix cores; 0 = the row form), "att_dsplit" (decode attention workgroups per head:
+   1/2/4/8), "ks_small" / "ks_down" (launch-plan K split defaults), "grid_big", and the
+   gemma_engine_time diagnostics "time_hot" / "ablate".  Returns 0, -1 (unknown name or bad value). */
+int gemma_engine_set_option(gemma_engine *e, const char *name, int value);
 int gemma_engine_graph_kernels(gemma_engine *e);            /* kernel launches per decode token (captured graph) */
 /* the decode step's layers as ONE persistent launch (opt-in: off by default, GHIP_PERSIST=1 or this
  * call; -1 = keep): returns 1 when it runs this engine's steps, 0 when not (hpc_last_error says why:

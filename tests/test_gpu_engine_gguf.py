@@ -172,17 +172,16 @@ def test_kquant_engine_batched_prefill_gemma2b_layer_shapes(mfma):
 @gpu
 @pytest.mark.parametrize("fuse,dual,pair", [(5, 1, 1), (5, 0, 0), (6, 1, 1), (3, 1, 1), (3, 1, 0), (3, 0, 1),
                                            (4, 1, 1), (2, 1, 1), (1, 1, 1), (0, 0, 0)])
-def test_kquant_engine_gemma2b_layer_shapes(monkeypatch, fuse, dual, pair):
+def test_kquant_engine_gemma2b_layer_shapes(fuse, dual, pair):
     # fuse: the Q8_K INIT plan (enqueue_step_kq; 5 default) — 3 norms in prologues + quantizations handed off,
     # 2 the producer tails (hand-off), 1 the consumer prologues,
-    # 0 separate norm / quantize launches; dual: gate and up in one launch
-    monkeypatch.setenv("GHIP_KQ_FUSE", str(fuse))
-    monkeypatch.setenv("GHIP_KQ_DUAL", str(dual))
-    monkeypatch.setenv("GHIP_KQ_PAIR", str(pair))  # q|k and v in one launch
-    monkeypatch.setenv("GHIP_KQ_GU2", "1" if fuse == 3 else "0")  # gate/up with K split in two
+    # 0 separate norm / quantize launches; dual: gate and up in one launch; pair: q|k and v in one launch
     shape = dict(O.GEMMA_2B, n_layer=2, n_vocab=8192)
     m = O.Model(O.make_config(shape, n_ctx=256, kmix=1))
     e = G.Engine(shape, n_ctx=256, wtype=G.GGML_TYPE_Q4_K)
+    e.set_option("kq_fuse", fuse)
+    e.set_option("kq_dual", dual)
+    e.set_option("kq_pair", pair)
     _compare(e, m, shape, 13, 6)
     e.close()
     m.close()

@@ -128,7 +128,7 @@ def _run(tmp_path, shape, wtype, n_prompt, n_decode, ctx, gguf=False, kmix=0, fa
         args = [DRIVER, str(wpath), str(ppath), str(opath)] + [str(shape[k]) for k in
                 ("n_layer", "n_embd", "n_head", "n_head_kv", "head_dim", "n_ff", "n_vocab")] + [str(ctx), str(wtype),
                                                                                               str(n_decode)]
-    env = dict(os.environ, GHIP_GGML_FAST=str(fast), GHIP_GGML_FAST_WHY="1", DRIVER_NO_REGISTER=str(1 - register))
+    env = dict(os.environ, GHIP_GGML_FAST=str(fast), GHIP_GGML_DEBUG="1", DRIVER_NO_REGISTER=str(1 - register))
     if m2 is not None:
         env["DRIVER_SECOND"] = str(tmp_path / "w2.bin")
     r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)

@@ -162,17 +162,17 @@ def test_engine_adversarial_embedding(tmp_path, wtype, fmt):
 
 @gpu
 @pytest.mark.parametrize("fuse", [5, 0, 2])
-def test_kquant_engine_adversarial_embedding(tmp_path, monkeypatch, fuse):
+def test_kquant_engine_adversarial_embedding(tmp_path, fuse):
     """Q8_K INIT plans (engine.cpp enqueue_step_kq): 5 norms in the consumers' prologues, 0 as
     k_norm_q8K launches, 2 in the producers' hand-off tails"""
     import gemma_hip as G
     from test_gpu_ggml_graph import write_gguf
-    monkeypatch.setenv("GHIP_KQ_FUSE", str(fuse))
     m = O.Model(O.make_config(KSHAPE, n_ctx=128, kmix=1))
     _poke_model(m, "q6_K", "q8_K", KSHAPE["n_embd"])
     path = tmp_path / "adv_kq.gguf"
     write_gguf(m, KSHAPE, path, 1)
     e = G.Engine.from_gguf(str(path), n_ctx=128)
+    e.set_option("kq_fuse", fuse)
     _engine_vs_oracle(e, m, _prompt(KSHAPE["n_vocab"], 10), 5)
     e.close()
     m.close()

@@ -43,11 +43,13 @@ def test_synthetic_out_gain_matches_oracle():
     _check_decode(O.TINY, n_prompt=7, n_decode=12, n_ctx=128, out_gain=4.0)
 
 
-def _check_decode(shape, n_prompt, n_decode, n_ctx, wtype=O.Q4_0, use_graph=True, out_gain=0.0):
+def _check_decode(shape, n_prompt, n_decode, n_ctx, wtype=O.Q4_0, use_graph=True, out_gain=0.0, options=None):
     m = O.Model(O.make_config(shape, n_ctx=n_ctx, wtype=wtype, out_gain=out_gain))
     prompt = O.make_prompt(n_prompt, shape["n_vocab"])
     seq_ref, lg_ref = m.generate(prompt, n_decode)
     e = _engine(shape, n_ctx=n_ctx, wtype=wtype, out_gain=out_gain)
+    for k, v in (options or {}).items():
+        e.set_option(k, v)
     e.begin(prompt)
     lg = e.step(n_prompt + n_decode, want_logits=True, use_graph=use_graph)
     toks = e.tokens()
@@ -94,18 +96,16 @@ def test_decode_gemma2b_attention_forms_bitexact(attention):
 
 
 @gpu
-@pytest.mark.parametrize("dsplit", ["4", "1"])
-def test_decode_attention_v_dma_bitexact(monkeypatch, dsplit):
-    """the decode attention with its V rows copied into LDS by DMA (GHIP_ATT_VDMA=1, off by default),
-    4 and 1 workgroups per head, through positions past 32 (several V steps) and the own-position
-    patch; tiny GQA and Gemma-2B shapes against the oracle"""
-    monkeypatch.setenv("GHIP_ATT_VDMA", "1")
-    monkeypatch.setenv("GHIP_ATT_DSPLIT", dsplit)
+@pytest.mark.parametrize("dsplit", [8, 2, 1])
+def test_decode_attention_dsplit_bitexact(dsplit):
+    """the decode attention with 8 / 2 / 1 workgroups per head (option att_dsplit; 4 is the default),
+    through positions past 32 (several V steps) and past 256 (the KQV's long-context branch), the
+    own-position patch; tiny GQA and Gemma-2B shapes against the oracle"""
     O.lib().orc_set_threads(16)
-    _check_decode(dict(O.TINY, n_head=4, n_head_kv=2, n_embd=1024), n_prompt=5, n_decode=40, n_ctx=128)
-    # past 256 positions the KQV reads V from the cache again (the LDS copy holds 256)
-    _check_decode(dict(O.TINY, n_head=4, n_head_kv=2, n_embd=1024), n_prompt=250, n_decode=20, n_ctx=512)
-    _check_decode(O.GEMMA_2B, n_prompt=6, n_decode=3, n_ctx=256)
+    opt = {"att_dsplit": dsplit}
+    _check_decode(dict(O.TINY, n_head=4, n_head_kv=2, n_embd=1024), n_prompt=5, n_decode=40, n_ctx=128, options=opt)
+    _check_decode(dict(O.TINY, n_head=4, n_head_kv=2, n_embd=1024), n_prompt=250, n_decode=20, n_ctx=512, options=opt)
+    _check_decode(O.GEMMA_2B, n_prompt=6, n_decode=3, n_ctx=256, options=opt)
 
 
 @gpu

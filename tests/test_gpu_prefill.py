@@ -238,7 +238,7 @@ def test_prefill_exact_gemma7b_layers():
                                            n_vocab=4096), 333),
                                      (dict(n_layer=1, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, n_ff=2048,
                                            n_vocab=4096), 129)])
-def test_prefill_attention_mfma_equals_rows(shape, T, monkeypatch):
+def test_prefill_attention_mfma_equals_rows(shape, T):
     """The exact prefill attention on the f32 matrix cores (attn_mx.hip) against the v_fma_mix row
     form (k_attn_rows): every prompt row's logits and the decode that continues from the cache
     bit-identical (G = 8 / 2 / 1 query heads per kv head; T not a multiple of 16 or 32)."""
@@ -246,8 +246,8 @@ def test_prefill_attention_mfma_equals_rows(shape, T, monkeypatch):
     prompt = O.make_prompt(T, shape["n_vocab"], seed=3)
     out = {}
     for mx in ("1", "0"):
-        monkeypatch.setenv("GHIP_ATT_MX", mx)
         e = G.Engine(shape, n_ctx=(T + 64) // 32 * 32 + 32, device=0)
+        e.set_option("att_mx", int(mx))
         e.begin(prompt)
         tok, last, allv = e.prefill(T, want_all=True, exact=True)
         lg = e.step(3, want_logits=True, use_graph=True)
