@@ -571,6 +571,8 @@ static int enqueue_step(gemma_engine *e) {
             f.o.x = e->att_act; f.o.x_da = e->att_da; f.o.y = e->sa + r0; f.o.resid = e->x + r0;
             f.cnt = e->ao_cnt + (size_t)il * 16 * 32;
             f.err = e->ao_err;
+            f.t.dbg_t = nullptr;  // (the fused kernel's stamps: 16 per workgroup in the attention region)
+            f.dbg_t = stamp_region(e, il, 1);
             if (attn_o_supported(wt, f.t, f.o)) {
                 if (launch_attn_o(wt, f, s)) return -1;
                 const size_t tap = (size_t)il * (e->qkv_rows + e->qw + E);
@@ -1452,12 +1454,12 @@ extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_
         n -= 1;
         if (ensure_graph(e)) return -1;
     }
-    // Flow control: at most FC_EVERY * FC_SLOTS decode graphs (x 92 kernels) queued ahead of the GPU.
-    // Before the bound, a long step queued every launch at once (a 176-step call: ~16,000 dispatch
-    // packets); rocprofv3 --kernel-trace crashed inside the HIP runtime's graph-launch path on exactly
-    // such calls (175 and 191 queued graphs) and completed on calls of <= 127.  Waiting
-    // on the event of the launch FC_EVERY * FC_SLOTS back never drains the queue, so the GPU never
-    // idles: the host only stops running ahead.
+    // Flow control: at most FC_EVERY * FC_SLOTS decode graphs (x 92 kernels) queued ahead of the GPU,
+    // so a long call never parks thousands of dispatch packets in the HW queue.  Waiting on the event
+    // of the launch FC_EVERY * FC_SLOTS back never drains the queue: the GPU never idles, the host only
+    // stops running ahead.  (It was added as the first lead on the rocprofv3 crash of DESIGN.md §11 and
+    // did not cure it: that crash is the profiler reading past the end of the 1 MiB AQL ring when a
+    // HIP 7.2 graph launch's packet batch wraps around it, whatever the queue depth.)
     constexpr int FC_EVERY = 16, FC_SLOTS = 4;
     for (int i = 0; i < n; ++i) {
         if (use_graph && !logits && i % FC_EVERY == 0) {
@@ -1768,23 +1770,24 @@ extern "C" int gemma_engine_tune(gemma_engine *e, int iters) {
         }
         e->plan[cls] = win;
         if (cls != MC_LOGITS) best = best_cls;
-        if (cls == MC_O && rc == 0 && e->ag.nwg && e->cfg.n_ctx <= 2048 && e->cfg.head_dim <= 256) {
-            // attention form (feeds attn-out): one workgroup per head vs the XCD-colocated split
-            e->att_mode ^= 1;
-            const double t = trial();
+        // on / off switches: the incumbent re-measured beside the challenger and the same 0.2 %
+        // hysteresis as the plans (a bare t < best flipped on noise).  Every condition is
+        // structural, never a measured outcome, so every rank of a TP job runs the same trials.
+        auto toggle = [&](auto flip) {
+            if (rc) return;
+            const double inc = trial();
+            flip();
+            const double t = inc < 0 ? -1.0 : trial();
             if (t < 0) rc = -1;
-            if (t >= 0 && t < best) best = t;
-            else e->att_mode ^= 1;
-        }
+            if (t >= 0 && t < inc * 0.998) best = t;
+            else flip();
+        };
+        if (cls == MC_O && e->ag.nwg && e->cfg.n_ctx <= 2048 && e->cfg.head_dim <= 256)
+            toggle([&] { e->att_mode ^= 1; });  // attention form: one workgroup per head vs the split
         // the producer-written activation image, at the winning launch shape
-        const bool img_ok = (cls == MC_O && e->att_act && att_img_ok(e)) || (cls == MC_DOWN && e->h_act);
-        if (img_ok && rc == 0) {
-            e->plan[cls].img ^= 1;
-            const double t = trial();
-            if (t < 0) rc = -1;
-            if (t >= 0 && t < best) best = t;
-            else e->plan[cls].img ^= 1;
-        }
+        if ((cls == MC_O && e->att_act) || (cls == MC_DOWN && e->h_act)) toggle([&] { e->plan[cls].img ^= 1; });
+        // attention + attn-out in one launch (takes effect with the image and the rr attn-out form)
+        if (cls == MC_O && e->ao_cnt && e->n_virtual == 1) toggle([&] { e->att_o ^= 1; });
     }
     drop_graph(e);
     (void)hipEventDestroy(t0);

@@ -319,6 +319,7 @@ struct attn_o_args {
     unsigned *cnt = nullptr;  // this layer's counters: 8 replicas + the consumers' done count, 128 B apart;
                               // zero before the launch, and the launch leaves them zero
     int *err = nullptr;       // sticky: a hand-off poll timed out (err[0]; err[1..4] diagnostics)
+    unsigned long long *dbg_t = nullptr;  // stamps build: 16 s_memrealtime per workgroup
 };
 bool attn_o_supported(int wtype, const attn_args &t, const mv_args &o);
 int launch_attn_o(int wtype, const attn_o_args &f, hipStream_t s);

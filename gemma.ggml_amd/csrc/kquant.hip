@@ -224,8 +224,10 @@ __device__ __forceinline__ void stage_q8k(const kq_args &a, uint8_t *xs, int col
 // The column's Q8_K image in LDS = ggml's INIT for K-quant src0, fused into the matvec (no separate
 // k_norm_q8K / k_quant_q8_K launch): KQP_COPY copies precomputed Q8_K rows (x); KQP_F32 runs
 // quantize_row_q8_K on f32 xf (k_quant_q8_K: one wave per super-block); KQP_NORM first applies
-// rms_norm(xf)*norm_w with k_norm_q8K's exact double-sum order (partials of 4 consecutive squares,
-// the pairwise tree h = (n+1)/2), so the bytes equal the separate kernels'.
+// rms_norm(xf)*norm_w.  Its double sum of squares is a DPP wave sum plus one LDS word per wave (any
+// order): rms_mean_certain (device_util.h) proves the resulting float mean equal to
+// ggml's sequential sum's, else seq_sumsq_wave runs ggml's own order — so the bytes equal the
+// separate kernels' (k_norm_q8K takes the same certified-tree-or-sequential path).
 // Two halves: kq_pro_load issues every f32 load of this wave's super-blocks (wave w takes
 // w, w+nw, ...; at most XJ of them; surplus slots load a clamped block and are ignored) BEFORE the
 // weight prologue loads, so one counted wait covers them and the serial load -> quantize round
@@ -437,10 +439,12 @@ __device__ __forceinline__ bool kq_count(unsigned *cnt, unsigned target, int lan
     return true;
 }
 
-// k_norm_q8K's sum over the column: partial p = the squares of elements 4p..4p+3 (p = j*64 + lane,
-// held as part[j]), then the pairwise tree h = (n+1)/2 — levels whose halves are whole 64-partial
-// rows combine registers, the last six (n <= 64) combine lanes; anything else goes through `lds`
-// (free: every dot loop of the grid has finished).  Returns the total in every lane.
+// The hand-off tail's sum of squares over the column: partial p = the squares of elements 4p..4p+3
+// (p = j*64 + lane, held as part[j]), then a pairwise tree h = (n+1)/2 — levels whose halves are whole
+// 64-partial rows combine registers, the last six (n <= 64) combine lanes; anything else goes through
+// `lds` (free: every dot loop of the grid has finished).  Returns the total in every lane.  The tree's
+// order is not ggml's: the caller keeps its mean only when rms_mean_certain proves it equal to the
+// sequential sum's, and otherwise runs seq_sumsq_wave.
 __device__ __forceinline__ double kq_tree(double part[8], int J, int lane, double *lds) {
     int n = J * 64;
     bool regs = true;

@@ -76,9 +76,21 @@ __device__ __forceinline__ void signal_after_stores(unsigned *cnt) {
 //                 Q8_0 image (sc1 loads), EPI_ADD with plain stores (consumed after the launch).
 // Both tiles' weights are always issued (a missing second tile re-reads the first: L2 hits) so the
 // compiler's counted waits stay exact.
-template <int WT, int PRO, int EPI, bool WAIT>
+struct no_hook {
+    __device__ void operator()() const {}
+};
+// one 16-B load through to the handed-off bytes (sc1: past this CU's L1), waited for here
+__device__ __forceinline__ uint4 ld_sc1_16(const void *p) {
+    uint4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+// on_poll: run by thread 0 right after its poll matched (before the workgroup's barrier)
+template <int WT, int PRO, int EPI, bool WAIT, typename Hook = no_hook>
 __device__ void rr_tiles(const mv_args &a, int64_t rt0, int64_t rt1, uint8_t *smem, const unsigned *wcnt,
-                         unsigned wtarget, int *err) {
+                         unsigned wtarget, int *err, unsigned long long *stp = nullptr, Hook on_poll = Hook()) {
+#define RT_STAMP(i) \
+    if (GHIP_STAMPS && stp && threadIdx.x == 0) stp[i] = __builtin_amdgcn_s_memrealtime()
     using G = rr_geom<WT>;
     constexpr int BT = G::BT, SB = wfmt<WT>::SCALE_BYTES, R = 1;
     constexpr bool NSA = true;
@@ -112,21 +124,30 @@ __device__ void rr_tiles(const mv_args &a, int64_t rt0, int64_t rt1, uint8_t *sm
     }
     if (WAIT) {
         static_assert(!WAIT || PRO == PRO_IMG, "the handed-off activation is a Q8_0 image");
-        if (tid == 0) poll_counters(wcnt, 1, [&](int) { return wtarget; }, err, 2);
+        RT_STAMP(1);
+        if (tid == 0) {
+            poll_counters(wcnt, 1, [&](int) { return wtarget; }, err, 2);
+            on_poll();
+        }
         __syncthreads();
+        RT_STAMP(2);
+        // the image: one 16-B sc1 load per item, only by the threads that own an item (build_activation
+        // stores items < T only; clamped duplicates were 8x the loads on one line)
         const int64_t T = a.nb * 2 + a.nb / 4;  // image items (host: T <= 2 * LF_NTH)
 #pragma unroll
         for (int i = 0; i < 2 * R; ++i) {
-            int64_t it = tid + (int64_t)i * LF_NTH;
-            it = it < T ? it : T - 1;
-            const uint32_t *p = (const uint32_t *)img_item(a, it);
+            const int64_t it = tid + (int64_t)i * LF_NTH;
             float *dst = (i & 1) ? &ar.w[i >> 1][0] : &ar.x[i >> 1][0];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) dst[k] = __builtin_bit_cast(float, ld_sc1_u(p + k));
+            if (it < T) {
+                const uint4 v = ld_sc1_16(img_item(a, it));
+                dst[0] = __builtin_bit_cast(float, v.x); dst[1] = __builtin_bit_cast(float, v.y);
+                dst[2] = __builtin_bit_cast(float, v.z); dst[3] = __builtin_bit_cast(float, v.w);
+            }
         }
         build_activation<WT, PRO, R, NSA, LF_NTH>(a, 0, smem, m, ar);  // PRO_IMG: no norm
     }
     lds_barrier();
+    RT_STAMP(3);
     if (wave == RR_NL) __builtin_amdgcn_s_setprio(3);
     auto slot_s = [&](int r) { return (float *)(smem + slot0 + (size_t)(r & 1) * G::SLOT); };
     auto slot_d = [&](int r) { return (float *)(smem + slot0 + (size_t)(r & 1) * G::SLOT + G::S_BYTES); };
@@ -159,6 +180,8 @@ __device__ void rr_tiles(const mv_args &a, int64_t rt0, int64_t rt1, uint8_t *sm
         }
         __builtin_amdgcn_s_setprio(0);
     }
+    RT_STAMP(4);
+#undef RT_STAMP
 }
 
 // Workgroup roles over a grid of G = one workgroup per CU (every workgroup resident: the waiters
@@ -193,7 +216,7 @@ __global__ void __launch_bounds__(LF_NTH) k_layer_front(front_args f) {
                     if (threadIdx.x == 0) __hip_atomic_store((gu32_t *)f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(4);
             }
         }
         __syncthreads();
@@ -235,19 +258,22 @@ __global__ void __launch_bounds__(LF_NTH) k_attn_o(attn_o_args f) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int b = blockIdx.x, S = f.t.dsplit, H = f.t.H, G = H / f.t.Hkv;
     const int hs = b >> 3, h = hs / S, sp = hs % S, att = (h / G) & 7, j = b & 7;
+    unsigned long long *stp = GHIP_STAMPS && f.dbg_t ? f.dbg_t + (int64_t)b * 16 : nullptr;
+    if (GHIP_STAMPS && stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
     if (j == att) {  // the attention of (head h, dims split sp), exactly k_attn_head's body
         attn_head_dev<AH_THREADS, false, AH_KPF, AH_VPF, false, true>(f.t, h, smem, nullptr, sp);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's image stores have landed
         __syncthreads();
         if (threadIdx.x < LF_NREP) add_cnt(f.cnt + threadIdx.x * LF_CS);
+        if (GHIP_STAMPS && stp && threadIdx.x == 0) stp[5] = __builtin_amdgcn_s_memrealtime();
         return;
     }
     const int nc = (int)(gridDim.x >> 3) * 7;        // consumers (launcher: nc <= n_rt <= 2 nc)
     const int c = hs * 7 + (j < att ? j : j - 1);   // this consumer's index
     const int no = (int)f.o.n_rt, P = H * S;
-    rr_tiles<WT, PRO_IMG, EPI_ADD, true>(f.o, c, c + nc < no ? c + nc : -1, smem, f.cnt + (c & (LF_NREP - 1)) * LF_CS,
-                                         (unsigned)P, f.err);
-    if (threadIdx.x == 0) {
+    // the done count right behind the poll (its returned add and the resets overlap this
+    // workgroup's image and rounds instead of trailing the launch)
+    auto done = [&] {
         const unsigned old = __hip_atomic_fetch_add((gu32_t *)(f.cnt + AO_DONE * LF_CS), 1u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
         if (old == (unsigned)nc - 1) {  // every consumer is past its poll: return the counters to zero
@@ -256,7 +282,9 @@ __global__ void __launch_bounds__(LF_NTH) k_attn_o(attn_o_args f) {
             __hip_atomic_fetch_sub((gu32_t *)(f.cnt + AO_DONE * LF_CS), (unsigned)nc, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
-    }
+    };
+    rr_tiles<WT, PRO_IMG, EPI_ADD, true>(f.o, c, c + nc < no ? c + nc : -1, smem, f.cnt + (c & (LF_NREP - 1)) * LF_CS,
+                                         (unsigned)P, f.err, stp, done);
 }
 
 }  // namespace

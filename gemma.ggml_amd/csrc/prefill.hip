@@ -1027,8 +1027,13 @@ int allow_full_lds(const void *fn, int slot) {
         set_error("allow_full_lds: bad slot or device");
         return -1;
     }
+    // the device's opt-in limit (160 KiB on gfx950; a smaller-LDS target keeps launching what fits
+    // instead of failing on an attribute it cannot grant — ADVICE r5)
     std::call_once(once[slot][dev], [&] {
-        err[slot][dev] = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        int optin = 0;
+        err[slot][dev] = hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev);
+        if (err[slot][dev] == hipSuccess && optin > 64 * 1024)
+            err[slot][dev] = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, optin);
     });
     GHIP_CHECK(err[slot][dev]);
     return 0;
