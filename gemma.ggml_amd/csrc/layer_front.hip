@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(LF_NTH) k_layer_front(front_args f) {
                     if (threadIdx.x == 0) __hip_atomic_store((gu32_t *)f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(4);
+                __builtin_amdgcn_s_sleep(1);
             }
         }
         __syncthreads();
