@@ -320,6 +320,19 @@ def latest_profile(name):
     return os.path.join(pdir, name)
 
 
+def load_graph_profile():
+    """the per-class table of the benched path (hipGraph replays under rocprofv3 --kernel-trace,
+    scripts/decode_prof.py + scripts/decode_classes.py) from the newest profiles/rNN, or None"""
+    path = latest_profile("decode_kernels_graph.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        d["source_file"] = os.path.relpath(path, ROOT)
+        return d
+    except Exception:
+        return None
+
+
 def load_traffic(kernel_id):
     """HBM bytes per launch of the roofline kernel from the committed PMC summary (or None)."""
     path = latest_profile("pmc_traffic.json")
@@ -628,7 +641,8 @@ def main():
     achieved = algo / (us * 1e-6) / 1e9
     traffic = load_traffic(dominant)
     # measured HBM read roofline on this box: streaming read of 4 GiB (defeats the Infinity Cache)
-    hbm_measured = eng.L.gemma_hbm_read_gbs(local_rank, 4 << 30, 5)
+    hbm_probes = [eng.L.gemma_hbm_read_probe(local_rank, 4 << 30, 5, v) for v in (0, 1)]
+    hbm_measured = max(hbm_probes)
 
     log('cpu baseline')
     cpu = None
@@ -676,8 +690,12 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "avg_us": round(us, 3), "algo_bytes": int(algo),
                          "measured_peak": round(hbm_measured, 1),
+                         "measured_peak_probes": {"vgpr_loads_nt": round(hbm_probes[0], 1), "lds_dma_nt": round(hbm_probes[1], 1),
+                                                  "what": "4 GiB streaming reads; measured_peak = the faster (the guide's "
+                                                          "float4 copy: 6.29 TB/s)"},
                          "frac_of_measured": round(achieved / hbm_measured, 4) if hbm_measured > 0 else None,
                          "timing": "hipEvents over back-to-back launches rotating over the 18 layers' matrices",
+                         "graph_profile": load_graph_profile(),
                          "classes": {KERNEL_NAMES[k]: {"avg_us": round(v[0], 3), "algo_bytes": int(v[1]),
                                                        "GB/s": round(v[1] / (v[0] * 1e-6) / 1e9, 1),
                                                        "frac": round(v[1] / (v[0] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),

@@ -2428,7 +2428,10 @@ extern "C" int gemma_test_rms_norm(int kind, const float *x, const float *w, int
 
 // Measured HBM read roofline: a streaming read of `bytes` (>= 4 GB defeats the
 // Infinity Cache), `iters` passes timed with hipEvents; returns GB/s (negative on error).
-extern "C" double gemma_hbm_read_gbs(int device, size_t bytes, int iters) {
+// measured HBM read rate (GB/s) of one probe: variant 0 = 16-B nontemporal loads into VGPRs (8 in
+// flight per lane), 1 = LDS-DMA (global_load_lds_dwordx4 nt, 16 KiB in flight per wave); a buffer
+// far beyond the 256 MB Infinity Cache
+extern "C" double gemma_hbm_read_probe(int device, size_t bytes, int iters, int variant) {
     set_error("");
     if (hipSetDevice(device) != hipSuccess) return -1.0;
     void *buf = nullptr;
@@ -2444,9 +2447,9 @@ extern "C" double gemma_hbm_read_gbs(int device, size_t bytes, int iters) {
     (void)hipEventCreate(&t0);
     (void)hipEventCreate(&t1);
     double gbs = -1.0;
-    if (launch_stream_read(buf, bytes, sink, s) == 0) {
+    if (launch_stream_read(buf, bytes, sink, s, variant) == 0) {
         (void)hipEventRecord(t0, s);
-        for (int i = 0; i < iters; ++i) (void)launch_stream_read(buf, bytes, sink, s);
+        for (int i = 0; i < iters; ++i) (void)launch_stream_read(buf, bytes, sink, s, variant);
         (void)hipEventRecord(t1, s);
         (void)hipEventSynchronize(t1);
         float ms = 0;
@@ -2459,6 +2462,12 @@ extern "C" double gemma_hbm_read_gbs(int device, size_t bytes, int iters) {
     (void)hipFree(buf);
     (void)hipFree(sink);
     return gbs;
+}
+
+// the measured HBM read roofline: the faster of the two probes
+extern "C" double gemma_hbm_read_gbs(int device, size_t bytes, int iters) {
+    const double a = gemma_hbm_read_probe(device, bytes, iters, 0), b = gemma_hbm_read_probe(device, bytes, iters, 1);
+    return a > b ? a : b;
 }
 
 // diagnostics: the prefill (exact or MFMA) with the residual stream after every layer copied to host_taps

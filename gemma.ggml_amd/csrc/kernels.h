@@ -376,7 +376,7 @@ int launch_embed(const uint8_t *qs, const uint8_t *sc, int wtype, int64_t n_bt, 
                  float *out, int64_t E, hipStream_t s);
 // reduces the n_parts per-workgroup argmax keys, appends the token, advances the position
 int launch_exp_f16_all(uint16_t *out, hipStream_t s);
-int launch_stream_read(const void *buf, size_t bytes, unsigned *sink, hipStream_t s);  // roofline probe  // the softmax's exp for all 65536 f16 codes (tests)
+int launch_stream_read(const void *buf, size_t bytes, unsigned *sink, hipStream_t s, int variant = 0);  // roofline probe  // the softmax's exp for all 65536 f16 codes (tests)
 int launch_reduce_keys(const unsigned long long *keys, int n, int64_t row_base, unsigned long long *out, hipStream_t s);
 struct rope_row {  // k_advance also publishes the new position's RoPE row: cur = [cos | sin | (int)pos]
     const float *cos = nullptr, *sin = nullptr;
@@ -385,7 +385,6 @@ struct rope_row {  // k_advance also publishes the new position's RoPE row: cur 
     unsigned *epoch = nullptr;  // if set, incremented (the persistent token launch's granule tags)
 };
 // read `n` weight regions with allocating loads (MALL warm-up for a later kernel), `grid` workgroups
-int launch_mall_warm(const void *const *ptrs, const int64_t *bytes, int n, int grid, hipStream_t s);
 int launch_advance(const unsigned long long *keys, int n_parts, int *token, int *pos, int *hist, int hist_cap,
                    const int *n_fixed, const rope_row &r, hipStream_t s);
 int launch_set_position(int token, int p, int *pos, int *hist, int *n_fixed, int fixed, const rope_row &r, hipStream_t s);

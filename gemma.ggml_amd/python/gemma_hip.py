@@ -29,7 +29,7 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact", "gemma_kq_time", "hpc_graph_compute",
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
-           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_att_o", "gemma_engine_set_option", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs",
+           "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_att_o", "gemma_engine_set_option", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs", "gemma_hbm_read_probe",
            "gemma_tp_unique_id", "gemma_engine_create_tp", "gemma_engine_tp_info", "gemma_engine_set_persist_timeout",
            "gguf_init_from_file", "gguf_free", "gguf_get_n_kv", "gguf_get_key", "gguf_get_kv_type",
            "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
@@ -131,6 +131,8 @@ def lib():
     L.gemma_kq_time.argtypes = [C.c_int, i64, i64, C.c_int, C.POINTER(C.c_double)]
     L.gemma_hbm_read_gbs.restype = C.c_double
     L.gemma_hbm_read_gbs.argtypes = [C.c_int, C.c_size_t, C.c_int]
+    L.gemma_hbm_read_probe.restype = C.c_double
+    L.gemma_hbm_read_probe.argtypes = [C.c_int, C.c_size_t, C.c_int, C.c_int]
     L.gemma_engine_sync.restype = C.c_int
     L.gemma_engine_sync.argtypes = [vp]
     L.gemma_engine_create_from_gguf.restype = vp

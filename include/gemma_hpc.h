@@ -169,8 +169,11 @@ int gemma_test_gemm_exact(int type, int64_t rows, int64_t K, int64_t T, const vo
 /* K-quant matvec (Q4_K / Q6_K x Q8_K) timed alone: avg µs per launch over
  * `iters` launches rotating over cold weight copies; *algo_bytes = weights + Q8_K column + y */
 double gemma_kq_time(int type, int64_t rows, int64_t K, int iters, double *algo_bytes);
-/* measured HBM read roofline: streaming read of `bytes` on `device`, `iters` passes; GB/s */
+/* measured HBM read roofline: streaming read of `bytes` on `device`, `iters` passes; GB/s — the
+   faster of the two probes below */
 double gemma_hbm_read_gbs(int device, size_t bytes, int iters);
+/* one probe: variant 0 = 16-B nontemporal loads into registers, 1 = LDS-DMA (global_load_lds nt) */
+double gemma_hbm_read_probe(int device, size_t bytes, int iters, int variant);
 /* per-op test entry: the softmax's exp(f16) for all 65536 codes (compared with ggml's table) */
 int gemma_test_exp_f16(uint16_t *out);
 /* per-op test entry: one rms_norm kernel on host rows (ggml rms_norm):

@@ -4,8 +4,11 @@ the exact kernel template name, launches per token and the average duration over
 tokens (the decode positions; the prompt's tokens before them are skipped), so every
 `roofline.classes` fraction of the bench line can be recomputed from algorithmic bytes / avg µs.
 
-  python3 scripts/decode_classes.py {run_results.db | run_kernel_trace.csv} PROMPT STEPS [plan] > decode_kernels.md
+  python3 scripts/decode_classes.py {run_results.db | run_kernel_trace.csv} PROMPT STEPS [plan] [out.json] > decode_kernels.md
+
+With out.json the same table is also written as JSON (bench.py embeds the newest profiles/rNN copy).
 """
+import json
 import csv
 import re
 import sys
@@ -27,6 +30,9 @@ CLASSES = OrderedDict([
 def main():
     path, prompt, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     plan = sys.argv[4] if len(sys.argv) > 4 else ""
+    jpath = sys.argv[5] if len(sys.argv) > 5 else None
+    js = {"source": "rocprofv3 --kernel-trace of scripts/decode_prof.py", "prompt": prompt, "steps": steps, "plan": plan,
+          "classes": []}
     rows = []
     if path.endswith(".db"):  # rocprofv3's default rocpd SQLite output: the `kernels` view
         import sqlite3
@@ -54,6 +60,7 @@ def main():
     if plan:
         print(f"Launch plan (k_split, rows_per_wg, image per class): `{plan}`\n")
     print(f"Token wall time in the trace (k_advance to k_advance): {t_tok:.1f} µs\n")
+    js["token_wall_us"] = round(t_tok, 3)
     print("| class | kernel (exact template) | launches / token | avg µs | min µs | max µs | algo bytes / launch | GB/s | frac of 8 TB/s |")
     print("|---|---|---|---|---|---|---|---|---|")
     used = set()
@@ -70,12 +77,20 @@ def main():
             frac = f"{algo / avg / 1e3 / 8000:.3f}" if algo else "—"
             print(f"| {cls} | `{n}` | {len(d) / steps:g} | {avg:.3f} | {min(d):.3f} | {max(d):.3f} | "
                   f"{algo if algo else '—'} | {gbs} | {frac} |")
+            js["classes"].append({"class": cls, "kernel": n, "launches_per_token": len(d) / steps, "avg_us": round(avg, 3),
+                                  "min_us": round(min(d), 3), "max_us": round(max(d), 3), "algo_bytes": algo,
+                                  "GB/s": round(algo / avg / 1e3, 1) if algo else None,
+                                  "frac": round(algo / avg / 1e3 / 8000, 4) if algo else None})
     other = [(s, e, n) for (s, e, n) in win if n not in used]
     for n in sorted(set(n for _, _, n in other)):
         d = [(e - s) / 1e3 for (s, e, nn) in other if nn == n]
         tot += sum(d) / steps
         print(f"| other | `{n}` | {len(d) / steps:g} | {sum(d) / len(d):.3f} | {min(d):.3f} | {max(d):.3f} | — | — | — |")
     print(f"\nSum of kernel time per token: {tot:.1f} µs of {t_tok:.1f} µs (the rest: gaps between launches).")
+    js["kernel_sum_us_per_token"] = round(tot, 3)
+    if jpath:
+        with open(jpath, "w") as f:
+            json.dump(js, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -27,7 +27,7 @@ for w in $WHAT; do
     prof) timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu --steps 32 > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; } ;
           find $OUT/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/kernel_stats.csv ; head -12 $OUT/kernel_stats.csv | cut -c1-200 ;;
     profgraph) TORCH_FIRST=${TORCH_FIRST:-1} PROF_MAPS=$OUT/maps_profg.txt GHIP_PROF_GRAPH=1 PLAN=$PLAN timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profg -o run -- python3 scripts/decode_prof.py 48 > $OUT/profg.log 2>&1 || { tail -40 $OUT/profg.log; exit 1; } ;
-          python3 scripts/decode_classes.py $(find $OUT/profg -name "run_kernel_trace.csv" | head -1) 128 48 "$PLAN (hipGraph replay)" > $OUT/decode_kernels_graph.md && cat $OUT/decode_kernels_graph.md ;;
+          python3 scripts/decode_classes.py $(find $OUT/profg -name "run_kernel_trace.csv" | head -1) 128 48 "$PLAN (hipGraph replay)" $OUT/decode_kernels_graph.json > $OUT/decode_kernels_graph.md && cat $OUT/decode_kernels_graph.md ;;
     pmcprefill) bash scripts/pmc_prefill.sh $TAG/pmcp 2048 q4_0 > $OUT/pmcp.log 2>&1 || { tail -20 $OUT/pmcp.log; exit 1; } ; tail -20 $OUT/pmcp.log ;;
     pmc) timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_size -o run -- python3 scripts/pmc_probe.py > $OUT/pmc1.log 2>&1 || { tail -20 $OUT/pmc1.log; exit 1; } ;
          timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_size -o run -- python3 scripts/pmc_probe.py > $OUT/pmc2.log 2>&1 || { tail -20 $OUT/pmc2.log; exit 1; } ;
