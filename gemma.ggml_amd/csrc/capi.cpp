@@ -257,6 +257,7 @@ extern "C" int hpc_register_weight(const void *host, int type, int64_t ne00, int
 }
 
 extern "C" void hpc_set_kq_gemm_min(int min_cols) { set_kq_gemm_min(min_cols); }
+extern "C" void hpc_set_gemm_x4(int on) { set_gemm_x4(on); }
 
 extern "C" void mul_mat(int64_t ne01, int64_t ne11, int64_t ne12, int64_t nb01, int64_t ne1, int64_t nb1, int64_t nb2,
                         size_t row_size, int64_t shared_edge, struct ggml_tensor *src0, struct ggml_tensor *src1,

@@ -8,6 +8,7 @@
 // block order instead of 8 lane chains + fold), so prefill logits match the CPU path to ~1e-6
 // relative (tests: 1e-3), while the per-token decode path stays bit-exact.
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 
@@ -713,6 +714,203 @@ k_gemm_x(gemm_args g) {
         }
 }
 
+// ---- exact GEMM on the K = 4 multi-block MFMA ------------------------------------
+// v_mfma_f32_16x16x4_4b_f16 = FOUR independent 16x16x4 products, one per block of 16 lanes: block
+// b of the instruction is ONE AVX2 lane l of ggml's vec_dot_q4_0_q8_0 — A = the 4 weights 4l..4l+3
+// of 16 rows, B = the same 4 activations of 16 tokens — so D[b][row][token] = isum_l exactly (4
+// products of small integers, f32 accumulate; tests/micro/mfma_k4.hip: every output integral and
+// equal) and EVERY product is useful: the W32 form's A fragments are 3/4 zeros (8x the Q4_0 bytes
+// in LDS), here they are the 8 dense bytes of (row, lane).  Two instructions cover a block's 8
+// lanes.  Layout (probed, tests/micro/mfma_k4.hip): A lane L = (block L/16, row L%16), B lane L =
+// (block L/16, token L%16), D register r of lane L = (block r/4, row 4*(L/16) + r%4, token L%16):
+// each lane holds 4 rows x 8 lanes of one token per token group, so the fmaf chains and the final
+// hsum ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7)) stay in the lane's registers.  Same operands, same
+// d = d_w*d_a, same fmaf sequence in block order as k_gemm_x: bit-identical.
+// Tile: 4 waves = 2 row groups (16 rows) x 2 token groups (32 tokens); XKB = 8 blocks per stage.
+// LDS: A as [block][row group][lane][16 rows] x 8 B (a 32-lane half of a b64 read = 256 contiguous
+// bytes: conflict-free), tokens as k_gemm_x's padded f16 rows.
+typedef _Float16 xh4 __attribute__((ext_vector_type(4)));
+constexpr int X4_ACOL = 16 * 8;                          // bytes per (block, row group, lane) column
+constexpr int X4_ABLK = 2 * 8 * X4_ACOL;                 // bytes per block (32 rows x 8 lanes x 8 B)
+#ifndef GHIP_X4_WPE
+#define GHIP_X4_WPE 3  // waves per SIMD the register budget must allow (LDS: 53 KB per workgroup fits 3 per CU)
+#endif
+#ifndef GHIP_X4_PF
+#define GHIP_X4_PF 0   // 1: the next stage's global loads in registers during the compute (k_gemm_x's form)
+#endif
+#ifndef GHIP_X4_SEQ
+#define GHIP_X4_SEQ 1  // 1: a block's two token groups one after the other (half the MFMA results live)
+#endif
+template <int WT, int EPI>
+__global__ void __launch_bounds__(XNT)
+#if GHIP_X4_WPE
+__attribute__((amdgpu_waves_per_eu(GHIP_X4_WPE, GHIP_X4_WPE)))
+#endif
+k_gemm_x4(gemm_args g) {
+    static_assert(XNT == 256 && XM == 32 && XN == 64, "k_gemm_x4 takes k_gemm_x's default tile (32 rows x 64 tokens)");
+    __shared__ __attribute__((aligned(16))) uint8_t Wa[XKB * X4_ABLK];
+    __shared__ __attribute__((aligned(16))) uint8_t Xs[XN * XS_ROW];
+    __shared__ __attribute__((aligned(16))) float dws[XKB][XM];
+    __shared__ __attribute__((aligned(16))) float das[XKB][XN];
+    constexpr int BT = wfmt<WT>::BT;
+    constexpr int WRECS = (WT == T_Q4_0) ? 256 : 512;  // 16-B weight records per stage
+    constexpr int WREC = (WRECS + XNT - 1) / XNT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rg = wave & 1, tg = wave >> 1;           // this wave: rows 16*rg.., tokens 32*tg..
+    const int q = lane >> 4, l16 = lane & 15;
+    const int64_t t0 = (int64_t)blockIdx.x * XN, r0 = (int64_t)blockIdx.y * XM;
+    const int64_t n_rt = g.n_rt, n_bt = g.n_bt, nb = g.nb;
+
+    // [token group][AVX2 lane][row pair]: rows (2p, 2p+1) of one lane chain pair as one float2, as
+    // their D registers sit side by side, so each v_pk_fma_f32 takes them with no register moves
+    // (two independent fmaf chains per instruction: the same roundings as two v_fma_f32)
+    typedef float xf2 __attribute__((ext_vector_type(2)));
+    xf2 acc[2][8][2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int l = 0; l < 8; ++l)
+#pragma unroll
+            for (int p2 = 0; p2 < 2; ++p2) acc[c][l][p2] = xf2{0.0f, 0.0f};
+
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    u4v wq[WREC], ws[WREC], xr[XREC];
+    float xd[XDA];
+    auto gload = [&](int64_t kb0) {  // k_gemm_x's stage loads
+#pragma unroll
+        for (int k = 0; k < WREC; ++k) {
+            const int rec = tid + XNT * k, tile_i = (rec >> 6) & 7, ln = rec & 63, rr = ln >> 3;
+            if (rec >= WRECS) break;  // wave-uniform
+            const int rti = (WT == T_Q4_0) ? (tile_i & 3) : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
+            int64_t rt = r0 / 8 + rti, bt = kb0 / BT + bti;
+            const bool ok = rt < n_rt && bt < n_bt;
+            rt = ok ? rt : 0;
+            bt = ok ? bt : 0;
+            wq[k] = *(const u4v *)(g.qs + (rt * n_bt + bt) * 1024 + ln * 16);
+            const uint8_t *sp = g.sc + ((rt * n_bt + bt) * 8 + rr) * wfmt<WT>::SCALE_BYTES;
+            if (WT == T_Q4_0) ws[k] = *(const u4v *)sp;
+            else { const uint2 s2 = *(const uint2 *)sp; ws[k] = u4v{s2.x, s2.y, 0u, 0u}; }
+            if (!ok) { wq[k] = u4v{0u, 0u, 0u, 0u}; ws[k] = u4v{0u, 0u, 0u, 0u}; }
+        }
+#pragma unroll
+        for (int k = 0; k < XREC; ++k) {
+            const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
+            const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
+            xr[k] = *(const u4v *)(g.xh + t * g.ldq + kb0 * 32 + seg * 8);
+        }
+#pragma unroll
+        for (int k = 0; k < XDA; ++k) {
+            const int c = (tid + XNT * k) % (XN * 8), tok = c >> 3, b = c & 7;
+            const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
+            xd[k] = (kb0 + b < nb) ? g.da[t * g.ldd + kb0 + b] : 0.0f;
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int k = 0; k < WREC; ++k) {
+            const int rec = tid + XNT * k, tile_i = (rec >> 6) & 7, ln = rec & 63, rr = ln >> 3, l = ln & 7;
+            if (rec >= WRECS) break;  // wave-uniform
+            const int rti = (WT == T_Q4_0) ? (tile_i & 3) : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
+            const int row = rti * 8 + rr;  // 0..31
+            const uint32_t qd[4] = {wq[k].x, wq[k].y, wq[k].z, wq[k].w};
+            const uint32_t sd[4] = {ws[k].x, ws[k].y, ws[k].z, ws[k].w};
+            uint8_t *col = Wa + ((row >> 4) * 8 + l) * X4_ACOL + (row & 15) * 8;
+            auto put = [&](int b, uint2 f) { *(uint2 *)(col + b * X4_ABLK) = f; };
+            if (WT == T_Q4_0) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {  // nibble n -> f16(n - 8): bias 1032
+                    put(2 * p, bytes_to_f16x4(qd[p] & 0x0F0F0F0Fu, 0x64086408u));
+                    put(2 * p + 1, bytes_to_f16x4((qd[p] >> 4) & 0x0F0F0F0Fu, 0x64086408u));
+                }
+            } else {
+#pragma unroll
+                for (int p = 0; p < 4; ++p)  // int8 q -> f16(q): byte q ^ 0x80 = q + 128, bias 1152
+                    put(bti * 4 + p, bytes_to_f16x4(qd[p] ^ 0x80808080u, 0x64806480u));
+            }
+            if (l == 0) {
+#pragma unroll
+                for (int b = 0; b < BT; ++b) dws[(WT == T_Q4_0 ? 0 : bti * 4) + b][row] = h2f(sd[b >> 1] >> (16 * (b & 1)));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < XREC; ++k) {
+            const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
+            *(u4v *)(Xs + tok * XS_ROW + seg * 16) = xr[k];
+        }
+#pragma unroll
+        for (int k = 0; k < XDA; ++k) {
+            const int c = tid + XNT * k;
+            if (c < XN * 8) das[c & 7][c >> 3] = xd[k];
+        }
+    };
+    // this lane's operand addresses: A column (row group rg, AVX2 lane 4*ih + q, row l16), B (token
+    // 32*tg + 16*c + l16, the same lane's 4 elements)
+    const uint8_t *a_base = Wa + (rg * 8 + q) * X4_ACOL + l16 * 8;
+    const uint8_t *b_base = Xs + (32 * tg + l16) * XS_ROW + q * 8;
+    auto block = [&](int b) {
+        const xh4 a0 = *(const xh4 *)(a_base + b * X4_ABLK), a1 = *(const xh4 *)(a_base + b * X4_ABLK + 4 * X4_ACOL);
+        xh4 bb[2][2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            bb[c][0] = *(const xh4 *)(b_base + c * 16 * XS_ROW + b * 64);
+            bb[c][1] = *(const xh4 *)(b_base + c * 16 * XS_ROW + b * 64 + 32);
+        }
+        const float4 dw4 = *(const float4 *)&dws[b][16 * rg + 4 * q];
+        const float dw[4] = {dw4.x, dw4.y, dw4.z, dw4.w};
+        float da[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) da[c] = das[b][32 * tg + 16 * c + l16];
+        const xf16v z = {};
+        auto group = [&](int c) {
+            xf16v d[2];
+            d[0] = __builtin_amdgcn_mfma_f32_16x16x4f16(a0, bb[c][0], z, 0, 0, 0);
+            d[1] = __builtin_amdgcn_mfma_f32_16x16x4f16(a1, bb[c][1], z, 0, 0, 0);
+            xf2 dd[2];
+#pragma unroll
+            for (int p2 = 0; p2 < 2; ++p2) dd[p2] = xf2{dw[2 * p2] * da[c], dw[2 * p2 + 1] * da[c]};
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int bq = 0; bq < 4; ++bq)  // D registers 4*bq .. 4*bq+3: AVX2 lane 4*h + bq, rows 0..3
+#pragma unroll
+                    for (int p2 = 0; p2 < 2; ++p2) {
+                        const xf2 dv = {d[h][4 * bq + 2 * p2], d[h][4 * bq + 2 * p2 + 1]};
+                        acc[c][4 * h + bq][p2] = __builtin_elementwise_fma(dd[p2], dv, acc[c][4 * h + bq][p2]);
+                    }
+        };
+        group(0);
+        if (GHIP_X4_SEQ) __builtin_amdgcn_sched_barrier(0);  // token group 1's MFMAs after group 0's chains
+        group(1);
+    };
+
+    if (GHIP_X4_PF) gload(0);
+    for (int64_t kb0 = 0; kb0 < nb; kb0 += XKB) {
+        if (!GHIP_X4_PF) gload(kb0);  // (no register prefetch: the other workgroups of the CU overlap)
+        lstore();
+        __syncthreads();
+        if (GHIP_X4_PF && kb0 + XKB < nb) gload(kb0 + XKB);
+        const int nbs = (int)(nb - kb0 < XKB ? nb - kb0 : XKB);
+#pragma unroll 1
+        for (int b = 0; b < nbs; ++b) block(b);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int64_t t = t0 + 32 * tg + 16 * c + l16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float a[8];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) a[l] = acc[c][l][i >> 1][i & 1];
+            float o = ((a[0] + a[4]) + (a[2] + a[6])) + ((a[1] + a[5]) + (a[3] + a[7]));
+            const int64_t r = r0 + 16 * rg + 4 * q + i;
+            if (t >= g.T || r >= g.rows) continue;
+            if (EPI == EPI_ADD) o = o + g.resid[t * g.ldy + r];
+            g.y[t * g.ldy + r] = o;
+        }
+    }
+}
+
 // ---- RoPE + q scale + KV store for T prompt tokens (positions p0 .. p0+T-1) --------------------
 // Same per-element arithmetic as the decode attention (src/gemma_model.cpp:698-718, 499-518).
 __global__ void __launch_bounds__(256) k_rope_kv_prefill(ropekv_args a) {
@@ -962,6 +1160,12 @@ int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s) {
     return 0;
 }
 
+// which exact GEMM runs (hpc_set_gemm_x4 / the engine option "gemm_x4"): 0 the lane-masked W32 form
+// (k_gemm_x), 1 the K = 4 multi-block form (k_gemm_x4); same bits either way
+static std::atomic<int> g_gemm_x4{0};
+bool gemm_x4_on() { return g_gemm_x4.load() != 0; }
+void set_gemm_x4(int v) { g_gemm_x4.store(v); }
+
 int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
     if (g.ldq % 256 || g.nb * 32 > g.ldq || g.T <= 0 || g.rows <= 0 || !g.xh) {
         set_error("gemm_exact: needs the f16 activation image, padded to 256 elements");
@@ -973,6 +1177,18 @@ int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
         return -1;
     }
     const dim3 grid((unsigned)((g.T + XN - 1) / XN), (unsigned)gy);
+    if (gemm_x4_on()) {  // the K = 4 multi-block MFMA form
+        if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x4<T_Q4_0, EPI_STORE>), grid, dim3(XNT), 0, s, g);
+        else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x4<T_Q4_0, EPI_ADD>), grid, dim3(XNT), 0, s, g);
+        else if (wtype == T_Q8_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x4<T_Q8_0, EPI_STORE>), grid, dim3(XNT), 0, s, g);
+        else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x4<T_Q8_0, EPI_ADD>), grid, dim3(XNT), 0, s, g);
+        else {
+            set_error("gemm_exact: unsupported (type, epilogue)");
+            return -1;
+        }
+        GHIP_CHECK(hipGetLastError());
+        return 0;
+    }
     constexpr bool W32 = GHIP_X32 != 0;
     if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_STORE, W32>), grid, dim3(XNT), 0, s, g);
     else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x<T_Q4_0, EPI_ADD, W32>), grid, dim3(XNT), 0, s, g);

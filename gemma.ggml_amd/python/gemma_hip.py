@@ -24,7 +24,7 @@ GGML_TYPE_Q4_K, GGML_TYPE_Q6_K, GGML_TYPE_Q8_K = 12, 14, 15
 
 # exported symbols (checked against include/gemma_hpc.h by tests/test_capi_symbols.py)
 EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_last_error", "hpc_set_error_mode",
-           "hpc_weight_cache_entries", "hpc_set_matvec_ks", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
+           "hpc_weight_cache_entries", "hpc_set_matvec_ks", "hpc_set_gemm_x4", "gemma_engine_debug_step", "gemma_engine_stamp_step", "gemma_engine_create", "gemma_engine_free", "gemma_engine_begin",
            "gemma_engine_step", "gemma_engine_tokens", "gemma_engine_pos", "gemma_engine_prefill",
            "gemma_engine_prefill_fast", "gemma_engine_prefill_taps", "gemma_test_gemm", "gemma_test_gemm_exact", "gemma_kq_time", "hpc_graph_compute",
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
@@ -86,6 +86,8 @@ def lib():
     L.hpc_set_error_mode.argtypes = [C.c_int]
     L.hpc_weight_cache_entries.restype = C.c_int
     L.hpc_set_matvec_ks.argtypes = [C.c_int]
+    L.hpc_set_gemm_x4.argtypes = [C.c_int]
+    L.hpc_set_gemm_x4.restype = None
     L.gemma_engine_debug_step.restype = C.c_int
     L.gemma_engine_debug_step.argtypes = [vp, vp, vp]
     L.gemma_engine_stamp_step.restype = C.c_int

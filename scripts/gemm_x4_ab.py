@@ -1,0 +1,35 @@
+"""A/B of the exact T = 2048 Gemma-2B Q4_0 prefill with the W32 GEMM (hpc_set_gemm_x4(0)) and the
+K = 4 multi-block form (1), interleaved reps on one engine.  usage: gemm_x4_ab.py [reps] [T]"""
+import os
+import sys
+import time
+
+import torch  # noqa: F401  (the runtime bench.py runs on)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gemma.ggml_amd", "python"))
+sys.path.insert(0, ROOT)
+import gemma_hip as G  # noqa: E402
+from bench import GEMMA_2B, make_prompt  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+e = G.Engine(GEMMA_2B, n_ctx=T + 64, device=0)
+p = make_prompt(T, GEMMA_2B["n_vocab"], seed=2)
+res = {0: [], 1: []}
+toks = {}
+for r in range(reps + 1):
+    for on in (0, 1):
+        G.lib().hpc_set_gemm_x4(on)
+        e.begin(p)
+        e.sync()
+        t0 = time.perf_counter()
+        tok = e.prefill(T)[0]
+        dt = time.perf_counter() - t0
+        toks[on] = tok
+        if r:
+            res[on].append(dt * 1e3)
+        print(f"rep {r} x4 {on}: {dt * 1e3:.2f} ms token {tok}", flush=True)
+G.lib().hpc_set_gemm_x4(0)
+print("W32 ms", [round(v, 2) for v in res[0]], "x4 ms", [round(v, 2) for v in res[1]], "tokens equal", toks[0] == toks[1])
+e.close()
