@@ -42,6 +42,10 @@ for w in $WHAT; do
     # the graph-replay trace on /opt/rocm's HIP runtime (no torch): the configuration that crashed in
     # rounds 4-6; its mappings are kept so the frames resolve exactly.  LAST in a call: a crash ends it.
     crashrepro) TORCH_FIRST=0 PROF_MAPS=$OUT/maps_crash.txt GHIP_PROF_GRAPH=1 PLAN=$PLAN timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc -o run -- python3 scripts/decode_prof.py 48 > $OUT/profc.log 2>&1; echo "crashrepro rc=$?"; tail -40 $OUT/profc.log; exit 0 ;;
+    # summaries of the prof / pmc passes into $OUT/summary, then the raw traces removed (gpurun
+    # brings back at most 64 MiB of gpurun_out)
+    summarize) python3 scripts/summarize_profiles.py $OUT $OUT/summary > $OUT/summarize.log 2>&1 || { tail -20 $OUT/summarize.log; exit 1; } ;
+               rm -rf $OUT/prof $OUT/profg $OUT/profc $OUT/pmc_fetch_size $OUT/pmc_write_size ; ls $OUT/summary ;;
     *) echo "unknown mode $w"; exit 2 ;;
   esac
 done

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 outputs into profiles/<tag>/: kernel stats (trace pass) and per-dispatch HBM
 bytes of the hot matvec kernels (separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE x2
-correction per MI355X_MICROARCH §HBM).  usage: summarize_profiles.py <gpurun_out dir> <tag>"""
+correction per MI355X_MICROARCH §HBM).  usage: summarize_profiles.py <gpurun_out dir> <tag | out dir>"""
 import csv
 import glob
 import json
@@ -9,7 +9,8 @@ import sys
 
 src, tag = sys.argv[1], sys.argv[2]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-out = os.path.join(ROOT, "profiles", tag)
+# tag: a round name (profiles/<tag>) or a directory path (e.g. on the GPU box, under gpurun_out/)
+out = tag if os.sep in tag else os.path.join(ROOT, "profiles", tag)
 os.makedirs(out, exist_ok=True)
 
 
