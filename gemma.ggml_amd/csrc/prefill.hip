@@ -814,7 +814,10 @@ k_gemm_x4(gemm_args g) {
             const int row = rti * 8 + rr;  // 0..31
             const uint32_t qd[4] = {wq[k].x, wq[k].y, wq[k].z, wq[k].w};
             const uint32_t sd[4] = {ws[k].x, ws[k].y, ws[k].z, ws[k].w};
-            uint8_t *col = Wa + ((row >> 4) * 8 + l) * X4_ACOL + (row & 15) * 8;
+            // row slot swizzled by the lane: (row & 15) ^ 2l, so each 16-lane group (rr 2 values x l 0..7)
+            // of a ds_write_b64 lands on 32 distinct banks (unswizzled: 8-way, 50 % of the LDS cycles
+            // conflicts in the PMC; scripts/lds_banks.py); a 16-row column stays one contiguous 128 B
+            uint8_t *col = Wa + ((row >> 4) * 8 + l) * X4_ACOL + (((row & 15) ^ (2 * l)) & 15) * 8;
             auto put = [&](int b, uint2 f) { *(uint2 *)(col + b * X4_ABLK) = f; };
             if (WT == T_Q4_0) {
 #pragma unroll
@@ -832,10 +835,14 @@ k_gemm_x4(gemm_args g) {
                 for (int b = 0; b < BT; ++b) dws[(WT == T_Q4_0 ? 0 : bti * 4) + b][row] = h2f(sd[b >> 1] >> (16 * (b & 1)));
             }
         }
+        // token rows: the 8-B chunks of tokens 8..15 (of every 16) swapped within their 16 B, so the
+        // compiler's ds_read2_b64 of B (16-lane groups, banks mod 32) sees tokens j and j + 8 on
+        // different banks (pitch 528 B alone: 2-way)
 #pragma unroll
         for (int k = 0; k < XREC; ++k) {
             const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
-            *(u4v *)(Xs + tok * XS_ROW + seg * 16) = xr[k];
+            const u4v v = xr[k];
+            *(u4v *)(Xs + tok * XS_ROW + seg * 16) = (tok & 8) ? u4v{v.z, v.w, v.x, v.y} : v;
         }
 #pragma unroll
         for (int k = 0; k < XDA; ++k) {
@@ -845,10 +852,11 @@ k_gemm_x4(gemm_args g) {
     };
     // this lane's operand addresses: A column (row group rg, AVX2 lane 4*ih + q, row l16), B (token
     // 32*tg + 16*c + l16, the same lane's 4 elements)
-    const uint8_t *a_base = Wa + (rg * 8 + q) * X4_ACOL + l16 * 8;
-    const uint8_t *b_base = Xs + (32 * tg + l16) * XS_ROW + q * 8;
+    const uint8_t *a_base = Wa + (rg * 8 + q) * X4_ACOL + ((l16 ^ (2 * q)) & 15) * 8;              // lane q
+    const uint8_t *a_base1 = Wa + (rg * 8 + 4 + q) * X4_ACOL + ((l16 ^ (8 + 2 * q)) & 15) * 8;     // lane 4 + q
+    const uint8_t *b_base = Xs + (32 * tg + l16) * XS_ROW + (q ^ ((l16 >> 3) & 1)) * 8;  // chunk 4*ih + q, swapped
     auto block = [&](int b) {
-        const xh4 a0 = *(const xh4 *)(a_base + b * X4_ABLK), a1 = *(const xh4 *)(a_base + b * X4_ABLK + 4 * X4_ACOL);
+        const xh4 a0 = *(const xh4 *)(a_base + b * X4_ABLK), a1 = *(const xh4 *)(a_base1 + b * X4_ABLK);
         xh4 bb[2][2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
