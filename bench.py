@@ -297,7 +297,8 @@ def prefill_roofline(T, prefill):
             pmc = json.load(f)
         keys = ("mfma_util", "lds_busy", "lds_bank_conflict_frac", "valu_inst_per_wave_cycle", "wait_any_frac", "what")
         src = os.path.relpath(path, ROOT)
-        for names, field in ((("k_gemm_x",), "pmc_exact_gemm"), (("k_attn_mx", "k_attn_rows"), "pmc_exact_attention")):
+        for names, field in ((("k_gemm_x4", "k_gemm_x<", "k_gemm_x"), "pmc_exact_gemm"),
+                             (("k_attn_mx", "k_attn_rows"), "pmc_exact_attention")):
             k_name = next((n for n in names if n in pmc), None)
             if k_name:
                 out[field] = dict({k: pmc[k_name][k] for k in keys if k in pmc[k_name]}, kernel=k_name, source=src)
@@ -575,8 +576,8 @@ def main():
             best = min(times[1:])
             prefill[name] = {"tok_s": round(args.prefill / best, 1), "ms": round(best * 1e3, 3)}
         pe.close()
-        prefill["exact"]["path"] = ("ggml AVX2 lane order: lane-masked f16 MFMA GEMMs + fmaf lane chains, per-row exact attention; bit-identical "
-                                    "logits to the CPU path")
+        prefill["exact"]["path"] = ("ggml AVX2 lane order: v_mfma_f32_16x16x4_4b_f16 GEMMs (one instruction block = one AVX2 "
+                                    "lane) + fmaf lane chains, exact attention on f32 MFMA; bit-identical logits to the CPU path")
         prefill["fast"]["path"] = ("int8 MFMA GEMMs + f16 MFMA attention; fp32 order differs from the CPU "
                                    "path (DESIGN.md Prefill)")
         prefill["tok_s"] = prefill["exact"]["tok_s"]

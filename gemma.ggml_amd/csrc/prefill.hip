@@ -731,7 +731,6 @@ k_gemm_x(gemm_args g) {
 // bytes: conflict-free), tokens as k_gemm_x's padded f16 rows.
 typedef _Float16 xh4 __attribute__((ext_vector_type(4)));
 constexpr int X4_ACOL = 16 * 8;                          // bytes per (block, row group, lane) column
-constexpr int X4_ABLK = 2 * 8 * X4_ACOL;                 // bytes per block (32 rows x 8 lanes x 8 B)
 #ifndef GHIP_X4_WPE
 #define GHIP_X4_WPE 3  // waves per SIMD the register budget must allow (LDS: 53 KB per workgroup fits 3 per CU)
 #endif
@@ -741,24 +740,28 @@ constexpr int X4_ABLK = 2 * 8 * X4_ACOL;                 // bytes per block (32 
 #ifndef GHIP_X4_SEQ
 #define GHIP_X4_SEQ 1  // 1: a block's two token groups one after the other (half the MFMA results live)
 #endif
-template <int WT, int EPI>
+// RGS: row groups (16 rows) per workgroup — 2: 32 rows x 64 tokens, 4: 64 rows x 32 tokens (the token
+// image, re-read by every row tile, is the bulk of the staging: 64 rows halve it)
+template <int WT, int EPI, int RGS>
 __global__ void __launch_bounds__(XNT)
 #if GHIP_X4_WPE
 __attribute__((amdgpu_waves_per_eu(GHIP_X4_WPE, GHIP_X4_WPE)))
 #endif
 k_gemm_x4(gemm_args g) {
-    static_assert(XNT == 256 && XM == 32 && XN == 64, "k_gemm_x4 takes k_gemm_x's default tile (32 rows x 64 tokens)");
+    static_assert(XNT == 256 && (RGS == 2 || RGS == 4), "4 waves: RGS row groups x 4/RGS token groups");
+    constexpr int M4 = 16 * RGS, N4 = 32 * (4 / RGS), X4_ABLK = RGS * 8 * X4_ACOL;
+    constexpr int XREC4 = N4 * XKB * 64 / 16 / XNT, XDA4 = (N4 * XKB + XNT - 1) / XNT;
     __shared__ __attribute__((aligned(16))) uint8_t Wa[XKB * X4_ABLK];
-    __shared__ __attribute__((aligned(16))) uint8_t Xs[XN * XS_ROW];
-    __shared__ __attribute__((aligned(16))) float dws[XKB][XM];
-    __shared__ __attribute__((aligned(16))) float das[XKB][XN];
+    __shared__ __attribute__((aligned(16))) uint8_t Xs[N4 * XS_ROW];
+    __shared__ __attribute__((aligned(16))) float dws[XKB][M4];
+    __shared__ __attribute__((aligned(16))) float das[XKB][N4];
     constexpr int BT = wfmt<WT>::BT;
-    constexpr int WRECS = (WT == T_Q4_0) ? 256 : 512;  // 16-B weight records per stage
+    constexpr int WRECS = (M4 / 8) * 64 * (WT == T_Q4_0 ? 1 : 2);  // 16-B weight records per stage
     constexpr int WREC = (WRECS + XNT - 1) / XNT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int rg = wave & 1, tg = wave >> 1;           // this wave: rows 16*rg.., tokens 32*tg..
+    const int rg = wave % RGS, tg = wave / RGS;        // this wave: rows 16*rg.., tokens 32*tg..
     const int q = lane >> 4, l16 = lane & 15;
-    const int64_t t0 = (int64_t)blockIdx.x * XN, r0 = (int64_t)blockIdx.y * XM;
+    const int64_t t0 = (int64_t)blockIdx.x * N4, r0 = (int64_t)blockIdx.y * M4;
     const int64_t n_rt = g.n_rt, n_bt = g.n_bt, nb = g.nb;
 
     // [token group][AVX2 lane][row pair]: rows (2p, 2p+1) of one lane chain pair as one float2, as
@@ -774,14 +777,14 @@ k_gemm_x4(gemm_args g) {
             for (int p2 = 0; p2 < 2; ++p2) acc[c][l][p2] = xf2{0.0f, 0.0f};
 
     typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-    u4v wq[WREC], ws[WREC], xr[XREC];
-    float xd[XDA];
+    u4v wq[WREC], ws[WREC], xr[XREC4];
+    float xd[XDA4];
     auto gload = [&](int64_t kb0) {  // k_gemm_x's stage loads
 #pragma unroll
         for (int k = 0; k < WREC; ++k) {
-            const int rec = tid + XNT * k, tile_i = (rec >> 6) & 7, ln = rec & 63, rr = ln >> 3;
+            const int rec = tid + XNT * k, tile_i = rec >> 6, ln = rec & 63, rr = ln >> 3;
             if (rec >= WRECS) break;  // wave-uniform
-            const int rti = (WT == T_Q4_0) ? (tile_i & 3) : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
+            const int rti = (WT == T_Q4_0) ? tile_i : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
             int64_t rt = r0 / 8 + rti, bt = kb0 / BT + bti;
             const bool ok = rt < n_rt && bt < n_bt;
             rt = ok ? rt : 0;
@@ -793,14 +796,14 @@ k_gemm_x4(gemm_args g) {
             if (!ok) { wq[k] = u4v{0u, 0u, 0u, 0u}; ws[k] = u4v{0u, 0u, 0u, 0u}; }
         }
 #pragma unroll
-        for (int k = 0; k < XREC; ++k) {
+        for (int k = 0; k < XREC4; ++k) {
             const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
             const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
             xr[k] = *(const u4v *)(g.xh + t * g.ldq + kb0 * 32 + seg * 8);
         }
 #pragma unroll
-        for (int k = 0; k < XDA; ++k) {
-            const int c = (tid + XNT * k) % (XN * 8), tok = c >> 3, b = c & 7;
+        for (int k = 0; k < XDA4; ++k) {
+            const int c = (tid + XNT * k) % (N4 * 8), tok = c >> 3, b = c & 7;
             const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
             xd[k] = (kb0 + b < nb) ? g.da[t * g.ldd + kb0 + b] : 0.0f;
         }
@@ -808,10 +811,10 @@ k_gemm_x4(gemm_args g) {
     auto lstore = [&]() {
 #pragma unroll
         for (int k = 0; k < WREC; ++k) {
-            const int rec = tid + XNT * k, tile_i = (rec >> 6) & 7, ln = rec & 63, rr = ln >> 3, l = ln & 7;
+            const int rec = tid + XNT * k, tile_i = rec >> 6, ln = rec & 63, rr = ln >> 3, l = ln & 7;
             if (rec >= WRECS) break;  // wave-uniform
-            const int rti = (WT == T_Q4_0) ? (tile_i & 3) : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
-            const int row = rti * 8 + rr;  // 0..31
+            const int rti = (WT == T_Q4_0) ? tile_i : (tile_i >> 1), bti = (WT == T_Q4_0) ? 0 : (tile_i & 1);
+            const int row = rti * 8 + rr;  // 0..M4-1
             const uint32_t qd[4] = {wq[k].x, wq[k].y, wq[k].z, wq[k].w};
             const uint32_t sd[4] = {ws[k].x, ws[k].y, ws[k].z, ws[k].w};
             // row slot swizzled by the lane: (row & 15) ^ 2l, so each 16-lane group (rr 2 values x l 0..7)
@@ -839,15 +842,15 @@ k_gemm_x4(gemm_args g) {
         // compiler's ds_read2_b64 of B (16-lane groups, banks mod 32) sees tokens j and j + 8 on
         // different banks (pitch 528 B alone: 2-way)
 #pragma unroll
-        for (int k = 0; k < XREC; ++k) {
+        for (int k = 0; k < XREC4; ++k) {
             const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
             const u4v v = xr[k];
             *(u4v *)(Xs + tok * XS_ROW + seg * 16) = (tok & 8) ? u4v{v.z, v.w, v.x, v.y} : v;
         }
 #pragma unroll
-        for (int k = 0; k < XDA; ++k) {
+        for (int k = 0; k < XDA4; ++k) {
             const int c = tid + XNT * k;
-            if (c < XN * 8) das[c & 7][c >> 3] = xd[k];
+            if (c < N4 * 8) das[c & 7][c >> 3] = xd[k];
         }
     };
     // this lane's operand addresses: A column (row group rg, AVX2 lane 4*ih + q, row l16), B (token
@@ -1168,10 +1171,12 @@ int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s) {
     return 0;
 }
 
-// which exact GEMM runs (hpc_set_gemm_x4 / the engine option "gemm_x4"): 0 the lane-masked W32 form
-// (k_gemm_x), 1 the K = 4 multi-block form (k_gemm_x4); same bits either way
-static std::atomic<int> g_gemm_x4{0};
+// which exact GEMM runs (hpc_set_gemm_x4): 0 the lane-masked W32 form (k_gemm_x), 1 the K = 4
+// multi-block form (k_gemm_x4, 32 rows x 64 tokens per workgroup: the default, T = 2048 prefill 70.9
+// vs 77.6 ms), 2 the same with 64 x 32 (72.3 ms); same bits every way
+static std::atomic<int> g_gemm_x4{1};
 bool gemm_x4_on() { return g_gemm_x4.load() != 0; }
+int gemm_x4_mode() { return g_gemm_x4.load(); }  // 1: 32 rows x 64 tokens per workgroup, 2: 64 x 32
 void set_gemm_x4(int v) { g_gemm_x4.store(v); }
 
 int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
@@ -1186,10 +1191,18 @@ int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
     }
     const dim3 grid((unsigned)((g.T + XN - 1) / XN), (unsigned)gy);
     if (gemm_x4_on()) {  // the K = 4 multi-block MFMA form
-        if (wtype == T_Q4_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x4<T_Q4_0, EPI_STORE>), grid, dim3(XNT), 0, s, g);
-        else if (wtype == T_Q4_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x4<T_Q4_0, EPI_ADD>), grid, dim3(XNT), 0, s, g);
-        else if (wtype == T_Q8_0 && epi == EPI_STORE) hipLaunchKernelGGL((k_gemm_x4<T_Q8_0, EPI_STORE>), grid, dim3(XNT), 0, s, g);
-        else if (wtype == T_Q8_0 && epi == EPI_ADD) hipLaunchKernelGGL((k_gemm_x4<T_Q8_0, EPI_ADD>), grid, dim3(XNT), 0, s, g);
+        const int rgs = gemm_x4_mode() == 2 ? 4 : 2;
+        const dim3 grid4((unsigned)((g.T + 32 * (4 / rgs) - 1) / (32 * (4 / rgs))), (unsigned)((g.rows + 16 * rgs - 1) / (16 * rgs)));
+#define X4_GO(W, E)                                                                                          \
+    do {                                                                                                     \
+        if (rgs == 4) hipLaunchKernelGGL((k_gemm_x4<W, E, 4>), grid4, dim3(XNT), 0, s, g);                   \
+        else hipLaunchKernelGGL((k_gemm_x4<W, E, 2>), grid4, dim3(XNT), 0, s, g);                            \
+    } while (0)
+        if (wtype == T_Q4_0 && epi == EPI_STORE) X4_GO(T_Q4_0, EPI_STORE);
+        else if (wtype == T_Q4_0 && epi == EPI_ADD) X4_GO(T_Q4_0, EPI_ADD);
+        else if (wtype == T_Q8_0 && epi == EPI_STORE) X4_GO(T_Q8_0, EPI_STORE);
+        else if (wtype == T_Q8_0 && epi == EPI_ADD) X4_GO(T_Q8_0, EPI_ADD);
+#undef X4_GO
         else {
             set_error("gemm_exact: unsupported (type, epilogue)");
             return -1;

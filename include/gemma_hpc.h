@@ -50,8 +50,9 @@ void hpc_set_matvec_ks(int ks);          /* K-split of the quantized matvec (1/2
 /* columns from which K-quant mul_mats (and the K-quant engine prefill) run the MFMA GEMM
  * (prefill_kq.hip) instead of the dot4 kernels; -1 = GHIP_KQ_MFMA_MIN or 8 (tests: same bytes) */
 void hpc_set_kq_gemm_min(int min_cols);
-/* the exact Q4_0 / Q8_0 prefill GEMM's form: 1 = K = 4 multi-block MFMA (k_gemm_x4, dense lane
-   fragments), 0 = the lane-masked 32x32x16 form (k_gemm_x); bit-identical either way */
+/* the exact Q4_0 / Q8_0 prefill GEMM's form: 1 (default) = K = 4 multi-block MFMA (k_gemm_x4, dense
+   lane fragments, 32 rows x 64 tokens per workgroup), 2 = the same with 64 x 32, 0 = the lane-masked
+   32x32x16 form (k_gemm_x); bit-identical every way */
 void hpc_set_gemm_x4(int on);
 
 /* ---- graph executor (SURVEY §8(b) `hpc_graph_compute(ggml_cgraph*)`): runs a graph built with the

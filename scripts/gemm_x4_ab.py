@@ -16,10 +16,10 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
 e = G.Engine(GEMMA_2B, n_ctx=T + 64, device=0)
 p = make_prompt(T, GEMMA_2B["n_vocab"], seed=2)
-res = {0: [], 1: []}
+res = {0: [], 1: [], 2: []}
 toks = {}
 for r in range(reps + 1):
-    for on in (0, 1):
+    for on in (0, 1, 2):
         G.lib().hpc_set_gemm_x4(on)
         e.begin(p)
         e.sync()
@@ -30,6 +30,7 @@ for r in range(reps + 1):
         if r:
             res[on].append(dt * 1e3)
         print(f"rep {r} x4 {on}: {dt * 1e3:.2f} ms token {tok}", flush=True)
-G.lib().hpc_set_gemm_x4(0)
-print("W32 ms", [round(v, 2) for v in res[0]], "x4 ms", [round(v, 2) for v in res[1]], "tokens equal", toks[0] == toks[1])
+G.lib().hpc_set_gemm_x4(1)
+print("W32 ms", [round(v, 2) for v in res[0]], "x4 32x64 ms", [round(v, 2) for v in res[1]], "x4 64x32 ms",
+      [round(v, 2) for v in res[2]], "tokens equal", toks[0] == toks[1] == toks[2])
 e.close()

@@ -11,7 +11,9 @@ import sys
 
 root, out = sys.argv[1], sys.argv[2]
 KERNELS = {
-    "k_gemm_x": "exact Q4_0 prefill GEMMs (all 18 layers + logits, one T=2048 pass); MFMA util counts ISSUED "
+    "k_gemm_x4": "exact Q4_0 prefill GEMMs on v_mfma_f32_16x16x4_4b_f16 (all 18 layers + logits, one T=2048 pass): one "
+                 "instruction block = one AVX2 lane, every product useful; 3 waves per SIMD (DESIGN.md §5b)",
+    "k_gemm_x<": "exact Q4_0 prefill GEMMs (all 18 layers + logits, one T=2048 pass); MFMA util counts ISSUED "
                 "MFMA cycles: the lane-masked f16 MFMAs carry 4x the useful products (DESIGN.md §5b)",
     "k_attn_rows": "exact prefill attention, row form (per row, v_fma_mix chains; GHIP_ATT_MX=0)",
     "k_attn_mx": "exact prefill attention on the f32 matrix cores (vec_dot_f16's 32 fmaf chains on "
@@ -23,7 +25,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(root + "/pmc*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         for k in KERNELS:
-            if k in r["Kernel_Name"]:
+            if k in r["Kernel_Name"].replace("ghip::(anonymous namespace)::", ""):
                 agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
 res = {}
 for k, a in agg.items():

@@ -13,8 +13,8 @@ from bench import GEMMA_2B, make_prompt  # noqa: E402
 T = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 exact = (sys.argv[2] != "0") if len(sys.argv) > 2 else True
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-if os.environ.get("X4") == "1":  # the K = 4 multi-block exact GEMM (k_gemm_x4)
-    G.lib().hpc_set_gemm_x4(1)
+if os.environ.get("X4"):  # the exact GEMM form (hpc_set_gemm_x4: 0 W32, 1 K = 4 (default), 2 K = 4 64 x 32)
+    G.lib().hpc_set_gemm_x4(int(os.environ["X4"]))
 e = G.Engine(GEMMA_2B, n_ctx=T + 64, device=0)
 p = make_prompt(T, GEMMA_2B["n_vocab"], seed=2)
 for r in range(reps + 1):

@@ -11,12 +11,17 @@ from test_gpu_prefill import _gemm, _prefill_exact_case
 gpu = pytest.mark.gpu
 
 
-@pytest.fixture
-def x4():
+DEFAULT = 1  # hpc_set_gemm_x4's default form
+
+
+@pytest.fixture(params=[0, 1, 2], ids=["w32", "x4_32x64", "x4_64x32"])
+def x4(request):
+    """every exact GEMM form: the lane-masked W32 kernel (0), the K = 4 kernel with 32 rows x 64
+    tokens (1, the default) and 64 x 32 (2)"""
     import gemma_hip as G
-    G.lib().hpc_set_gemm_x4(1)
-    yield
-    G.lib().hpc_set_gemm_x4(0)
+    G.lib().hpc_set_gemm_x4(request.param)
+    yield request.param
+    G.lib().hpc_set_gemm_x4(DEFAULT)
 
 
 @gpu
@@ -82,7 +87,7 @@ def test_prefill_x4_full_size_equals_w32():
     prompt = O.make_prompt(T, shape["n_vocab"], seed=2)
     out = []
     try:
-        for on in (0, 1):
+        for on in (0, 1, 2):
             G.lib().hpc_set_gemm_x4(on)
             e = G.Engine(shape, n_ctx=T + 64, device=0)
             e.begin(prompt)
@@ -90,7 +95,8 @@ def test_prefill_x4_full_size_equals_w32():
             out.append((tok, last, e.step(2, want_logits=True, use_graph=True)))
             e.close()
     finally:
-        G.lib().hpc_set_gemm_x4(0)
-    assert out[0][0] == out[1][0]
-    assert np.array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))
-    assert np.array_equal(out[0][2].view(np.uint32), out[1][2].view(np.uint32))
+        G.lib().hpc_set_gemm_x4(DEFAULT)
+    for o in out[1:]:
+        assert out[0][0] == o[0]
+        assert np.array_equal(out[0][1].view(np.uint32), o[1].view(np.uint32))
+        assert np.array_equal(out[0][2].view(np.uint32), o[2].view(np.uint32))
