@@ -4,6 +4,8 @@ import os
 import sys
 import time
 
+import torch  # noqa: F401  (the HIP runtime bench.py runs on)
+
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gemma.ggml_amd", "python"))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import gemma_hip as G  # noqa: E402
