@@ -1,5 +1,5 @@
 """A/B of the exact T = 2048 Gemma-2B Q4_0 prefill with the W32 GEMM (hpc_set_gemm_x4(0)) and the
-K = 4 multi-block form (1), interleaved reps on one engine.  usage: gemm_x4_ab.py [reps] [T]"""
+K = 4 multi-block forms (1: 32x64, 2: 64x32), interleaved reps on one engine.  usage: gemm_x4_ab.py [reps] [T] [modes, e.g. 0,1,3]"""
 import os
 import sys
 import time
@@ -14,12 +14,13 @@ from bench import GEMMA_2B, make_prompt  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+MODES = [int(m) for m in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1, 2]
 e = G.Engine(GEMMA_2B, n_ctx=T + 64, device=0)
 p = make_prompt(T, GEMMA_2B["n_vocab"], seed=2)
-res = {0: [], 1: [], 2: []}
+res = {m: [] for m in MODES}
 toks = {}
 for r in range(reps + 1):
-    for on in (0, 1, 2):
+    for on in MODES:
         G.lib().hpc_set_gemm_x4(on)
         e.begin(p)
         e.sync()
@@ -31,6 +32,7 @@ for r in range(reps + 1):
             res[on].append(dt * 1e3)
         print(f"rep {r} x4 {on}: {dt * 1e3:.2f} ms token {tok}", flush=True)
 G.lib().hpc_set_gemm_x4(1)
-print("W32 ms", [round(v, 2) for v in res[0]], "x4 32x64 ms", [round(v, 2) for v in res[1]], "x4 64x32 ms",
-      [round(v, 2) for v in res[2]], "tokens equal", toks[0] == toks[1] == toks[2])
+NAMES = {0: "W32", 1: "x4 32x64", 2: "x4 64x32"}
+print(" ".join(f"{NAMES[m]} ms {[round(v, 2) for v in res[m]]}" for m in MODES),
+      "tokens equal", len(set(toks.values())) == 1)
 e.close()

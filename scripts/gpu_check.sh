@@ -36,7 +36,7 @@ for w in $WHAT; do
     steps) export GHIP_ALLOW_ALT_LIB=1; GHIP_LIB=ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 9 > $OUT/stamp_step.log 2>&1 && GHIP_LIB=ab_libs/libstamps.so timeout -k 10 180 python tests/stamp_step.py 17 >> $OUT/stamp_step.log 2>&1 || { cat $OUT/stamp_step.log; exit 1; } ; cat $OUT/stamp_step.log ;;
     k4probe) timeout -k 10 120 tests/micro/mfma_k4 > $OUT/mfma_k4.log 2>&1 || { tail -20 $OUT/mfma_k4.log; exit 1; } ; cat $OUT/mfma_k4.log ;;
     attostamps) GHIP_ALLOW_ALT_LIB=1 GHIP_LIB=ab_libs/libstamps.so timeout -k 10 180 python scripts/attn_o_stamps.py 9 > $OUT/attn_o_stamps.log 2>&1 || { tail -20 $OUT/attn_o_stamps.log; exit 1; } ; cat $OUT/attn_o_stamps.log ;;
-    x4ab) timeout -k 10 300 python scripts/gemm_x4_ab.py 3 2048 > $OUT/gemm_x4_ab.log 2>&1 || { tail -20 $OUT/gemm_x4_ab.log; exit 1; } ; cat $OUT/gemm_x4_ab.log ;;
+    x4ab) timeout -k 10 300 python scripts/gemm_x4_ab.py 3 2048 ${X4MODES:-0,1,2} > $OUT/gemm_x4_ab.log 2>&1 || { tail -20 $OUT/gemm_x4_ab.log; exit 1; } ; cat $OUT/gemm_x4_ab.log ;;
     attoab) timeout -k 10 300 python scripts/att_o_ab.py 3 64 > $OUT/att_o_ab.log 2>&1 || { tail -20 $OUT/att_o_ab.log; exit 1; } ; cat $OUT/att_o_ab.log ;;
     gputest) timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_sel.log 2>&1 || { tail -40 $OUT/pytest_sel.log; exit 1; } ; tail -15 $OUT/pytest_sel.log ;;
     # the graph-replay trace on /opt/rocm's HIP runtime (no torch): the configuration that crashed in
