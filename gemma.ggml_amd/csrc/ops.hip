@@ -714,7 +714,19 @@ __global__ void __launch_bounds__(256) k_reduce_keys(const unsigned long long *k
 __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys, int n_parts, int *token, int *pos,
                                                  int *hist, int hist_cap, const int *n_fixed, rope_row r) {
     __shared__ unsigned long long red[4];
-    __shared__ int sp;
+    // the next position does not depend on the argmax: every thread reads *pos first (one line), so
+    // the RoPE row copy of position p overlaps the key loads instead of waiting for the reduction and
+    // a second dependent load of *pos (three serial memory round trips -> one; thread 0 writes *pos
+    // only after the barrier below, which every read precedes)
+    const int p = *pos + 1;
+    const int fixed = hist ? *n_fixed : 0;
+    if (r.cur && p < r.ctx) {  // the RoPE row of the next position, at a fixed address (attention loads it without *pos)
+        for (int i = threadIdx.x; i < r.half; i += 256) {
+            r.cur[i] = r.cos[(int64_t)p * r.half + i];
+            r.cur[r.half + i] = r.sin[(int64_t)p * r.half + i];
+        }
+        if (threadIdx.x == 0) ((int *)r.cur)[2 * r.half] = p;
+    }
     unsigned long long best = 0;
     for (int i = threadIdx.x; i < n_parts; i += 256) best = keys[i] > best ? keys[i] : best;
 #pragma unroll
@@ -728,21 +740,10 @@ __global__ void __launch_bounds__(256) k_advance(const unsigned long long *keys,
         for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
         // strict '>' argmax, first max wins (src/gemma_model.cpp:538-543): the key's low word is ~index
         const int idx = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
-        const int p = *pos + 1;
         *token = idx;
-        if (hist && p < hist_cap && p >= *n_fixed) hist[p] = idx;  // never overwrite the prompt
+        if (hist && p < hist_cap && p >= fixed) hist[p] = idx;  // never overwrite the prompt
         *pos = p;
-        sp = p;
         if (r.epoch) ++*r.epoch;  // a new token: fresh granule tags for the persistent launch
-    }
-    __syncthreads();
-    // the RoPE row of the next position, at a fixed address (attention loads it without *pos)
-    if (r.cur && sp < r.ctx) {
-        for (int i = threadIdx.x; i < r.half; i += 256) {
-            r.cur[i] = r.cos[(int64_t)sp * r.half + i];
-            r.cur[r.half + i] = r.sin[(int64_t)sp * r.half + i];
-        }
-        if (threadIdx.x == 0) ((int *)r.cur)[2 * r.half] = sp;
     }
 }
 
