@@ -388,7 +388,7 @@ def main():
     ap.add_argument("--no-tune", action="store_true", help="default launch plan instead of the measured one")
     ap.add_argument("--tp-steps", type=int, default=48, help="Gemma-7B row-split decode leg steps (0 = skip)")
     ap.add_argument("--q8-steps", type=int, default=48, help="Gemma-2B Q8_0 decode leg steps (0 = skip)")
-    ap.add_argument("--tp-timeout", type=int, default=240, help="time limit of the TP leg's child processes (s)")
+    ap.add_argument("--tp-timeout", type=int, default=360, help="time limit of the TP leg's child processes (s)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -721,7 +721,7 @@ def main():
                 line["value"] = line["decode_tok_s"] = tp2["tok_s"]
                 line["ms_per_step"] = tp2["ms_per_token"]
                 line["scaling"] = "strong"
-                line["config"]["parallelism"] = f"row-split tp{world} (RCCL all-gather x4/layer)"
+                line["config"]["parallelism"] = tp2.get("parallelism") or f"row-split tp{world}"
                 line["config"]["workload"] = (f"ONE Gemma-2B {args.wtype.upper()} greedy decode stream, batch 1, every "
                                               f"weight matrix row-split over {world} GPUs, after a {args.prompt}-token "
                                               f"prompt (BASELINE config 2 partitioned as the north star asks)")

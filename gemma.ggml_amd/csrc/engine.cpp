@@ -212,6 +212,10 @@ struct gemma_engine {
     bool tp_n_keys = false;  // logits through per-rank argmax keys (row split: virtual ranks or an RCCL comm)
     ncclComm_t comm = nullptr;
     int64_t sh_qkv = 0, sh_e = 0, sh_ff = 0, sh_v = 0;  // rows per rank (qkv, n_embd, n_ff, n_vocab)
+    // GEMMA_TP_REP_ATTN: Wq|Wk|Wv and Wo whole on every rank (sh_qkv = all rows, sh_o = n_embd), so
+    // a layer needs 2 all-gathers (h, x) instead of 4; the FFN and the output head stay row-split
+    bool rep_attn = false;
+    int64_t sh_o = 0;
     unsigned long long *rank_keys = nullptr;           // [tp_n] one argmax key per rank
     attn_geom ag;                           // split-attention geometry and its scratch
     float *att_sbuf = nullptr;
@@ -525,7 +529,7 @@ static int enqueue_step(gemma_engine *e) {
         }
         {
         // K1: [embed | rms_norm*attn_norm] + quantize -> Wq|Wk|Wv   (:677-696); each rank its rows
-        for (int vr = 0; vr < e->n_virtual; ++vr) {
+        for (int vr = 0; vr < (e->rep_attn ? 1 : e->n_virtual); ++vr) {
             layer_dev &L = layer_of(e, il, vr);
             mv_args a;
             a.qs = L.qkv.qs; a.sc = L.qkv.sc; a.rows = L.qkv.rows; a.n_rt = L.qkv.n_rt; a.n_bt = L.qkv.n_bt;
@@ -542,10 +546,10 @@ static int enqueue_step(gemma_engine *e) {
                 a.x = e->x;
             }
             a.dbg_t = stamp_region(e, il, 0);
-            a.y = e->qkv + (size_t)rank_of(e, vr) * e->sh_qkv;  // this rank's rows of q|k|v
+            a.y = e->qkv + (e->rep_attn ? 0 : (size_t)rank_of(e, vr) * e->sh_qkv);  // this rank's rows of q|k|v
             if (launch_matvec(wt, pick_ks(wt, L.qkv.n_bt, e->plan[MC_QKV].ks), pro, EPI_STORE, a, mv_grid(e, MC_QKV, L.qkv.n_rt), s)) return -1;
         }
-        if (tp_gather(e, e->qkv, e->sh_qkv)) return -1;
+        if (!e->rep_attn && tp_gather(e, e->qkv, e->sh_qkv)) return -1;
         // K2: rope + scale + kv store + KQ + softmax + KQV  (:698-718, :454-518); replicated
         attn_args t;
         t.qkv = e->qkv;
@@ -564,7 +568,7 @@ static int enqueue_step(gemma_engine *e) {
         // attention + attn-out in one launch (k_attn_o): the attention's idle workgroups run attn-out
         if (e->att_o && att_img && e->n_virtual == 1 && e->ao_cnt && e->plan[MC_O].ks == KS_RR) {
             const layer_dev &L = layer_of(e, il, 0);
-            const size_t r0 = (size_t)rank_of(e, 0) * e->sh_e;
+            const size_t r0 = e->rep_attn ? 0 : (size_t)rank_of(e, 0) * e->sh_o;
             attn_o_args f;
             f.t = t;
             f.o.qs = L.o.qs; f.o.sc = L.o.sc; f.o.rows = L.o.rows; f.o.n_rt = L.o.n_rt; f.o.n_bt = L.o.n_bt; f.o.nb = L.o.nb;
@@ -579,7 +583,7 @@ static int enqueue_step(gemma_engine *e) {
                 if (e->dbg) GHIP_CHECK(hipMemcpyAsync(e->dbg + tap, e->qkv, (size_t)e->qkv_rows * 4, hipMemcpyDeviceToDevice, s));
                 if (e->dbg)
                     GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows, e->attn, (size_t)e->qw * 4, hipMemcpyDeviceToDevice, s));
-                if (tp_gather(e, e->sa, e->sh_e)) return -1;
+                if (!e->rep_attn && tp_gather(e, e->sa, e->sh_o)) return -1;
                 goto ffn;
             }
         }
@@ -589,9 +593,9 @@ static int enqueue_step(gemma_engine *e) {
         if (e->dbg)
             GHIP_CHECK(hipMemcpyAsync(e->dbg + tap + e->qkv_rows, e->attn, (size_t)e->qw * 4, hipMemcpyDeviceToDevice, s));
         // K3: quantize(attn) -> Wo, + inpL  (:493, :723)
-        for (int vr = 0; vr < e->n_virtual; ++vr) {
+        for (int vr = 0; vr < (e->rep_attn ? 1 : e->n_virtual); ++vr) {
             layer_dev &L = layer_of(e, il, vr);
-            const size_t r0 = (size_t)rank_of(e, vr) * e->sh_e;
+            const size_t r0 = e->rep_attn ? 0 : (size_t)rank_of(e, vr) * e->sh_o;
             mv_args b;
             b.qs = L.o.qs; b.sc = L.o.sc; b.rows = L.o.rows; b.n_rt = L.o.n_rt; b.n_bt = L.o.n_bt; b.nb = L.o.nb;
             b.x = e->attn; b.y = e->sa + r0; b.resid = e->x + r0;
@@ -601,7 +605,7 @@ static int enqueue_step(gemma_engine *e) {
                               mv_grid(e, MC_O, L.o.n_rt), s))
                 return -1;
         }
-        if (tp_gather(e, e->sa, e->sh_e)) return -1;
+        if (!e->rep_attn && tp_gather(e, e->sa, e->sh_o)) return -1;
         }
     ffn:
         // K4: rms_norm*ffn_norm + quantize -> gate & up -> gelu(gate)*up  (:724, :446-449)
@@ -755,7 +759,7 @@ static int enqueue_step_kq(gemma_engine *e, const rope_row &rr) {
             k.q8_abl = e->kq_abl;
         }
         if (up) k.w2 = up->w;
-                return k;
+        return k;
     };
     auto mv = [&](const kq_mat &W, float *y, const float *resid, const float *gate_in, const img &in, const out &o,
                   const kq_mat *up) { return launch_matvec_kq(W.type, args(W, y, resid, gate_in, in, o, up), s); };
@@ -878,7 +882,7 @@ static int upload_rows(const tiled_mat &dst, const void *host, int64_t r0, hipSt
 
 static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int tp_n, int tp_rank, const void *nccl_id,
                                    const host_weights *hw = nullptr, const std::vector<uint16_t *> *kc_ext = nullptr,
-                                   const std::vector<uint16_t *> *vc_ext = nullptr) {
+                                   const std::vector<uint16_t *> *vc_ext = nullptr, int tp_flags = 0) {
     set_error("");
     const gemma_hip_config &c = *cfg;
     const bool kq_layers = c.wtype == T_Q4_K;  // K-quant layers (Q4_K / Q6_K per matrix) + Q6_K output
@@ -913,15 +917,17 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     e->qkv_rows = e->qw + 2 * e->kvw;
     e->tp_n = tp_n;
     e->tp_rank = tp_rank;
-    // every matrix is cut into tp_n contiguous row ranges of whole 8-row tiles
-    if (tp_n < 1 || tp_rank < 0 || tp_rank >= tp_n || e->qkv_rows % (8 * tp_n) || c.n_embd % (8 * tp_n) ||
-        c.n_ff % (8 * tp_n) || c.n_vocab % (8 * tp_n)) {
+    e->rep_attn = tp_n > 1 && (tp_flags & GEMMA_TP_REP_ATTN);
+    // every split matrix is cut into tp_n contiguous row ranges of whole 8-row tiles
+    if (tp_n < 1 || tp_rank < 0 || tp_rank >= tp_n || (!e->rep_attn && e->qkv_rows % (8 * tp_n)) ||
+        c.n_embd % (8 * tp_n) || c.n_ff % (8 * tp_n) || c.n_vocab % (8 * tp_n) || (tp_flags & ~GEMMA_TP_REP_ATTN)) {
         set_error("gemma_engine_create: row split needs every matrix's rows to divide into 8-row tiles per rank");
         delete e;
         return nullptr;
     }
-    e->sh_qkv = e->qkv_rows / tp_n;
+    e->sh_qkv = e->rep_attn ? e->qkv_rows : e->qkv_rows / tp_n;
     e->sh_e = c.n_embd / tp_n;
+    e->sh_o = e->rep_attn ? c.n_embd : e->sh_e;
     e->sh_ff = c.n_ff / tp_n;
     e->sh_v = c.n_vocab / tp_n;
     const int wt = c.wtype;
@@ -1020,9 +1026,12 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
             make(K.down, H ? H->td : T_Q6_K, c.n_embd, c.n_ff, L_DOWN, 4.0 * sf, H ? H->down : nullptr);
             continue;
         }
+        // replicated attention block: one whole copy in slot 0 (virtual slots > 0 hold none)
+        const bool att_here = !e->rep_attn || vr == 0;
+        const int64_t o0 = e->rep_attn ? 0 : (int64_t)tp_rank * e->sh_o;
         // this rank's rows [r0, r0 + n) of the fused [Wq | Wk | Wv]: the pieces of each source tensor
-        const int64_t q0 = (int64_t)tp_rank * e->sh_qkv, qn = e->sh_qkv;
-        L.qkv = alloc_tiled(wt, qn, c.n_embd, s);
+        const int64_t q0 = e->rep_attn ? 0 : (int64_t)tp_rank * e->sh_qkv, qn = att_here ? e->sh_qkv : 0;
+        if (att_here) L.qkv = alloc_tiled(wt, qn, c.n_embd, s);
         const int64_t src_start[3] = {0, e->qw, e->qw + e->kvw}, src_rows[3] = {e->qw, e->kvw, e->kvw};
         const int src_tid[3] = {L_Q, L_K, L_V};
         const void *src_host[3] = {hw ? hw->layers[il].q : nullptr, hw ? hw->layers[il].k : nullptr,
@@ -1038,18 +1047,20 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         }
         if (hw) {
             const host_weights::layer &H = hw->layers[il];
-            L.o = alloc_tiled(wt, e->sh_e, e->qw, s);
+            if (att_here) L.o = alloc_tiled(wt, e->sh_o, e->qw, s);
             L.gate = alloc_tiled(wt, e->sh_ff, c.n_embd, s);
             L.up = alloc_tiled(wt, e->sh_ff, c.n_embd, s);
             L.down = alloc_tiled(wt, e->sh_e, c.n_ff, s);
-            up_fail |= upload_rows(L.o, H.o, (int64_t)tp_rank * e->sh_e, s) != 0;
+            if (att_here) up_fail |= upload_rows(L.o, H.o, o0, s) != 0;
             up_fail |= upload_rows(L.gate, H.gate, (int64_t)tp_rank * e->sh_ff, s) != 0;
             up_fail |= upload_rows(L.up, H.up, (int64_t)tp_rank * e->sh_ff, s) != 0;
             up_fail |= upload_rows(L.down, H.down, (int64_t)tp_rank * e->sh_e, s) != 0;
             continue;
         }
-        L.o = alloc_tiled(wt, e->sh_e, e->qw, s);
-        launch_synth_tiled(L.o, tensor_key(seed, tid_layer(il, L_O)), synth_scale(4.0 * sq), (int64_t)tp_rank * e->sh_e, s);
+        if (att_here) {
+            L.o = alloc_tiled(wt, e->sh_o, e->qw, s);
+            launch_synth_tiled(L.o, tensor_key(seed, tid_layer(il, L_O)), synth_scale(4.0 * sq), o0, s);
+        }
         L.gate = alloc_tiled(wt, e->sh_ff, c.n_embd, s);
         launch_synth_tiled(L.gate, tensor_key(seed, tid_layer(il, L_GATE)), synth_scale(se), (int64_t)tp_rank * e->sh_ff, s);
         L.up = alloc_tiled(wt, e->sh_ff, c.n_embd, s);
@@ -1345,6 +1356,14 @@ extern "C" gemma_engine *gemma_engine_create_tp(const gemma_hip_config *cfg, int
                                                 const void *nccl_id) {
     return engine_create(cfg, device, n_ranks, nccl_id ? rank : 0, nccl_id);
 }
+
+// the same with layout flags (GEMMA_TP_REP_ATTN: the attention block whole on every rank)
+extern "C" gemma_engine *gemma_engine_create_tp2(const gemma_hip_config *cfg, int device, int n_ranks, int rank,
+                                                 const void *nccl_id, int flags) {
+    return engine_create(cfg, device, n_ranks, nccl_id ? rank : 0, nccl_id, nullptr, nullptr, nullptr, flags);
+}
+
+extern "C" int gemma_engine_tp_flags(const gemma_engine *e) { return e ? (e->rep_attn ? GEMMA_TP_REP_ATTN : 0) : -1; }
 
 static void drop_graph(gemma_engine *e);
 

@@ -30,7 +30,7 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
            "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_att_o", "gemma_engine_set_option", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs", "gemma_hbm_read_probe",
-           "gemma_tp_unique_id", "gemma_engine_create_tp", "gemma_engine_tp_info", "gemma_engine_set_persist_timeout",
+           "gemma_tp_unique_id", "gemma_engine_create_tp", "gemma_engine_create_tp2", "gemma_engine_tp_flags", "gemma_engine_tp_info", "gemma_engine_set_persist_timeout",
            "gguf_init_from_file", "gguf_free", "gguf_get_n_kv", "gguf_get_key", "gguf_get_kv_type",
            "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
            "gguf_get_val_data", "gguf_get_n_tensors", "gguf_get_tensor_name", "gguf_get_tensor_type",
@@ -41,6 +41,9 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
 
 def build():
     subprocess.run(["make", "-s", "-j8", "-C", PKG_DIR], check=True)
+
+
+TP_REP_ATTN = 1  # include/gemma_hpc.h GEMMA_TP_REP_ATTN
 
 
 class GemmaConfig(C.Structure):
@@ -96,6 +99,10 @@ def lib():
     L.gemma_tp_unique_id.argtypes = [vp, C.c_int]
     L.gemma_engine_create_tp.restype = vp
     L.gemma_engine_create_tp.argtypes = [C.POINTER(GemmaConfig), C.c_int, C.c_int, C.c_int, vp]
+    L.gemma_engine_create_tp2.restype = vp
+    L.gemma_engine_create_tp2.argtypes = [C.POINTER(GemmaConfig), C.c_int, C.c_int, C.c_int, vp, C.c_int]
+    L.gemma_engine_tp_flags.restype = C.c_int
+    L.gemma_engine_tp_flags.argtypes = [vp]
     L.gemma_engine_create.restype = vp
     L.gemma_engine_create.argtypes = [C.POINTER(GemmaConfig), C.c_int]
     L.gemma_engine_free.argtypes = [vp]
@@ -209,15 +216,16 @@ def mul_mat(src0_bytes, src0_type, ne01, nb01, shared_edge, wdata, row_size, nco
 
 class Engine:
     def __init__(self, shape, n_ctx=512, wtype=GGML_TYPE_Q4_0, seed=0x6E6D6D61, eps=1e-6, rope_base=10000.0,
-                 gelu_clamp=0, device=0, tp=None, out_type=0, out_gain=0.0):
+                 gelu_clamp=0, device=0, tp=None, out_type=0, out_gain=0.0, tp_flags=0):
         """tp = (n_ranks, rank, rccl_id_bytes) for the row-split engine (one process per GPU);
-        rccl_id_bytes None = all ranks' shards virtual in this engine (single-GPU parity mode)."""
+        rccl_id_bytes None = all ranks' shards virtual in this engine (single-GPU parity mode).
+        tp_flags: TP_REP_ATTN keeps the attention block (Wq|Wk|Wv, Wo) whole on every rank."""
         self.cfg = GemmaConfig(n_ctx=n_ctx, wtype=wtype, eps=eps, rope_base=rope_base, seed=seed,
                                gelu_clamp=gelu_clamp, out_type=out_type, out_gain=out_gain, **shape)
         self.L = lib()
         if tp is not None and (tp[0] > 1 or tp[2] is not None):  # n_ranks 1 + id: a 1-rank RCCL comm
             idbuf = C.create_string_buffer(bytes(tp[2]), len(tp[2])) if tp[2] is not None else None
-            self.h = self.L.gemma_engine_create_tp(C.byref(self.cfg), device, tp[0], tp[1], idbuf)
+            self.h = self.L.gemma_engine_create_tp2(C.byref(self.cfg), device, tp[0], tp[1], idbuf, tp_flags)
         else:
             self.h = self.L.gemma_engine_create(C.byref(self.cfg), device)
         if not self.h:
@@ -341,6 +349,10 @@ class Engine:
     def set_persist_timeout(self, ticks):
         """the persistent launch's per-wait bound in 100 MHz ticks (0 = default; tests force timeouts)"""
         return self.L.gemma_engine_set_persist_timeout(self.h, ticks)
+
+    def tp_flags(self):
+        """layout flags of a row-split engine (TP_REP_ATTN)"""
+        return self.L.gemma_engine_tp_flags(self.h)
 
     def tp_info(self):
         """[ranks, rank, RCCL communicator present, shard slots in this engine]"""

@@ -16,6 +16,10 @@ tensors, so a test can drive it with world_size 2 on a machine without GPUs):
                 its split engine; the mismatch count is summed over ranks and any mismatch raises
                 ParityError (the leg's process exits 3)
   timed_steps   warmup, barrier + device sync, exactly K steps, device sync + barrier, max over ranks
+  layouts       the engine's row-split layouts (0: every matrix split, 4 all-gathers per layer;
+                TP_REP_ATTN: the attention block whole on every rank, 2 per layer) are each checked
+                and timed in lockstep; the faster (by the max-over-ranks time every rank holds) is
+                the stream's rate, the other is reported beside it
 
 The engine is injected (`make_engine(tp)`), so tests/test_tp_control.py runs this exact code with a
 stub engine on the CPU (gloo world 2, including a forced mismatch that must exit 3)."""
@@ -26,6 +30,12 @@ import numpy as np
 
 PLAN_CLASSES = ("qkv", "attn_out", "gate_up", "down", "logits")
 EXIT_PARITY = 3
+LAYOUT_NAMES = {0: "split", 1: "rep_attn"}
+
+
+def _mk(make_engine, tp, flags):
+    """make_engine(tp) for the plain split (the stub engines' signature), (tp, flags) otherwise"""
+    return make_engine(tp) if not flags else make_engine(tp, flags)
 
 
 class ParityError(RuntimeError):
@@ -164,16 +174,18 @@ def reference_hashes(comm, make_engine, prompt, n_check):
     return np.frombuffer(comm.bcast_bytes(raw, 8 * n_check), dtype=np.uint8), info
 
 
-def check_parity(comm, make_engine, make_id, prompt, n_check, ref):
+def check_parity(comm, make_engine, make_id, prompt, n_check, ref, layouts=(0,)):
     """Every rank's split engine(s) against the reference hashes; raises ParityError on any mismatch
     (after every rank has counted, so all ranks raise together).  World 1: 8 virtual ranks and a
-    1-rank RCCL communicator; world N: the N RCCL ranks."""
-    splits = [(comm.world, comm.rank, "rccl")] if comm.world > 1 else [(8, 0, None), (1, 0, "rccl")]
+    1-rank RCCL communicator; world N: the N RCCL ranks.  Each layout in `layouts` wherever the
+    engine has more than one rank (a 1-rank engine has a single layout)."""
+    base = [(comm.world, comm.rank, "rccl")] if comm.world > 1 else [(8, 0, None), (1, 0, "rccl")]
+    splits = [(sp, f) for f in layouts for sp in base if f == 0 or sp[0] > 1]
     nbad = 0
-    for split in splits:
+    for split, flags in splits:
         if split[2] == "rccl":
             split = (split[0], split[1], new_rccl_id(comm, make_id))
-        ce = make_engine(split)
+        ce = _mk(make_engine, split, flags)
         try:
             ce.begin(prompt)
             nbad += mismatched_rows(ref, row_hashes(ce.step(n_check, want_logits=True, use_graph=True)))
@@ -198,13 +210,15 @@ def timed_steps(comm, engine, steps, device_sync):
 
 
 def run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=True, tune_iters=6,
-               check_prompt=None, n_check=20, device_sync=lambda: None, unsplit_rate=True, kernel_iters=0):
+               check_prompt=None, n_check=20, device_sync=lambda: None, unsplit_rate=True, kernel_iters=0,
+               layouts=(0,)):
     """The whole row-split leg: parity of every rank against the unsplit engine, one timed stream
-    row-split over comm.world ranks, and (rank 0) the unsplit 1-GPU rate beside it.  Returns a dict
-    (meaningful on rank 0); raises ParityError on a mismatch."""
+    row-split over comm.world ranks per layout (the faster is the result), and (rank 0) the unsplit
+    1-GPU rate beside it.  Returns a dict (meaningful on rank 0); raises ParityError on a mismatch."""
     check_prompt = prompt[:16] if check_prompt is None else check_prompt
+    layouts = tuple(layouts) if comm.world > 1 else (0,)  # one rank: one layout
     ref, info = reference_hashes(comm, make_engine, check_prompt, n_check)
-    checked = check_parity(comm, make_engine, make_id, check_prompt, n_check, ref)
+    checked = check_parity(comm, make_engine, make_id, check_prompt, n_check, ref, layouts)
 
     tok_s_1, plan_1 = None, None
     if unsplit_rate and comm.rank == 0:  # the same treatment (tuned or not) as the split engine
@@ -221,26 +235,32 @@ def run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=True, tun
         finally:
             ue.close()
 
-    te = make_engine((comm.world, comm.rank, new_rccl_id(comm, make_id)))
-    try:
-        plan = share_plan(comm, te, tune, tune_iters)
-        te.begin(prompt)
-        te.step(len(prompt) + warmup, use_graph=True)  # the prompt token by token, then W warmup steps
-        dt = timed_steps(comm, te, steps, device_sync)
-        toks = [int(t) for t in te.tokens()]
-        kern = {}
-        for k in range(5 if kernel_iters > 0 else 0):
-            try:
-                us, algo = te.time_kernel(k, kernel_iters)
-                kern[k] = (us, algo)
-            except Exception:  # reported as missing, never fatal
-                pass
-    finally:
-        te.close()
+    runs = {}
+    for flags in layouts:  # every rank runs the same layouts in the same order (lockstep)
+        te = _mk(make_engine, (comm.world, comm.rank, new_rccl_id(comm, make_id)), flags)
+        try:
+            plan = share_plan(comm, te, tune, tune_iters)
+            te.begin(prompt)
+            te.step(len(prompt) + warmup, use_graph=True)  # the prompt token by token, then W warmup steps
+            dt = timed_steps(comm, te, steps, device_sync)
+            toks = [int(t) for t in te.tokens()]
+            kern = {}
+            for k in range(5 if kernel_iters > 0 else 0):
+                try:
+                    us, algo = te.time_kernel(k, kernel_iters)
+                    kern[k] = (us, algo)
+                except Exception:  # reported as missing, never fatal
+                    pass
+        finally:
+            te.close()
+        runs[flags] = (dt, plan, toks, kern)
+    best = min(runs, key=lambda f: runs[f][0])  # dt is the max over ranks: every rank picks the same
+    dt, plan, toks, kern = runs[best]
     tok_s = steps / dt
     out = {"ranks": comm.world, "tok_s": tok_s, "ms_per_token": dt / steps * 1e3, "steps": steps, "warmup": warmup,
            "timed_s": dt, "tok_s_unsplit_1gpu": tok_s_1, "launch_plan": plan, "launch_plan_unsplit": plan_1,
-           "tokens": toks, "kernels": kern,
+           "tokens": toks, "kernels": kern, "layout": LAYOUT_NAMES.get(best, best),
+           "layouts_tok_s": {LAYOUT_NAMES.get(f, f): steps / runs[f][0] for f in runs},
            "parity_check": {"rows": n_check, "mismatched_rows_all_ranks": 0,
                             "reference": "unsplit 1-GPU engine (rank 0), logits sha1 per row",
                             "split_checked": f"{comm.world} RCCL ranks" if comm.world > 1

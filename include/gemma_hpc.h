@@ -92,6 +92,13 @@ gemma_engine *gemma_engine_create_tp(const gemma_hip_config *cfg, int device, in
  * through RCCL (captured in the decode hipGraph) exactly as on N GPUs.  tp_info: [ranks, rank,
  * communicator present, shard slots in this engine] */
 int gemma_engine_tp_info(const gemma_engine *e, int *out4);
+/* layout flags for create_tp2: GEMMA_TP_REP_ATTN keeps Wq|Wk|Wv and Wo whole on every rank (the
+ * attention block replicated, 2 all-gathers per layer instead of 4; the FFN and the output head
+ * stay row-split; the same bits either way).  tp_flags returns the engine's flags. */
+#define GEMMA_TP_REP_ATTN 1
+gemma_engine *gemma_engine_create_tp2(const gemma_hip_config *cfg, int device, int n_ranks, int rank,
+                                      const void *nccl_id, int flags);
+int gemma_engine_tp_flags(const gemma_engine *e);
 void gemma_engine_free(gemma_engine *e);
 /* start a sequence: KV cache cleared, prompt stored on the device */
 int gemma_engine_begin(gemma_engine *e, const int32_t *prompt, int n_prompt);

@@ -54,15 +54,16 @@ def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None)
         wtype = G.GGML_TYPE_Q4_0 if wtype_s == "q4_0" else G.GGML_TYPE_Q8_0
         n_ctx = ((n_prompt + warmup + steps + 64) // 32 + 1) * 32
 
-        def make_engine(tp):
-            return G.Engine(shape, n_ctx=max(256, n_ctx), wtype=wtype, device=local_rank, tp=tp, out_gain=out_gain)
+        def make_engine(tp, flags=0):
+            return G.Engine(shape, n_ctx=max(256, n_ctx), wtype=wtype, device=local_rank, tp=tp, out_gain=out_gain,
+                            tp_flags=flags)
         make_id = G.tp_unique_id
         device_sync = lambda: torch.cuda.synchronize(local_rank)  # noqa: E731
     prompt = make_prompt(n_prompt, shape["n_vocab"])
     try:
         r = T.run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=tune,
                          check_prompt=make_prompt(16, shape["n_vocab"]), device_sync=device_sync or (lambda: None),
-                         kernel_iters=30 if model == "2b" else 0)
+                         kernel_iters=30 if model == "2b" else 0, layouts=(0, 1))
     except T.ParityError as ex:
         if comm.rank == 0:
             print(json.dumps({"error": str(ex)}), flush=True)
@@ -74,7 +75,8 @@ def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None)
         line = {"model": f"Gemma-{model.upper()} {wtype_s.upper()}", "ranks": world, "tok_s": round(tok_s, 2),
                 "ms_per_token": round(r["ms_per_token"], 4), "steps": steps, "warmup": warmup, "prompt": n_prompt,
                 "timed_s": round(r["timed_s"], 6),
-                "parallelism": f"row-split tp{world} (RCCL all-gather x4/layer)" if world > 1
+                "parallelism": (f"row-split tp{world}, layout {r['layout']} (RCCL all-gathers per layer: "
+                                f"{2 if r['layout'] == 'rep_attn' else 4})") if world > 1
                 else "1 GPU, 1-rank RCCL communicator (every gather through ncclAllGather in the hipGraph)",
                 "tok_s_unsplit_1gpu": round(tok_s_1, 2) if tok_s_1 else None,
                 # scaling fields only where ranks > 1; at N = 1 the ratio is the 1-rank RCCL
@@ -82,6 +84,8 @@ def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None)
                 "speedup_vs_1gpu": round(tok_s / tok_s_1, 3) if world > 1 and tok_s_1 else None,
                 "strong_scaling_efficiency": round(tok_s / tok_s_1 / world, 3) if world > 1 and tok_s_1 else None,
                 "rccl_overhead_vs_unsplit": round(tok_s / tok_s_1, 3) if world == 1 and tok_s_1 else None,
+                "layout": r["layout"] if world > 1 else None,
+                "layouts_tok_s": {k: round(v, 2) for k, v in r["layouts_tok_s"].items()} if world > 1 else None,
                 "parity_check": r["parity_check"], "tokens_head": toks,
                 "distinct_tokens_head": len(set(toks)), "synthetic_output_gain": out_gain or None,
                 "launch_plan": r["launch_plan"], "launch_plan_unsplit": r["launch_plan_unsplit"],

@@ -214,18 +214,22 @@ def test_unsupported_type_reports_error():
 
 
 @gpu
+@pytest.mark.parametrize("rep_attn", [0, 1], ids=["split", "rep_attn"])
 @pytest.mark.parametrize("n_ranks", [2, 4, 8])
-def test_row_split_virtual_ranks_bitexact(n_ranks):
+def test_row_split_virtual_ranks_bitexact(n_ranks, rep_attn):
     """the row-split engine (per-rank row shards of every matrix, shards assembled into
     full vectors, one argmax key per rank merged with global indices) reproduces the 1-GPU tokens
     and logits bit for bit.  Virtual ranks: all shards in one engine on the box's single GPU (RCCL
-    refuses two ranks per device); the multi-GPU run differs only in the all-gather transport."""
+    refuses two ranks per device); the multi-GPU run differs only in the all-gather transport.
+    rep_attn: the attention block (Wq|Wk|Wv, Wo) whole on every rank, only the FFN and the output
+    head split (2 gathers per layer instead of 4)."""
     import gemma_hip as G
     shape = dict(O.TINY)
     prompt = O.make_prompt(6, shape["n_vocab"])
     m = O.Model(O.make_config(shape, n_ctx=128))
     seq_ref, lg_ref = m.generate(prompt, 6)
-    e = G.Engine(shape, n_ctx=128, device=0, tp=(n_ranks, 0, None))
+    e = G.Engine(shape, n_ctx=128, device=0, tp=(n_ranks, 0, None), tp_flags=G.TP_REP_ATTN * rep_attn)
+    assert e.tp_flags() == G.TP_REP_ATTN * rep_attn
     e.begin(prompt)
     lg = e.step(len(prompt) + 6, want_logits=True, use_graph=True)
     toks = list(e.tokens()[: len(seq_ref)])
@@ -235,13 +239,14 @@ def test_row_split_virtual_ranks_bitexact(n_ranks):
 
 
 @gpu
-def test_row_split_virtual_ranks_gemma2b_shapes():
+@pytest.mark.parametrize("rep_attn", [0, 1], ids=["split", "rep_attn"])
+def test_row_split_virtual_ranks_gemma2b_shapes(rep_attn):
     import gemma_hip as G
     shape = dict(O.GEMMA_2B)
     prompt = O.make_prompt(5, shape["n_vocab"])
     m = O.Model(O.make_config(shape, n_ctx=64))
     seq_ref, lg_ref = m.generate(prompt, 2)
-    e = G.Engine(shape, n_ctx=64, device=0, tp=(8, 0, None))
+    e = G.Engine(shape, n_ctx=64, device=0, tp=(8, 0, None), tp_flags=G.TP_REP_ATTN * rep_attn)
     e.begin(prompt)
     lg = e.step(len(prompt) + 2, want_logits=True, use_graph=True)
     toks = list(e.tokens()[: len(seq_ref)])
@@ -251,16 +256,17 @@ def test_row_split_virtual_ranks_gemma2b_shapes():
 
 
 @gpu
-def test_row_split_virtual_ranks_gemma7b_layers():
+@pytest.mark.parametrize("rep_attn", [0, 1], ids=["split", "rep_attn"])
+def test_row_split_virtual_ranks_gemma7b_layers(rep_attn):
     """BASELINE config 4's partition: Gemma-7B layer shapes row-split over 8 ranks (384-row down
-    shards with K = 24576, MHA heads split 2 per rank)."""
+    shards with K = 24576, MHA heads split 2 per rank; or the attention block whole per rank)."""
     import gemma_hip as G
     O.lib().orc_set_threads(16)
     shape = dict(GEMMA_7B_LAYERS)
     prompt = O.make_prompt(5, shape["n_vocab"])
     m = O.Model(O.make_config(shape, n_ctx=64))
     seq_ref, lg_ref = m.generate(prompt, 3)
-    e = G.Engine(shape, n_ctx=64, device=0, tp=(8, 0, None))
+    e = G.Engine(shape, n_ctx=64, device=0, tp=(8, 0, None), tp_flags=G.TP_REP_ATTN * rep_attn)
     e.begin(prompt)
     lg = e.step(len(prompt) + 3, want_logits=True, use_graph=True)
     toks = list(e.tokens()[: len(seq_ref)])

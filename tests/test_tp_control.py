@@ -7,7 +7,9 @@ per decode step, as the real engine runs its RCCL all-gathers, so ranks whose st
 Checked: the RCCL id is made once by rank 0 per communicator and every rank receives the same bytes;
 every rank runs rank 0's tuned plan; the unsplit-engine hash check passes on equal logits; a forced
 one-row mismatch on rank 1 makes BOTH ranks exit 3 with rank 0 printing the error object; rank 0's
-JSON line carries the max-over-ranks time."""
+JSON line carries the max-over-ranks time; both row-split layouts (every matrix split / the attention
+block replicated) are checked and timed in the same order on every rank, and the faster is the line's
+rate."""
 import contextlib
 import io
 import json
@@ -35,14 +37,14 @@ def _free_port():
 class StubEngine:
     log = []
 
-    def __init__(self, tp, comm, corrupt):
-        self.tp, self.comm, self.corrupt = tp, comm, corrupt
+    def __init__(self, tp, comm, corrupt, flags=0):
+        self.tp, self.comm, self.corrupt, self.flags = tp, comm, corrupt, flags
         self.split = tp is not None and (tp[0] > 1 or tp[2] is not None)
         self.rccl = tp is not None and tp[2] is not None
         self._plan = {k: (1, 1, 0) for k in ("qkv", "attn_out", "gate_up", "down", "logits")}
         self._plan["attention"] = 0
         self.toks = []
-        StubEngine.log.append(("create", None if tp is None else (tp[0], tp[1], bytes(tp[2]) if tp[2] else None)))
+        StubEngine.log.append(("create", None if tp is None else (tp[0], tp[1], bytes(tp[2]) if tp[2] else None), flags))
 
     def _collective(self):  # the real engine's RCCL all-gathers: every rank must take part
         if self.rccl and self.comm.world > 1:
@@ -59,7 +61,7 @@ class StubEngine:
     def step(self, n, want_logits=False, use_graph=True):
         out = np.zeros((n, V), dtype=np.float32) if want_logits else None
         if n == 5 and self.tp and self.tp[1] == 1:  # rank 1 is the slow one in the timed region
-            time.sleep(0.3)
+            time.sleep(0.3 if self.flags == 0 else 0.15)  # (the replicated-attention layout "faster")
         for i in range(n):
             self._collective()
             lg = self._row(self.pos)
@@ -117,7 +119,8 @@ def _work(rank, world, port, corrupt, q):
 
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
-        rc = tp_leg.main(["5", "q4_0", "1", "2b", "3", "8"], make_engine=lambda tp: StubEngine(tp, comm, corrupt and rank == 1),
+        rc = tp_leg.main(["5", "q4_0", "1", "2b", "3", "8"],
+                         make_engine=lambda tp, flags=0: StubEngine(tp, comm, corrupt and rank == 1, flags),
                          make_id=make_id, comm=comm)
     q.put((rank, rc, buf.getvalue(), made, StubEngine.log))
 
@@ -154,15 +157,21 @@ def test_tp_leg_control_flow_world2():
     assert line["parity_check"]["mismatched_rows_all_ranks"] == 0
     assert line["launch_plan"]["gate_up"] == [1, 1, 0] or tuple(line["launch_plan"]["gate_up"]) == (1, 1, 0)
     assert "roofline" in line and line["roofline"]["kernel"]
-    assert line["timed_s"] >= 0.3  # the max over ranks (rank 1 slept in the timed region)
+    # the max over ranks (rank 1 slept in the timed region), of the faster layout
+    assert 0.15 <= line["timed_s"] < 0.3
+    assert line["layout"] == "rep_attn" and set(line["layouts_tok_s"]) == {"split", "rep_attn"}
+    assert line["layouts_tok_s"]["rep_attn"] > line["layouts_tok_s"]["split"]
     assert res[1][1] == ""  # only rank 0 prints
-    # ids: made on rank 0 only (one per communicator: parity engine + timed engine), same bytes everywhere
-    assert res[0][2] == [0, 0] and res[1][2] == []
+    # ids: made on rank 0 only (one per communicator: a parity and a timed engine per layout), same
+    # bytes everywhere
+    assert res[0][2] == [0, 0, 0, 0] and res[1][2] == []
+    for r in (0, 1):  # split engines in the same layout order on every rank
+        assert [e[2] for e in res[r][3] if e[0] == "create" and e[1] and e[1][2]] == [0, 1, 0, 1]
     ids = [[e[1][2] for e in res[r][3] if e[0] == "create" and e[1] and e[1][2]] for r in (0, 1)]
-    assert ids[0] == ids[1] and len(ids[0]) == 2 and ids[0][0] == bytes([0xA5, 1]) * 64
-    # every rank installed rank 0's plan (rank 1 tuned a different one)
+    assert ids[0] == ids[1] and len(ids[0]) == 4 and ids[0][0] == bytes([0xA5, 1]) * 64
+    # every rank installed rank 0's plan (rank 1 tuned a different one), once per timed layout
     for r in (0, 1):
-        assert [e[1] for e in res[r][3] if e[0] == "set_plan"] == [(1, 1, 0)]
+        assert [e[1] for e in res[r][3] if e[0] == "set_plan"] == [(1, 1, 0), (1, 1, 0)]
 
 
 def test_tp_leg_forced_mismatch_exits_3_on_every_rank():
