@@ -588,8 +588,11 @@ __device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t r
 #ifndef GHIP_KQ_WPE
 #define GHIP_KQ_WPE 0  // k_matvec_kq: minimum waves per SIMD the compiler must fit (0: its choice)
 #endif
-template <int WT, bool DUAL, int XJ, bool TL, int HO, int NSB = 0, int PF = KQ_PF>
-__global__ void __launch_bounds__(KQ_THREADS)
+// NT: threads per workgroup.  Every workgroup builds the column's whole Q8_K image (norm + quantize)
+// in its prologue, so two 4-wave workgroups per CU build it twice: the gate/up launch (2,048 row
+// groups) runs one 8-wave workgroup per CU instead (NT = 512, XJ = 1: one super-block per wave)
+template <int WT, bool DUAL, int XJ, bool TL, int HO, int NSB = 0, int PF = KQ_PF, int NT = KQ_THREADS>
+__global__ void __launch_bounds__(NT)
 #if GHIP_KQ_WPE
 __attribute__((amdgpu_waves_per_eu(GHIP_KQ_WPE)))
 #endif
@@ -598,7 +601,7 @@ k_matvec_kq(kq_args a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
     const int col = blockIdx.y;
     const int64_t n_groups = (a.rows + 7) / 8;
-    const int64_t g0 = (int64_t)blockIdx.x * (KQ_THREADS / 64) + wave;
+    const int64_t g0 = (int64_t)blockIdx.x * (NT / 64) + wave;
 #define KQ_STAMP(i)                                                                                              \
     do {                                                                                                         \
         if (GHIP_STAMPS && a.dbg_t && tid == 0)                                                                  \
@@ -610,7 +613,7 @@ k_matvec_kq(kq_args a) {
     // DUAL (ffn gate and up in one launch): the up matrix w2 (same type and shape) streams beside the
     // gate rows, each in its own ordered chain; the epilogue forms gelu(gate) * up in registers
     kq_pro_regs<XJ> pr;
-    kq_pro_load<XJ>(a, col, wave, KQ_THREADS / 64, lane, pr);
+    kq_pro_load<XJ>(a, col, wave, NT / 64, lane, pr);
     // NSB > 0 (compile-time super-blocks per row, one row group per wave): the rounds of PF
     // super-blocks are software-pipelined — round k + 1's loads go out before round k's arithmetic,
     // into the other half of rb — instead of each round's load waiting behind the previous round's
@@ -640,7 +643,7 @@ k_matvec_kq(kq_args a) {
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         KQ_STAMP(6);
     }
-    kq_pro_build<XJ>(a, xs, kq_red(xs, a.nsb), col, tid, KQ_THREADS, pr);
+    kq_pro_build<XJ>(a, xs, kq_red(xs, a.nsb), col, tid, NT, pr);
     KQ_STAMP(1);
     __syncthreads();
     KQ_STAMP(2);
@@ -684,7 +687,7 @@ k_matvec_kq(kq_args a) {
         KQ_STAMP(5);
         return;
     }
-    for (int64_t g = g0; g < n_groups; g += (int64_t)gridDim.x * (KQ_THREADS / 64)) {
+    for (int64_t g = g0; g < n_groups; g += (int64_t)gridDim.x * (NT / 64)) {
         const int64_t row_raw = g * 8 + rr;
         const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;  // all lanes stay active for the folds
         const uint8_t *wrow = a.w + row * a.row_bytes;
@@ -1338,7 +1341,12 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     // group has its own wave (the gate/up in that form measured 1,044-1,045 vs 1,044-1,054 tok/s
     // without it: dropped)
     const bool pipe8 = GHIP_KQ_EARLY && a.nsb == 8 && !wide && (int64_t)grid_x * (KQ_THREADS / 64) >= groups;
-    if (a.w2) {
+    if (a.w2 && !wide && a.nsb <= 8 && a.tiled && wtype == T_Q4_K && ho == 1) {
+        // one 8-wave workgroup per CU, so each CU builds the Q8_K image once (the 4-wave form builds
+        // it in both of a CU's workgroups: stamps put the build at 2.9 us of a 14 us launch)
+        const dim3 g8((unsigned)std::min<int64_t>((groups + 7) / 8, 4096), a.ncols);
+        hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, true, 1, true, 1, 0, KQ_PF, 512>), g8, dim3(512), lds, s, a);
+    } else if (a.w2) {
         if (wide) GHIP_KQ_LAUNCH(true, 8);
         else GHIP_KQ_LAUNCH(true, 2);
     } else if (single_out && pipe8) {
