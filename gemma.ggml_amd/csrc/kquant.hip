@@ -585,6 +585,9 @@ __device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t r
     }
 }
 
+#ifndef GHIP_KQ_HEAD_WGS
+#define GHIP_KQ_HEAD_WGS 1024  // the single-column output head's grid cap (0: every row group its own wave); Q6_K head cold, same box: uncapped / 512 / 768 / 1024 / 1280 / 2048 / 4096 WGs -> 102.0 / 92.4 / 104.0 / 92.2 / 99.2 / 95.0 / 99.3 us
+#endif
 #ifndef GHIP_KQ_WPE
 #define GHIP_KQ_WPE 0  // k_matvec_kq: minimum waves per SIMD the compiler must fit (0: its choice)
 #endif
@@ -650,11 +653,20 @@ k_matvec_kq(kq_args a) {
     if constexpr (NSB > 0 && GHIP_KQ_EARLY) {
         static_assert(NSB % PF == 0, "whole rounds");
         constexpr int NR = NSB / PF;
-        if (g0 < n_groups) {  // wave-uniform; the launch gives every row group its own wave
-            const int64_t row_raw = g0 * 8 + rr;
+        static_assert(NR % 2 == 0, "a group's rounds end on the buffer they started on");
+        // a wave takes row groups g0, g0 + stride, ... (one, when the grid gives every group its own
+        // wave); the pipeline runs ACROSS groups: a group's last round prefetches the next group's
+        // first, so a capped grid keeps its loads in flight without a per-workgroup prologue each
+        const int64_t stride = (int64_t)gridDim.x * (NT / 64);
+        for (int64_t g = g0; g < n_groups; g += stride) {  // wave-uniform
+            const int64_t row_raw = g * 8 + rr;
             const int64_t row = row_raw < a.rows ? row_raw : a.rows - 1;
             const uint8_t *wrow = a.w + row * a.row_bytes;
             const uint8_t *wrow2 = DUAL ? a.w2 + row * a.row_bytes : nullptr;
+            const bool more = g + stride < n_groups;
+            const int64_t row_n = more ? (g + stride) * 8 + rr < a.rows ? (g + stride) * 8 + rr : a.rows - 1 : row;
+            const uint8_t *wrow_n = a.w + row_n * a.row_bytes;
+            const uint8_t *wrow2_n = DUAL ? a.w2 + row_n * a.row_bytes : nullptr;
             float acc = 0.0f, accm = 0.0f, acc2 = 0.0f, accm2 = 0.0f;
 #pragma unroll
             for (int rd = 0; rd < NR; ++rd) {
@@ -663,6 +675,12 @@ k_matvec_kq(kq_args a) {
                     for (int p = 0; p < PF; ++p) {
                         rb[(rd + 1) & 1][p] = kq_load<WT, TL>(wrow, (rd + 1) * PF + p, l);
                         if (DUAL) rb2[(rd + 1) & 1][p] = kq_load<WT, TL>(wrow2, (rd + 1) * PF + p, l);
+                    }
+                } else if (more) {  // the next group's first round
+#pragma unroll
+                    for (int p = 0; p < PF; ++p) {
+                        rb[0][p] = kq_load<WT, TL>(wrow_n, p, l);
+                        if (DUAL) rb2[0][p] = kq_load<WT, TL>(wrow2_n, p, l);
                     }
                 }
 #pragma unroll
@@ -682,7 +700,7 @@ k_matvec_kq(kq_args a) {
             if (DUAL) kq_store_gu<WT>(a, col, row_raw, l, acc, accm, acc2, accm2);
             else kq_store<WT>(a, col, row_raw, l, acc, accm);
             KQ_STAMP(4);
-            kq_handoff<HO>(a, col, g0, lane, xs);
+            kq_handoff<HO>(a, col, g, lane, xs);
         }
         KQ_STAMP(5);
         return;
@@ -1312,7 +1330,7 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     // tok/s; the uncapped grid alone: 1,091-1,094; the gate/up rounds pipelined too: neutral, removed)
     const bool single_out = !a.w2 && a.pro == KQP_COPY && a.q8_mode == KQO_NONE && a.ncols == 1;
     const bool uncap = single_out;
-    const unsigned grid_x = (unsigned)std::min<int64_t>((groups + 3) / 4, uncap ? (int64_t)1 << 30 : 4096);
+    const unsigned grid_x = (unsigned)std::min<int64_t>((groups + 3) / 4, uncap ? (GHIP_KQ_HEAD_WGS ? GHIP_KQ_HEAD_WGS : (int64_t)1 << 30) : 4096);
     const size_t lds = std::max(img, red);
     if (lds > 64 * 1024) {
         set_error("matvec_kq: row too long for the LDS image");
@@ -1340,7 +1358,7 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
     // the output head's rows of 8 super-blocks: the software-pipelined rounds (NSB = 8) when every row
     // group has its own wave (the gate/up in that form measured 1,044-1,045 vs 1,044-1,054 tok/s
     // without it: dropped)
-    const bool pipe8 = GHIP_KQ_EARLY && a.nsb == 8 && !wide && (int64_t)grid_x * (KQ_THREADS / 64) >= groups;
+    const bool pipe8 = GHIP_KQ_EARLY && a.nsb == 8 && !wide;  // (a capped grid: several groups per wave, one pipeline)
     if (a.w2 && !wide && a.nsb <= 8 && a.tiled && wtype == T_Q4_K && ho == 1) {
         // one 8-wave workgroup per CU, so each CU builds the Q8_K image once (the 4-wave form builds
         // it in both of a CU's workgroups: stamps put the build at 2.9 us of a 14 us launch)

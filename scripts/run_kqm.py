@@ -21,5 +21,8 @@ t0 = time.perf_counter()
 e.step(steps, use_graph=True)
 e.L.gemma_engine_sync(e.h)
 dt = time.perf_counter() - t0
-print(f"q4_k_m decode {steps / dt:.1f} tok/s ({dt / steps * 1e3:.3f} ms/token), prompt {n_prompt}", flush=True)
+import zlib  # noqa: E402
+toks = e.tokens()
+print(f"q4_k_m decode {steps / dt:.1f} tok/s ({dt / steps * 1e3:.3f} ms/token), prompt {n_prompt}, "
+      f"tokens crc {zlib.crc32(toks.tobytes()):08x}", flush=True)
 e.close()
