@@ -588,6 +588,11 @@ __device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t r
 #ifndef GHIP_KQ_HEAD_WGS
 #define GHIP_KQ_HEAD_WGS 1024  // the single-column output head's grid cap (0: every row group its own wave); Q6_K head cold, same box: uncapped / 512 / 768 / 1024 / 1280 / 2048 / 4096 WGs -> 102.0 / 92.4 / 104.0 / 92.2 / 99.2 / 95.0 / 99.3 us
 #endif
+#ifndef GHIP_KQ_XJ8
+#define GHIP_KQ_XJ8 1  // prologue super-blocks per wave of the 8-wave K-split launches when K <= 2048 (q|k+v,
+                        // attn-out): 1 = one per wave, no clamped surplus loads; Q4_K_M decode, same box:
+                        // 1,160-1,164 vs 1,132-1,141 tok/s with 2
+#endif
 #ifndef GHIP_KQ_WPE
 #define GHIP_KQ_WPE 0  // k_matvec_kq: minimum waves per SIMD the compiler must fit (0: its choice)
 #endif
@@ -1215,7 +1220,9 @@ int launch_matvec_kq2(int t1, const kq_args &a, int t2, const kq_args &b, hipStr
     const dim3 grid((unsigned)(g1 + g2), 1);
 #define GHIP_KQ2(A, B)                                                                                       \
     do {                                                                                                     \
-        if (a.tiled) hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, 2, 2, true>), grid, dim3(512), lds, s, a, b, g1);  \
+        if (a.tiled && a.nsb <= 8 && b.nsb <= 8)                                                             \
+            hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, GHIP_KQ_XJ8, 2, true>), grid, dim3(512), lds, s, a, b, g1); \
+        else if (a.tiled) hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, 2, 2, true>), grid, dim3(512), lds, s, a, b, g1); \
         else hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, 2, 2, false>), grid, dim3(512), lds, s, a, b, g1);          \
     } while (0)
     if (t1 == T_Q4_K && t2 == T_Q4_K) GHIP_KQ2(T_Q4_K, T_Q4_K);
@@ -1315,7 +1322,8 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
             else hipLaunchKernelGGL((k_matvec_kq_ks<T_Q6_K, 8, XJ, PF, false>), grid, dim3(512), lds_ks, s, a);            \
         }                                                                                                   \
     } while (0)
-        if (a.nsb <= 16) GHIP_KQ_KS(2, 2);
+        if (a.nsb <= 8) GHIP_KQ_KS(GHIP_KQ_XJ8, 2);
+        else if (a.nsb <= 16) GHIP_KQ_KS(2, 2);
         else GHIP_KQ_KS(8, 2);
 #undef GHIP_KQ_KS
         GHIP_CHECK(hipGetLastError());
@@ -1363,6 +1371,7 @@ int launch_matvec_kq(int wtype, const kq_args &a, hipStream_t s) {
         // one 8-wave workgroup per CU, so each CU builds the Q8_K image once (the 4-wave form builds
         // it in both of a CU's workgroups: stamps put the build at 2.9 us of a 14 us launch)
         const dim3 g8((unsigned)std::min<int64_t>((groups + 7) / 8, 4096), a.ncols);
+        // (its rounds software-pipelined, NSB = 8: 816 vs 1,132-1,141 tok/s — not kept)
         hipLaunchKernelGGL((k_matvec_kq<T_Q4_K, true, 1, true, 1, 0, KQ_PF, 512>), g8, dim3(512), lds, s, a);
     } else if (a.w2) {
         if (wide) GHIP_KQ_LAUNCH(true, 8);
