@@ -216,6 +216,13 @@ struct gemma_engine {
     // a layer needs 2 all-gathers (h, x) instead of 4; the FFN and the output head stay row-split
     bool rep_attn = false;
     int64_t sh_o = 0;
+    // GEMMA_TP_P2P: the all-gathers by peer-to-peer pushes (p2p.hip) instead of RCCL: an uncached
+    // arena of inboxes + flags per rank, shared by IPC handles (gemma_engine_p2p_handle / _open)
+    bool p2p = false, p2p_ready = false;
+    uint8_t *p2p_arena = nullptr;
+    uint8_t *p2p_peer[P2P_MAX_RANKS] = {};
+    unsigned *p2p_seq = nullptr, *p2p_err = nullptr;
+    int64_t ib_qkv = 0, ib_sa = 0, ib_h = 0, ib_x = 0, ib_hact = 0, ib_hda = 0, ib_logits = 0, ib_keys = 0, ib_flags = 0;
     unsigned long long *rank_keys = nullptr;           // [tp_n] one argmax key per rank
     attn_geom ag;                           // split-attention geometry and its scratch
     float *att_sbuf = nullptr;
@@ -321,8 +328,38 @@ static int pick_ks(int wtype, int64_t n_bt, int target) {
     return ks;
 }
 
+// the inbox of a gathered working vector in every rank's p2p arena
+static int64_t p2p_inbox(const gemma_engine *e, const void *work) {
+    if (work == e->qkv) return e->ib_qkv;
+    if (work == e->sa) return e->ib_sa;
+    if (work == e->h) return e->ib_h;
+    if (work == e->x) return e->ib_x;
+    if (work == e->h_act) return e->ib_hact;
+    if (work == e->h_da) return e->ib_hda;
+    if (work == e->logits) return e->ib_logits;
+    if (work == e->rank_keys) return e->ib_keys;
+    return -1;
+}
+
+// one peer-to-peer gather of up to two segments (working vector, bytes per rank)
+static int p2p_gather(gemma_engine *e, void *w0, int64_t b0, void *w1 = nullptr, int64_t b1 = 0, hipStream_t s = nullptr) {
+    p2p_args a;
+    a.nseg = w1 ? 2 : 1;
+    a.seg[0].work = (uint8_t *)w0; a.seg[0].inbox = p2p_inbox(e, w0); a.seg[0].shard = b0;
+    if (w1) { a.seg[1].work = (uint8_t *)w1; a.seg[1].inbox = p2p_inbox(e, w1); a.seg[1].shard = b1; }
+    if (a.seg[0].inbox < 0 || (w1 && a.seg[1].inbox < 0)) {
+        set_error("p2p_gather: not a gathered vector");
+        return -1;
+    }
+    a.rank = e->tp_rank; a.n = e->tp_n;
+    for (int r = 0; r < e->tp_n; ++r) a.peer[r] = e->p2p_peer[r];
+    a.flags = e->ib_flags; a.seq = e->p2p_seq; a.err = e->p2p_err;
+    return launch_p2p_gather(a, s ? s : e->stream);
+}
+
 // in-place all-gather of a full vector whose rank-r shard [r*cnt, (r+1)*cnt) was just written
 static int tp_gather(gemma_engine *e, float *full, int64_t cnt) {
+    if (e->p2p) return p2p_gather(e, full, cnt * 4);
     if (!e->comm) return 0;  // one unsplit engine, or virtual ranks (shards already in place)
     const ncclResult_t r = ncclAllGather(full + (size_t)e->tp_rank * cnt, full, (size_t)cnt, ncclFloat, e->comm, e->stream);
     if (r != ncclSuccess) {
@@ -334,6 +371,7 @@ static int tp_gather(gemma_engine *e, float *full, int64_t cnt) {
 
 // in-place all-gather of the h image: per rank `act_bytes` of act (u32 groups) and `nda` scales
 static int tp_gather_bytes(gemma_engine *e, uint32_t *act, int64_t act_bytes, float *da, int64_t nda) {
+    if (e->p2p) return p2p_gather(e, act, act_bytes, da, nda * 4);
     if (!e->comm) return 0;
     ncclGroupStart();
     ncclResult_t r = ncclAllGather((uint8_t *)act + (size_t)e->tp_rank * act_bytes, act, (size_t)act_bytes, ncclUint8,
@@ -687,6 +725,7 @@ logits:
         if (launch_advance(e->key, lg_grid, e->token, e->pos, e->hist, c.n_ctx, e->nfix, rr, s)) return -1;
         return 0;
     }
+    if (e->p2p && p2p_gather(e, e->rank_keys, 8, nullptr, 0, s)) return -1;
     if (e->comm) {
         const ncclResult_t nr = ncclAllGather(e->rank_keys + e->tp_rank, e->rank_keys, 1, ncclUint64, e->comm, s);
         if (nr != ncclSuccess) {
@@ -918,9 +957,11 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     e->tp_n = tp_n;
     e->tp_rank = tp_rank;
     e->rep_attn = tp_n > 1 && (tp_flags & GEMMA_TP_REP_ATTN);
+    e->p2p = tp_n > 1 && !nccl_id && (tp_flags & GEMMA_TP_P2P);
     // every split matrix is cut into tp_n contiguous row ranges of whole 8-row tiles
     if (tp_n < 1 || tp_rank < 0 || tp_rank >= tp_n || (!e->rep_attn && e->qkv_rows % (8 * tp_n)) ||
-        c.n_embd % (8 * tp_n) || c.n_ff % (8 * tp_n) || c.n_vocab % (8 * tp_n) || (tp_flags & ~GEMMA_TP_REP_ATTN)) {
+        c.n_embd % (8 * tp_n) || c.n_ff % (8 * tp_n) || c.n_vocab % (8 * tp_n) ||
+        (tp_flags & ~(GEMMA_TP_REP_ATTN | GEMMA_TP_P2P)) || (e->p2p && tp_n > P2P_MAX_RANKS)) {
         set_error("gemma_engine_create: row split needs every matrix's rows to divide into 8-row tiles per rank");
         delete e;
         return nullptr;
@@ -961,7 +1002,7 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
         launch_synth_norm(e->out_norm, c.n_embd, tensor_key(seed, TID_OUT_NORM), synth_scale(0.05), s);
     }
     if (e->out_type == T_Q6_K && kq_retile_inplace(e->embd_q6k, T_Q6_K, c.n_vocab, c.n_embd, s, &e->embd_tiled)) up_fail = true;
-    e->n_virtual = (tp_n > 1 && !nccl_id) ? tp_n : 1;
+    e->n_virtual = (tp_n > 1 && !nccl_id && !e->p2p) ? tp_n : 1;
     e->layers.resize((size_t)c.n_layer * e->n_virtual);
     const double se = 1.0 / sqrt((double)c.n_embd), sq = 1.0 / sqrt((double)e->qw), sf = 1.0 / sqrt((double)c.n_ff);
     for (int il = 0; il < c.n_layer; ++il)
@@ -1174,6 +1215,26 @@ static gemma_engine *engine_create(const gemma_hip_config *cfg, int device, int 
     GHIP_FATAL(hipMemsetAsync(e->key, 0, (size_t)e->grid_big * 8, s));
     GHIP_FATAL(hipMemsetAsync(e->hist, 0, (size_t)(c.n_ctx + 1) * 4, s));
     GHIP_FATAL(hipMalloc(&e->rank_keys, (size_t)tp_n * 8));
+    if (e->p2p) {  // inboxes mirroring every gathered vector, then one flag word per source rank
+        size_t off = 0;
+        auto take = [&](int64_t &ib, size_t bytes) { ib = (int64_t)off; off += (bytes + 255) & ~(size_t)255; };
+        take(e->ib_qkv, (size_t)e->qkv_rows * 4);
+        take(e->ib_sa, (size_t)c.n_embd * 4);
+        take(e->ib_h, (size_t)c.n_ff * 4);
+        take(e->ib_x, (size_t)c.n_embd * 4);
+        take(e->ib_hact, e->h_act ? (size_t)c.n_ff : 0);
+        take(e->ib_hda, e->h_act ? (size_t)c.n_ff / 32 * 4 : 0);
+        take(e->ib_logits, (size_t)c.n_vocab * 4);
+        take(e->ib_keys, (size_t)tp_n * 8);
+        take(e->ib_flags, (size_t)P2P_MAX_RANKS * 4);
+        GHIP_FATAL(hipExtMallocWithFlags((void **)&e->p2p_arena, off, hipDeviceMallocUncached));
+        GHIP_FATAL(hipMemset(e->p2p_arena, 0, off));
+        GHIP_FATAL(hipMalloc(&e->p2p_seq, 64));
+        GHIP_FATAL(hipMemset(e->p2p_seq, 0, 64));
+        GHIP_FATAL(hipMalloc(&e->p2p_err, 64));
+        GHIP_FATAL(hipMemset(e->p2p_err, 0, 64));
+        e->p2p_peer[tp_rank] = e->p2p_arena;
+    }
     GHIP_FATAL(hipStreamSynchronize(s));
     // a communicator whenever an id is given, also for ONE rank: every gather, the key gather and
     // RCCL inside the captured hipGraph then run exactly as on N GPUs (a 1-rank all-gather in place)
@@ -1360,10 +1421,64 @@ extern "C" gemma_engine *gemma_engine_create_tp(const gemma_hip_config *cfg, int
 // the same with layout flags (GEMMA_TP_REP_ATTN: the attention block whole on every rank)
 extern "C" gemma_engine *gemma_engine_create_tp2(const gemma_hip_config *cfg, int device, int n_ranks, int rank,
                                                  const void *nccl_id, int flags) {
-    return engine_create(cfg, device, n_ranks, nccl_id ? rank : 0, nccl_id, nullptr, nullptr, nullptr, flags);
+    return engine_create(cfg, device, n_ranks, (nccl_id || (flags & GEMMA_TP_P2P)) ? rank : 0, nccl_id, nullptr, nullptr,
+                         nullptr, flags);
 }
 
-extern "C" int gemma_engine_tp_flags(const gemma_engine *e) { return e ? (e->rep_attn ? GEMMA_TP_REP_ATTN : 0) : -1; }
+// GEMMA_TP_P2P: this rank's arena as an IPC handle (hipIpcMemHandle_t bytes) for the other ranks
+extern "C" int gemma_engine_p2p_handle(const gemma_engine *e, void *out, int cap) {
+    set_error("");
+    if (!e || !e->p2p || !out || cap < (int)sizeof(hipIpcMemHandle_t)) {
+        set_error("gemma_engine_p2p_handle: not a p2p engine, or buffer too small");
+        return -1;
+    }
+    (void)hipSetDevice(e->device);
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, e->p2p_arena) != hipSuccess) {
+        set_error("gemma_engine_p2p_handle: hipIpcGetMemHandle failed");
+        return -1;
+    }
+    memcpy(out, &h, sizeof(h));
+    return (int)sizeof(h);
+}
+
+// every rank's handle in rank order (n = ranks, each hipIpcMemHandle_t bytes); this rank's own entry
+// is ignored.  Every rank must have opened its peers before any rank's first step (a host barrier).
+extern "C" int gemma_engine_p2p_open(gemma_engine *e, const void *handles, int n) {
+    set_error("");
+    if (!e || !e->p2p || !handles || n != e->tp_n || e->p2p_ready) {
+        set_error("gemma_engine_p2p_open: not a p2p engine, wrong rank count, or already open");
+        return -1;
+    }
+    (void)hipSetDevice(e->device);
+    for (int r = 0; r < n; ++r) {
+        if (r == e->tp_rank) continue;
+        hipIpcMemHandle_t h;
+        memcpy(&h, (const uint8_t *)handles + (size_t)r * sizeof(h), sizeof(h));
+        void *p = nullptr;
+        if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !p) {
+            set_error("gemma_engine_p2p_open: hipIpcOpenMemHandle failed for rank " + std::to_string(r));
+            return -1;
+        }
+        e->p2p_peer[r] = (uint8_t *)p;
+    }
+    e->p2p_ready = true;
+    return 0;
+}
+
+// the sticky timeout word of the p2p gathers (reset: clear it)
+extern "C" int gemma_engine_p2p_err(gemma_engine *e, int reset) {
+    if (!e || !e->p2p) return -1;
+    (void)hipSetDevice(e->device);
+    unsigned v = 0;
+    if (hipStreamSynchronize(e->stream) != hipSuccess || hipMemcpy(&v, e->p2p_err, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (reset) (void)hipMemset(e->p2p_err, 0, 4);
+    return (int)v;
+}
+
+extern "C" int gemma_engine_tp_flags(const gemma_engine *e) {
+    return e ? (e->rep_attn ? GEMMA_TP_REP_ATTN : 0) | (e->p2p ? GEMMA_TP_P2P : 0) : -1;
+}
 
 static void drop_graph(gemma_engine *e);
 
@@ -1373,6 +1488,13 @@ extern "C" void gemma_engine_free(gemma_engine *e) {
     (void)hipStreamSynchronize(e->stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->rank_keys) (void)hipFree(e->rank_keys);
+    if (e->p2p) {
+        for (int r = 0; r < e->tp_n; ++r)
+            if (r != e->tp_rank && e->p2p_peer[r]) (void)hipIpcCloseMemHandle(e->p2p_peer[r]);
+        if (e->p2p_arena) (void)hipFree(e->p2p_arena);
+        if (e->p2p_seq) (void)hipFree(e->p2p_seq);
+        if (e->p2p_err) (void)hipFree(e->p2p_err);
+    }
     if (e->ext_stage) (void)hipHostFree(e->ext_stage);
     if (e->ext_err) (void)hipHostFree(e->ext_err);
     drop_graph(e);
@@ -1456,6 +1578,10 @@ static int ensure_graph(gemma_engine *e) {
 extern "C" int gemma_engine_step(gemma_engine *e, int n, float *logits, int use_graph) {
     set_error("");
     (void)hipSetDevice(e->device);
+    if (e->p2p && !e->p2p_ready) {
+        set_error("gemma_engine_step: p2p engine whose peers are not open (gemma_engine_p2p_open)");
+        return -1;
+    }
     const gemma_hip_config &c = e->cfg;
     if (e->host_pos + n >= c.n_ctx) {
         set_error("gemma_engine_step: context full");

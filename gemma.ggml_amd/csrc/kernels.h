@@ -326,6 +326,26 @@ struct attn_o_args {
 bool attn_o_supported(int wtype, const attn_args &t, const mv_args &o);
 int launch_attn_o(int wtype, const attn_o_args &f, hipStream_t s);
 
+// peer-to-peer all-gather (p2p.hip, GEMMA_TP_P2P): each rank pushes [rank*shard, +shard) of every
+// segment's working vector into every peer's inbox (arena offset `inbox`), flags it, and copies
+// the peers' shards out of its own inbox; peer[r] = rank r's arena in this process's address space
+constexpr int P2P_MAX_RANKS = 8;
+struct p2p_seg {
+    uint8_t *work = nullptr;  // the full working vector (this rank's shard written by the producer)
+    int64_t inbox = 0;        // its inbox's offset in every rank's arena (16-byte aligned)
+    int64_t shard = 0;        // bytes per rank (multiple of 4)
+};
+struct p2p_args {
+    p2p_seg seg[2];
+    int nseg = 1;
+    int rank = 0, n = 1;
+    uint8_t *peer[P2P_MAX_RANKS] = {};
+    int64_t flags = 0;        // arena offset of the u32 flag words, one per source rank
+    unsigned *seq = nullptr;  // [0] gathers done, [1] workgroups finished in the current one (local)
+    unsigned *err = nullptr;  // sticky: a flag wait timed out
+};
+int launch_p2p_gather(const p2p_args &a, hipStream_t s);
+
 // ---- the whole decode token's layers as ONE persistent launch (token.hip) ----------
 // per layer: device pointers of the tiled matrices, norms and KV caches (a table in device memory,
 // read through the scalar cache: immutable for the launch)

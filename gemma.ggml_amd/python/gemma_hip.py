@@ -30,7 +30,7 @@ EXPORTS = ["mul_mat", "hpc_init", "hpc_shutdown", "hpc_register_weight", "hpc_la
            "ggml_init", "ggml_free", "ggml_new_tensor_2d", "ggml_mul_mat", "ggml_graph_compute_with_ctx",
            "gemma_engine_tensor", "gemma_engine_time", "gemma_engine_sync", "gemma_engine_tune",
            "gemma_engine_plan", "gemma_engine_set_plan", "gemma_engine_set_fuse", "gemma_engine_set_att_o", "gemma_engine_set_option", "gemma_engine_set_persist", "gemma_engine_persist_err", "gemma_engine_graph_kernels", "gemma_hbm_read_gbs", "gemma_hbm_read_probe",
-           "gemma_tp_unique_id", "gemma_engine_create_tp", "gemma_engine_create_tp2", "gemma_engine_tp_flags", "gemma_engine_tp_info", "gemma_engine_set_persist_timeout",
+           "gemma_tp_unique_id", "gemma_engine_create_tp", "gemma_engine_create_tp2", "gemma_engine_tp_flags", "gemma_engine_p2p_handle", "gemma_engine_p2p_open", "gemma_engine_p2p_err", "gemma_engine_tp_info", "gemma_engine_set_persist_timeout",
            "gguf_init_from_file", "gguf_free", "gguf_get_n_kv", "gguf_get_key", "gguf_get_kv_type",
            "gguf_get_arr_type", "gguf_get_arr_n", "gguf_get_arr_data", "gguf_get_arr_str", "gguf_get_val_str",
            "gguf_get_val_data", "gguf_get_n_tensors", "gguf_get_tensor_name", "gguf_get_tensor_type",
@@ -44,6 +44,7 @@ def build():
 
 
 TP_REP_ATTN = 1  # include/gemma_hpc.h GEMMA_TP_REP_ATTN
+TP_P2P = 2       # include/gemma_hpc.h GEMMA_TP_P2P: peer-to-peer gathers instead of RCCL (tp id None)
 
 
 class GemmaConfig(C.Structure):
@@ -103,6 +104,12 @@ def lib():
     L.gemma_engine_create_tp2.argtypes = [C.POINTER(GemmaConfig), C.c_int, C.c_int, C.c_int, vp, C.c_int]
     L.gemma_engine_tp_flags.restype = C.c_int
     L.gemma_engine_tp_flags.argtypes = [vp]
+    L.gemma_engine_p2p_handle.restype = C.c_int
+    L.gemma_engine_p2p_handle.argtypes = [vp, vp, C.c_int]
+    L.gemma_engine_p2p_open.restype = C.c_int
+    L.gemma_engine_p2p_open.argtypes = [vp, vp, C.c_int]
+    L.gemma_engine_p2p_err.restype = C.c_int
+    L.gemma_engine_p2p_err.argtypes = [vp, C.c_int]
     L.gemma_engine_create.restype = vp
     L.gemma_engine_create.argtypes = [C.POINTER(GemmaConfig), C.c_int]
     L.gemma_engine_free.argtypes = [vp]
@@ -349,6 +356,24 @@ class Engine:
     def set_persist_timeout(self, ticks):
         """the persistent launch's per-wait bound in 100 MHz ticks (0 = default; tests force timeouts)"""
         return self.L.gemma_engine_set_persist_timeout(self.h, ticks)
+
+    def p2p_handle(self):
+        """this rank's inbox arena as IPC handle bytes (GEMMA_TP_P2P engines)"""
+        buf = C.create_string_buffer(128)
+        n = self.L.gemma_engine_p2p_handle(self.h, buf, 128)
+        if n <= 0:
+            raise RuntimeError("gemma_engine_p2p_handle: " + last_error())
+        return buf.raw[:n]
+
+    def p2p_open(self, handles):
+        """every rank's handle (rank order); then a host barrier before the first step"""
+        raw = b"".join(handles)
+        if self.L.gemma_engine_p2p_open(self.h, C.create_string_buffer(raw, len(raw)), len(handles)) != 0:
+            raise RuntimeError("gemma_engine_p2p_open: " + last_error())
+
+    def p2p_err(self, reset=False):
+        """the sticky flag-wait timeout word of the p2p gathers"""
+        return self.L.gemma_engine_p2p_err(self.h, 1 if reset else 0)
 
     def tp_flags(self):
         """layout flags of a row-split engine (TP_REP_ATTN)"""

@@ -30,12 +30,49 @@ import numpy as np
 
 PLAN_CLASSES = ("qkv", "attn_out", "gate_up", "down", "logits")
 EXIT_PARITY = 3
-LAYOUT_NAMES = {0: "split", 1: "rep_attn"}
+TP_REP_ATTN, TP_P2P = 1, 2  # include/gemma_hpc.h GEMMA_TP_REP_ATTN / GEMMA_TP_P2P
+LAYOUT_NAMES = {0: "split", TP_REP_ATTN: "rep_attn", TP_P2P: "p2p", TP_P2P | TP_REP_ATTN: "p2p_rep_attn"}
 
 
 def _mk(make_engine, tp, flags):
     """make_engine(tp) for the plain split (the stub engines' signature), (tp, flags) otherwise"""
     return make_engine(tp) if not flags else make_engine(tp, flags)
+
+
+def make_split(comm, make_engine, make_id, flags, tp=None):
+    """This rank's split engine of layout `flags`, made in lockstep on every rank.  RCCL layouts:
+    a fresh id per communicator.  P2P layouts (an experimental transport): the engine is made, its
+    inbox handle exchanged and the peers mapped only if that worked on EVERY rank; otherwise every
+    rank returns None (the candidate is skipped, never fatal)."""
+    if not flags & TP_P2P:
+        return _mk(make_engine, tp or (comm.world, comm.rank, new_rccl_id(comm, make_id)), flags)
+    e, ok = None, True
+    try:
+        e = _mk(make_engine, (comm.world, comm.rank, None), flags)
+    except Exception:
+        ok = False
+    if comm.sum_int(0 if ok else 1):
+        if e is not None:
+            e.close()
+        return None
+    try:
+        mine = e.p2p_handle()
+    except Exception:
+        mine, ok = b"", False
+    handles = [comm.bcast_bytes(mine if r == comm.rank else b"", 64, src=r) for r in range(comm.world)]
+    try:
+        if ok and all(handles):
+            e.p2p_open(handles)
+        else:
+            ok = False
+    except Exception:
+        ok = False
+    if comm.sum_int(0 if ok else 1):
+        comm.barrier()
+        e.close()
+        return None
+    comm.barrier()  # every rank has mapped its peers before any rank pushes
+    return e
 
 
 class ParityError(RuntimeError):
@@ -72,18 +109,18 @@ class Comm:
         if self.dist is not None:
             self.dist.barrier()
 
-    def bcast_bytes(self, raw, n):
-        """rank 0's `raw` (at most n bytes) on every rank"""
+    def bcast_bytes(self, raw, n, src=0):
+        """rank src's `raw` (at most n bytes) on every rank"""
         if self.dist is None:
             return bytes(raw)
         import torch
         t = torch.zeros(n + 4, dtype=torch.uint8)
-        if self.rank == 0:
+        if self.rank == src:
             if len(raw) > n:
                 raise ValueError(f"broadcast payload {len(raw)} > {n} bytes")
             t[:4] = torch.tensor(list(len(raw).to_bytes(4, "little")), dtype=torch.uint8)
             t[4:4 + len(raw)] = torch.tensor(list(raw), dtype=torch.uint8)
-        self.dist.broadcast(t, 0)
+        self.dist.broadcast(t, src)
         b = bytes(t.numpy())
         return b[4:4 + int.from_bytes(b[:4], "little")]
 
@@ -118,6 +155,15 @@ class Comm:
 def new_rccl_id(comm, make_id):
     """A fresh RCCL unique id for one communicator: rank 0 calls make_id(), all ranks get its bytes."""
     return comm.bcast_bytes(make_id() if comm.rank == 0 else b"", 256)
+
+
+def open_p2p(comm, engine):
+    """GEMMA_TP_P2P engines: every rank's inbox arena handle to every rank (rank order), each rank
+    maps its peers' arenas, then a barrier, so no rank pushes before every peer has mapped."""
+    mine = engine.p2p_handle()
+    handles = [comm.bcast_bytes(mine if r == comm.rank else b"", len(mine), src=r) for r in range(comm.world)]
+    engine.p2p_open(handles)
+    comm.barrier()
 
 
 def plan_to_ints(plan):
@@ -176,13 +222,35 @@ def reference_hashes(comm, make_engine, prompt, n_check):
 
 def check_parity(comm, make_engine, make_id, prompt, n_check, ref, layouts=(0,)):
     """Every rank's split engine(s) against the reference hashes; raises ParityError on any mismatch
-    (after every rank has counted, so all ranks raise together).  World 1: 8 virtual ranks and a
-    1-rank RCCL communicator; world N: the N RCCL ranks.  Each layout in `layouts` wherever the
-    engine has more than one rank (a 1-rank engine has a single layout)."""
+    of an RCCL layout (after every rank has counted, so all ranks raise together).  World 1: 8
+    virtual ranks and a 1-rank RCCL communicator; world N: the N RCCL ranks.  Each layout in
+    `layouts` wherever the engine has more than one rank (a 1-rank engine has a single layout).
+    A P2P layout that cannot be made, times out or mismatches is dropped (returned in `dropped`
+    with the reason), not fatal.  Returns (splits checked, layouts that passed, dropped)."""
     base = [(comm.world, comm.rank, "rccl")] if comm.world > 1 else [(8, 0, None), (1, 0, "rccl")]
     splits = [(sp, f) for f in layouts for sp in base if f == 0 or sp[0] > 1]
-    nbad = 0
+    nbad, passed, dropped = 0, [], {}
     for split, flags in splits:
+        if flags & TP_P2P:
+            ce = make_split(comm, make_engine, make_id, flags)
+            if ce is None:
+                dropped[LAYOUT_NAMES.get(flags, flags)] = "engine or peer mapping failed on some rank"
+                continue
+            bad = 0
+            try:
+                ce.begin(prompt)
+                bad = mismatched_rows(ref, row_hashes(ce.step(n_check, want_logits=True, use_graph=True)))
+                bad += n_check if ce.p2p_err() else 0
+            except Exception:
+                bad = n_check
+            comm.barrier()
+            ce.close()
+            total = comm.sum_int(bad)
+            if total:
+                dropped[LAYOUT_NAMES.get(flags, flags)] = f"{total} mismatched or timed-out rows over all ranks"
+            elif flags not in passed:
+                passed.append(flags)
+            continue
         if split[2] == "rccl":
             split = (split[0], split[1], new_rccl_id(comm, make_id))
         ce = _mk(make_engine, split, flags)
@@ -191,10 +259,12 @@ def check_parity(comm, make_engine, make_id, prompt, n_check, ref, layouts=(0,))
             nbad += mismatched_rows(ref, row_hashes(ce.step(n_check, want_logits=True, use_graph=True)))
         finally:
             ce.close()
+        if flags not in passed:
+            passed.append(flags)
     total = comm.sum_int(nbad)
     if total:
         raise ParityError(f"row-split logits differ from the unsplit engine: {total} rows over all ranks")
-    return splits
+    return splits, passed, dropped
 
 
 def timed_steps(comm, engine, steps, device_sync):
@@ -218,7 +288,7 @@ def run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=True, tun
     check_prompt = prompt[:16] if check_prompt is None else check_prompt
     layouts = tuple(layouts) if comm.world > 1 else (0,)  # one rank: one layout
     ref, info = reference_hashes(comm, make_engine, check_prompt, n_check)
-    checked = check_parity(comm, make_engine, make_id, check_prompt, n_check, ref, layouts)
+    checked, layouts, dropped = check_parity(comm, make_engine, make_id, check_prompt, n_check, ref, layouts)
 
     tok_s_1, plan_1 = None, None
     if unsplit_rate and comm.rank == 0:  # the same treatment (tuned or not) as the split engine
@@ -237,7 +307,10 @@ def run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=True, tun
 
     runs = {}
     for flags in layouts:  # every rank runs the same layouts in the same order (lockstep)
-        te = _mk(make_engine, (comm.world, comm.rank, new_rccl_id(comm, make_id)), flags)
+        te = make_split(comm, make_engine, make_id, flags)
+        if te is None:
+            dropped[LAYOUT_NAMES.get(flags, flags)] = "engine or peer mapping failed on some rank (timed run)"
+            continue
         try:
             plan = share_plan(comm, te, tune, tune_iters)
             te.begin(prompt)
@@ -251,9 +324,16 @@ def run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=True, tun
                     kern[k] = (us, algo)
                 except Exception:  # reported as missing, never fatal
                     pass
+            bad = comm.sum_int(1 if (flags & TP_P2P and te.p2p_err()) else 0)
         finally:
+            comm.barrier()
             te.close()
+        if bad:
+            dropped[LAYOUT_NAMES.get(flags, flags)] = "a flag wait timed out in the timed run"
+            continue
         runs[flags] = (dt, plan, toks, kern)
+    if not runs:
+        raise ParityError(f"no row-split layout passed: {dropped}")
     best = min(runs, key=lambda f: runs[f][0])  # dt is the max over ranks: every rank picks the same
     dt, plan, toks, kern = runs[best]
     tok_s = steps / dt
@@ -261,9 +341,11 @@ def run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=True, tun
            "timed_s": dt, "tok_s_unsplit_1gpu": tok_s_1, "launch_plan": plan, "launch_plan_unsplit": plan_1,
            "tokens": toks, "kernels": kern, "layout": LAYOUT_NAMES.get(best, best),
            "layouts_tok_s": {LAYOUT_NAMES.get(f, f): steps / runs[f][0] for f in runs},
+           "layouts_dropped": dropped,
            "parity_check": {"rows": n_check, "mismatched_rows_all_ranks": 0,
                             "reference": "unsplit 1-GPU engine (rank 0), logits sha1 per row",
-                            "split_checked": f"{comm.world} RCCL ranks" if comm.world > 1
+                            "split_checked": (f"{comm.world} ranks, layouts "
+                                              f"{[LAYOUT_NAMES.get(f, f) for f in layouts]}") if comm.world > 1
                             else "8 virtual ranks + the 1-rank RCCL engine",
                             "min_top1_top2_rel_margin": info.get("margin"),
                             "tokens_unsplit": info.get("tokens"), "splits": len(checked)}}

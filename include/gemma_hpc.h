@@ -96,6 +96,15 @@ int gemma_engine_tp_info(const gemma_engine *e, int *out4);
  * attention block replicated, 2 all-gathers per layer instead of 4; the FFN and the output head
  * stay row-split; the same bits either way).  tp_flags returns the engine's flags. */
 #define GEMMA_TP_REP_ATTN 1
+/* GEMMA_TP_P2P (nccl_id NULL, n_ranks > 1, one process per GPU): the all-gathers by peer-to-peer
+ * pushes into each peer's uncached inbox arena (p2p.hip) instead of RCCL.  Each rank publishes its
+ * arena with gemma_engine_p2p_handle (an IPC handle, <= 64 B), every rank passes all handles in
+ * rank order to gemma_engine_p2p_open, then a host barrier, then steps.  p2p_err: a flag wait timed
+ * out (sticky; reset clears). */
+#define GEMMA_TP_P2P 2
+int gemma_engine_p2p_handle(const gemma_engine *e, void *out, int cap);
+int gemma_engine_p2p_open(gemma_engine *e, const void *handles, int n);
+int gemma_engine_p2p_err(gemma_engine *e, int reset);
 gemma_engine *gemma_engine_create_tp2(const gemma_hip_config *cfg, int device, int n_ranks, int rank,
                                       const void *nccl_id, int flags);
 int gemma_engine_tp_flags(const gemma_engine *e);

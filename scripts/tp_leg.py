@@ -4,7 +4,12 @@ process of every rank with a time limit, so a collective that never completes ca
 line.  Rank 0 prints one JSON line; a parity mismatch on any rank prints an error object and every
 rank exits 3.
 
-usage: tp_leg.py <steps> <wtype q4_0|q8_0> <tune 0|1> [model 2b|7b] [warmup] [prompt]
+usage: tp_leg.py <steps> <wtype q4_0|q8_0> <tune 0|1> [model 2b|7b] [warmup] [prompt] [layouts] [shared]
+
+  layouts  comma list of engine layout flags to check and time (default 2b: 0,1,2,3; 7b: 0,1):
+           0 split / 1 attention replicated, +2 = peer-to-peer gathers instead of RCCL
+  shared   every rank on device 0 (a one-GPU box: only the p2p layouts, RCCL refuses two ranks
+           per device) — the p2p transport's end-to-end check, not a scaling measurement
 
   2b  Gemma-2B (BASELINE config 2 row-split over N GPUs: the headline of `bench.py --gpus N`, N > 1),
       the bench's synthetic weights and prompt
@@ -41,6 +46,8 @@ def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None)
     model = argv[3] if len(argv) > 3 else "7b"
     warmup = int(argv[4]) if len(argv) > 4 else 4
     n_prompt = int(argv[5]) if len(argv) > 5 else 16
+    layouts = tuple(int(v) for v in argv[6].split(",")) if len(argv) > 6 else ((0, 1, 2, 3) if model == "2b" else (0, 1))
+    shared = len(argv) > 7 and argv[7] == "shared"
     import gemma_tp as T
     from bench import GEMMA_2B, GEMMA_7B, HBM_PEAK_GBS, make_prompt
     shape = GEMMA_2B if model == "2b" else GEMMA_7B
@@ -50,7 +57,7 @@ def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None)
         import torch
 
         import gemma_hip as G
-        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        local_rank = 0 if shared else int(os.environ.get("LOCAL_RANK", "0"))
         wtype = G.GGML_TYPE_Q4_0 if wtype_s == "q4_0" else G.GGML_TYPE_Q8_0
         n_ctx = ((n_prompt + warmup + steps + 64) // 32 + 1) * 32
 
@@ -63,7 +70,7 @@ def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None)
     try:
         r = T.run_stream(comm, make_engine, make_id, prompt, steps, warmup, tune=tune,
                          check_prompt=make_prompt(16, shape["n_vocab"]), device_sync=device_sync or (lambda: None),
-                         kernel_iters=30 if model == "2b" else 0, layouts=(0, 1))
+                         kernel_iters=30 if model == "2b" else 0, layouts=layouts)
     except T.ParityError as ex:
         if comm.rank == 0:
             print(json.dumps({"error": str(ex)}), flush=True)
@@ -75,8 +82,9 @@ def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None)
         line = {"model": f"Gemma-{model.upper()} {wtype_s.upper()}", "ranks": world, "tok_s": round(tok_s, 2),
                 "ms_per_token": round(r["ms_per_token"], 4), "steps": steps, "warmup": warmup, "prompt": n_prompt,
                 "timed_s": round(r["timed_s"], 6),
-                "parallelism": (f"row-split tp{world}, layout {r['layout']} (RCCL all-gathers per layer: "
-                                f"{2 if r['layout'] == 'rep_attn' else 4})") if world > 1
+                "parallelism": (f"row-split tp{world}, layout {r['layout']} ("
+                                f"{'peer-to-peer pushes' if 'p2p' in r['layout'] else 'RCCL all-gathers'} per layer: "
+                                f"{2 if 'rep_attn' in r['layout'] else 4})") if world > 1
                 else "1 GPU, 1-rank RCCL communicator (every gather through ncclAllGather in the hipGraph)",
                 "tok_s_unsplit_1gpu": round(tok_s_1, 2) if tok_s_1 else None,
                 # scaling fields only where ranks > 1; at N = 1 the ratio is the 1-rank RCCL
@@ -86,6 +94,7 @@ def main(argv=None, make_engine=None, make_id=None, comm=None, device_sync=None)
                 "rccl_overhead_vs_unsplit": round(tok_s / tok_s_1, 3) if world == 1 and tok_s_1 else None,
                 "layout": r["layout"] if world > 1 else None,
                 "layouts_tok_s": {k: round(v, 2) for k, v in r["layouts_tok_s"].items()} if world > 1 else None,
+                "layouts_dropped": r["layouts_dropped"] if world > 1 else None,
                 "parity_check": r["parity_check"], "tokens_head": toks,
                 "distinct_tokens_head": len(set(toks)), "synthetic_output_gain": out_gain or None,
                 "launch_plan": r["launch_plan"], "launch_plan_unsplit": r["launch_plan_unsplit"],

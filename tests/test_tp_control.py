@@ -40,14 +40,15 @@ class StubEngine:
     def __init__(self, tp, comm, corrupt, flags=0):
         self.tp, self.comm, self.corrupt, self.flags = tp, comm, corrupt, flags
         self.split = tp is not None and (tp[0] > 1 or tp[2] is not None)
+        assert not (flags & 2) or (tp is not None and tp[2] is None), "p2p engines take no RCCL id"
         self.rccl = tp is not None and tp[2] is not None
         self._plan = {k: (1, 1, 0) for k in ("qkv", "attn_out", "gate_up", "down", "logits")}
         self._plan["attention"] = 0
         self.toks = []
         StubEngine.log.append(("create", None if tp is None else (tp[0], tp[1], bytes(tp[2]) if tp[2] else None), flags))
 
-    def _collective(self):  # the real engine's RCCL all-gathers: every rank must take part
-        if self.rccl and self.comm.world > 1:
+    def _collective(self):  # the real engine's all-gathers (RCCL or p2p): every rank must take part
+        if (self.rccl or self.flags & 2) and self.comm.world > 1:
             self.comm.sum_int(1)
 
     def begin(self, prompt):
@@ -61,11 +62,11 @@ class StubEngine:
     def step(self, n, want_logits=False, use_graph=True):
         out = np.zeros((n, V), dtype=np.float32) if want_logits else None
         if n == 5 and self.tp and self.tp[1] == 1:  # rank 1 is the slow one in the timed region
-            time.sleep(0.3 if self.flags == 0 else 0.15)  # (the replicated-attention layout "faster")
+            time.sleep({0: 0.3, 1: 0.15, 2: 0.25, 3: 0.2}[self.flags])  # (the replicated-attention layout "fastest")
         for i in range(n):
             self._collective()
             lg = self._row(self.pos)
-            if self.corrupt and self.split and i == 3:
+            if self.corrupt and self.split and i == 3 and (self.corrupt != "p2p" or self.flags & 2):
                 lg[7] = np.nextafter(lg[7], np.float32(np.inf))  # one ulp on one logit of one row
             if want_logits:
                 out[i] = lg
@@ -90,6 +91,15 @@ class StubEngine:
 
     def sync(self):
         pass
+
+    def p2p_handle(self):  # the GEMMA_TP_P2P engine's inbox handle
+        return bytes([0x50, self.tp[1]]) * 32
+
+    def p2p_open(self, handles):
+        StubEngine.log.append(("p2p_open", tuple(h[1] for h in handles)))
+
+    def p2p_err(self):
+        return 0
 
     def tokens(self):
         return np.array(self.toks, dtype=np.int32)
@@ -120,7 +130,7 @@ def _work(rank, world, port, corrupt, q):
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
         rc = tp_leg.main(["5", "q4_0", "1", "2b", "3", "8"],
-                         make_engine=lambda tp, flags=0: StubEngine(tp, comm, corrupt and rank == 1, flags),
+                         make_engine=lambda tp, flags=0: StubEngine(tp, comm, corrupt if rank == 1 else False, flags),
                          make_id=make_id, comm=comm)
     q.put((rank, rc, buf.getvalue(), made, StubEngine.log))
 
@@ -159,19 +169,33 @@ def test_tp_leg_control_flow_world2():
     assert "roofline" in line and line["roofline"]["kernel"]
     # the max over ranks (rank 1 slept in the timed region), of the faster layout
     assert 0.15 <= line["timed_s"] < 0.3
-    assert line["layout"] == "rep_attn" and set(line["layouts_tok_s"]) == {"split", "rep_attn"}
+    assert line["layout"] == "rep_attn"
+    assert set(line["layouts_tok_s"]) == {"split", "rep_attn", "p2p", "p2p_rep_attn"} and not line["layouts_dropped"]
     assert line["layouts_tok_s"]["rep_attn"] > line["layouts_tok_s"]["split"]
     assert res[1][1] == ""  # only rank 0 prints
     # ids: made on rank 0 only (one per communicator: a parity and a timed engine per layout), same
     # bytes everywhere
     assert res[0][2] == [0, 0, 0, 0] and res[1][2] == []
-    for r in (0, 1):  # split engines in the same layout order on every rank
+    for r in (0, 1):  # split engines in the same layout order on every rank (RCCL ones with an id)
         assert [e[2] for e in res[r][3] if e[0] == "create" and e[1] and e[1][2]] == [0, 1, 0, 1]
+        assert [e[2] for e in res[r][3] if e[0] == "create" and e[1] and e[1][0] == 2] == [0, 1, 2, 3, 0, 1, 2, 3]
+        # p2p engines: every rank's handle, in rank order, once per p2p engine
+        assert [e[1] for e in res[r][3] if e[0] == "p2p_open"] == [(0, 1)] * 4
     ids = [[e[1][2] for e in res[r][3] if e[0] == "create" and e[1] and e[1][2]] for r in (0, 1)]
     assert ids[0] == ids[1] and len(ids[0]) == 4 and ids[0][0] == bytes([0xA5, 1]) * 64
     # every rank installed rank 0's plan (rank 1 tuned a different one), once per timed layout
     for r in (0, 1):
-        assert [e[1] for e in res[r][3] if e[0] == "set_plan"] == [(1, 1, 0), (1, 1, 0)]
+        assert [e[1] for e in res[r][3] if e[0] == "set_plan"] == [(1, 1, 0)] * 4
+
+
+def test_tp_leg_p2p_mismatch_drops_the_p2p_layouts_only():
+    """a mismatch confined to the (experimental) peer-to-peer transport drops its layouts; the RCCL
+    layouts still give the line, and no rank exits 3"""
+    res = _run(corrupt="p2p")
+    assert res[0][0] == 0 and res[1][0] == 0, res
+    line = json.loads(res[0][1].strip().splitlines()[-1])
+    assert set(line["layouts_tok_s"]) == {"split", "rep_attn"} and line["layout"] == "rep_attn"
+    assert set(line["layouts_dropped"]) == {"p2p", "p2p_rep_attn"}
 
 
 def test_tp_leg_forced_mismatch_exits_3_on_every_rank():
