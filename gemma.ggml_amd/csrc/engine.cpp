@@ -2160,7 +2160,8 @@ static int enqueue_prefill(gemma_engine *e, int T, bool exact, float *taps = nul
     auto quant = [&](int mode, const float *x, const float *x2, int64_t K, const float *norm_w) {
         qrow_args a;
         a.x = x; a.x2 = x2; a.ldx = K; a.K = K; a.norm_w = norm_w; a.eps = c.eps;
-        a.q = exact ? nullptr : p.XQ; a.qh = exact ? p.XH : nullptr; a.ldq = p.ldq; a.da = p.DA; a.ldd = p.ldd;
+        const bool i8img = exact && gemm_x4_i8();  // the int8-staged exact GEMM reads the int8 image
+        a.q = (!exact || i8img) ? p.XQ : nullptr; a.qh = (exact && !i8img) ? p.XH : nullptr; a.ldq = p.ldq; a.da = p.DA; a.ldd = p.ldd;
         a.gelu_tab = e->gelu_tab; a.gelu_clamp = c.gelu_clamp;
         if (mode == QR_EMBED_NORM) {
             a.tokens = e->hist; a.emb_qs = e->embd.qs; a.emb_sc = e->embd.sc; a.emb_type = wt;

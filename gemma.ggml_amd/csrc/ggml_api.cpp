@@ -423,15 +423,17 @@ int run_mul_mat(run_state &rs, ggml_tensor *node) {
     const int64_t ldq = (K + 255) / 256 * 256, ldd = ldq / 32;
     qrow_args q;
     q.x = (const float *)x; q.ldx = K; q.K = K;
-    q.q = nullptr;
-    q.qh = (uint16_t *)scratch_take(rs, (size_t)(cols * ldq * 2));
+    // the image the exact GEMM's form stages from: int8 (gemm_x4_i8) or f16
+    const bool i8img = gemm_x4_i8();
+    q.q = i8img ? (int8_t *)scratch_take(rs, (size_t)(cols * ldq)) : nullptr;
+    q.qh = i8img ? nullptr : (uint16_t *)scratch_take(rs, (size_t)(cols * ldq * 2));
     q.ldq = ldq;
     q.da = (float *)scratch_take(rs, (size_t)(cols * ldd * 4));
     q.ldd = ldd;
     if (launch_quant_rows(QR_F32, q, (int)cols, e.stream)) return -1;
     gemm_args g;
     g.qs = W->qs; g.sc = W->sc; g.rows = W->rows; g.n_rt = W->n_rt; g.n_bt = W->n_bt; g.nb = W->nb;
-    g.xh = q.qh; g.ldq = ldq; g.da = q.da; g.ldd = ldd; g.T = cols; g.y = y; g.ldy = a->ne[1];
+    g.xq = q.q; g.xh = q.qh; g.ldq = ldq; g.da = q.da; g.ldd = ldd; g.T = cols; g.y = y; g.ldy = a->ne[1];
     return launch_gemm_exact(a->type, EPI_STORE, g, e.stream);
 }
 

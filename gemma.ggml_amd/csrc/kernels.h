@@ -227,6 +227,7 @@ struct gemm_args {  // Y[t][r] (stride ldy) = W (tiled) x Xq[t] (+ resid), t < T
 int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s);
 // the same product in ggml's AVX2 lane order (bit-identical to mul_mat)
 int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s);
+bool gemm_x4_i8();        // mode 3: k_gemm_x4 stages the activation from the int8 image (xq)
 bool gemm_x4_on();        // the exact GEMM's form: the K = 4 multi-block MFMA kernel (k_gemm_x4) or W32
 void set_gemm_x4(int v);
 

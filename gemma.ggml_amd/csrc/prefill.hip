@@ -745,7 +745,10 @@ constexpr int X4_ACOL = 16 * 8;                          // bytes per (block, ro
 #endif
 // RGS: row groups (16 rows) per workgroup — 2: 32 rows x 64 tokens, 4: 64 rows x 32 tokens (the token
 // image, re-read by every row tile, is the bulk of the staging: 64 rows halve it)
-template <int WT, int EPI, int RGS>
+// XI: the activation staged from the int8 Q8_0 image (g.xq, 32 B per block and token: half the
+// global / L2 bytes of the f16 image) and converted to f16 while it is written to LDS (q ^ 0x80
+// over bias 1152: exact), instead of read as the f16 image g.xh
+template <int WT, int EPI, int RGS, int XI = 0>
 __global__ void __launch_bounds__(XNT)
 #if GHIP_X4_WPE
 __attribute__((amdgpu_waves_per_eu(GHIP_X4_WPE, GHIP_X4_WPE)))
@@ -753,7 +756,8 @@ __attribute__((amdgpu_waves_per_eu(GHIP_X4_WPE, GHIP_X4_WPE)))
 k_gemm_x4(gemm_args g) {
     static_assert(XNT == 256 && (RGS == 2 || RGS == 4), "4 waves: RGS row groups x 4/RGS token groups");
     constexpr int M4 = 16 * RGS, N4 = 32 * (4 / RGS), X4_ABLK = RGS * 8 * X4_ACOL;
-    constexpr int XREC4 = N4 * XKB * 64 / 16 / XNT, XDA4 = (N4 * XKB + XNT - 1) / XNT;
+    constexpr int XREC4 = N4 * XKB * (XI ? 32 : 64) / 16 / XNT, XDA4 = (N4 * XKB + XNT - 1) / XNT;
+    constexpr int XSEG = XKB * (XI ? 32 : 64) / 16;  // 16-B global records per token and stage
     __shared__ __attribute__((aligned(16))) uint8_t Wa[XKB * X4_ABLK];
     __shared__ __attribute__((aligned(16))) uint8_t Xs[N4 * XS_ROW];
     __shared__ __attribute__((aligned(16))) float dws[XKB][M4];
@@ -800,9 +804,10 @@ k_gemm_x4(gemm_args g) {
         }
 #pragma unroll
         for (int k = 0; k < XREC4; ++k) {
-            const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
+            const int rec = tid + XNT * k, tok = rec / XSEG, seg = rec % XSEG;
             const int64_t t = t0 + tok < g.T ? t0 + tok : 0;
-            xr[k] = *(const u4v *)(g.xh + t * g.ldq + kb0 * 32 + seg * 8);
+            if (XI) xr[k] = *(const u4v *)(g.xq + t * g.ldq + kb0 * 32 + seg * 16);
+            else xr[k] = *(const u4v *)(g.xh + t * g.ldq + kb0 * 32 + seg * 8);
         }
 #pragma unroll
         for (int k = 0; k < XDA4; ++k) {
@@ -846,9 +851,18 @@ k_gemm_x4(gemm_args g) {
         // different banks (pitch 528 B alone: 2-way)
 #pragma unroll
         for (int k = 0; k < XREC4; ++k) {
-            const int rec = tid + XNT * k, tok = rec >> 5, seg = rec & 31;
+            const int rec = tid + XNT * k, tok = rec / XSEG, seg = rec % XSEG;
             const u4v v = xr[k];
-            *(u4v *)(Xs + tok * XS_ROW + seg * 16) = (tok & 8) ? u4v{v.z, v.w, v.x, v.y} : v;
+            if (XI) {  // 16 int8 -> 16 f16 = two 16-B chunks of the f16 row
+                const uint2 c0 = bytes_to_f16x4(v.x ^ 0x80808080u, 0x64806480u), c1 = bytes_to_f16x4(v.y ^ 0x80808080u, 0x64806480u);
+                const uint2 c2 = bytes_to_f16x4(v.z ^ 0x80808080u, 0x64806480u), c3 = bytes_to_f16x4(v.w ^ 0x80808080u, 0x64806480u);
+                const u4v h0 = (tok & 8) ? u4v{c1.x, c1.y, c0.x, c0.y} : u4v{c0.x, c0.y, c1.x, c1.y};
+                const u4v h1 = (tok & 8) ? u4v{c3.x, c3.y, c2.x, c2.y} : u4v{c2.x, c2.y, c3.x, c3.y};
+                *(u4v *)(Xs + tok * XS_ROW + seg * 32) = h0;
+                *(u4v *)(Xs + tok * XS_ROW + seg * 32 + 16) = h1;
+            } else {
+                *(u4v *)(Xs + tok * XS_ROW + seg * 16) = (tok & 8) ? u4v{v.z, v.w, v.x, v.y} : v;
+            }
         }
 #pragma unroll
         for (int k = 0; k < XDA4; ++k) {
@@ -1199,16 +1213,18 @@ int launch_gemm_q(int wtype, int epi, const gemm_args &g, hipStream_t s) {
 }
 
 // which exact GEMM runs (hpc_set_gemm_x4): 0 the lane-masked W32 form (k_gemm_x), 1 the K = 4
-// multi-block form (k_gemm_x4, 32 rows x 64 tokens per workgroup: the default, T = 2048 prefill 70.9
-// vs 77.6 ms), 2 the same with 64 x 32 (72.3 ms); same bits every way
-static std::atomic<int> g_gemm_x4{1};
+// multi-block form (k_gemm_x4, 32 rows x 64 tokens per workgroup; T = 2048 prefill 70.9 vs 77.6 ms),
+// 2 the same with 64 x 32 (72.3 ms), 3 = 1 with the activation staged from the int8 image (the
+// default: 68.0 vs 70.8 ms), 4 = 2 staged from the int8 image; same bits every way
+static std::atomic<int> g_gemm_x4{3};
 bool gemm_x4_on() { return g_gemm_x4.load() != 0; }
+bool gemm_x4_i8() { const int m = g_gemm_x4.load(); return m == 3 || m == 4; }  // staged from the int8 image
 int gemm_x4_mode() { return g_gemm_x4.load(); }  // 1: 32 rows x 64 tokens per workgroup, 2: 64 x 32
 void set_gemm_x4(int v) { g_gemm_x4.store(v); }
 
 int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
-    if (g.ldq % 256 || g.nb * 32 > g.ldq || g.T <= 0 || g.rows <= 0 || !g.xh) {
-        set_error("gemm_exact: needs the f16 activation image, padded to 256 elements");
+    if (g.ldq % 256 || g.nb * 32 > g.ldq || g.T <= 0 || g.rows <= 0 || !(gemm_x4_i8() ? (const void *)g.xq : (const void *)g.xh)) {
+        set_error("gemm_exact: needs the activation image of its form (int8 or f16), padded to 256 elements");
         return -1;
     }
     const int64_t gy = (g.rows + XM - 1) / XM;
@@ -1218,11 +1234,17 @@ int launch_gemm_exact(int wtype, int epi, const gemm_args &g, hipStream_t s) {
     }
     const dim3 grid((unsigned)((g.T + XN - 1) / XN), (unsigned)gy);
     if (gemm_x4_on()) {  // the K = 4 multi-block MFMA form
-        const int rgs = gemm_x4_mode() == 2 ? 4 : 2;
+        const int mode = gemm_x4_mode(), rgs = (mode == 2 || mode == 4) ? 4 : 2, xi = mode >= 3;
+        if (xi && !g.xq) {
+            set_error("gemm_exact: the int8-staged form needs the int8 image");
+            return -1;
+        }
         const dim3 grid4((unsigned)((g.T + 32 * (4 / rgs) - 1) / (32 * (4 / rgs))), (unsigned)((g.rows + 16 * rgs - 1) / (16 * rgs)));
 #define X4_GO(W, E)                                                                                          \
     do {                                                                                                     \
-        if (rgs == 4) hipLaunchKernelGGL((k_gemm_x4<W, E, 4>), grid4, dim3(XNT), 0, s, g);                   \
+        if (rgs == 4 && xi) hipLaunchKernelGGL((k_gemm_x4<W, E, 4, 1>), grid4, dim3(XNT), 0, s, g);         \
+        else if (rgs == 4) hipLaunchKernelGGL((k_gemm_x4<W, E, 4>), grid4, dim3(XNT), 0, s, g);              \
+        else if (xi) hipLaunchKernelGGL((k_gemm_x4<W, E, 2, 1>), grid4, dim3(XNT), 0, s, g);                 \
         else hipLaunchKernelGGL((k_gemm_x4<W, E, 2>), grid4, dim3(XNT), 0, s, g);                            \
     } while (0)
         if (wtype == T_Q4_0 && epi == EPI_STORE) X4_GO(T_Q4_0, EPI_STORE);

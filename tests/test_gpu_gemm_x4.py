@@ -11,10 +11,10 @@ from test_gpu_prefill import _gemm, _prefill_exact_case
 gpu = pytest.mark.gpu
 
 
-DEFAULT = 1  # hpc_set_gemm_x4's default form
+DEFAULT = 3  # hpc_set_gemm_x4's default form
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["w32", "x4_32x64", "x4_64x32"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["w32", "x4_32x64", "x4_64x32", "x4_i8", "x4_64x32_i8"])
 def x4(request):
     """every exact GEMM form: the lane-masked W32 kernel (0), the K = 4 kernel with 32 rows x 64
     tokens (1, the default) and 64 x 32 (2)"""
@@ -87,7 +87,7 @@ def test_prefill_x4_full_size_equals_w32():
     prompt = O.make_prompt(T, shape["n_vocab"], seed=2)
     out = []
     try:
-        for on in (0, 1, 2):
+        for on in (0, 1, 2, 3, 4):
             G.lib().hpc_set_gemm_x4(on)
             e = G.Engine(shape, n_ctx=T + 64, device=0)
             e.begin(prompt)
