@@ -858,8 +858,11 @@ k_gemm_x4(gemm_args g) {
                 const uint2 c2 = bytes_to_f16x4(v.z ^ 0x80808080u, 0x64806480u), c3 = bytes_to_f16x4(v.w ^ 0x80808080u, 0x64806480u);
                 const u4v h0 = (tok & 8) ? u4v{c1.x, c1.y, c0.x, c0.y} : u4v{c0.x, c0.y, c1.x, c1.y};
                 const u4v h1 = (tok & 8) ? u4v{c3.x, c3.y, c2.x, c2.y} : u4v{c2.x, c2.y, c3.x, c3.y};
-                *(u4v *)(Xs + tok * XS_ROW + seg * 32) = h0;
-                *(u4v *)(Xs + tok * XS_ROW + seg * 32 + 16) = h1;
+                // a record's two f16 chunks go to the row's two halves (chunk 2s at s, 2s + 1 at 16 + s),
+                // so each b128 store instruction covers consecutive 16-B slots (chunks 2s, 2s + 1 side
+                // by side put a 32-B lane stride in every store: 21 % conflict cycles in the PMC)
+                *(u4v *)(Xs + tok * XS_ROW + seg * 16) = h0;
+                *(u4v *)(Xs + tok * XS_ROW + 256 + seg * 16) = h1;
             } else {
                 *(u4v *)(Xs + tok * XS_ROW + seg * 16) = (tok & 8) ? u4v{v.z, v.w, v.x, v.y} : v;
             }
@@ -874,7 +877,11 @@ k_gemm_x4(gemm_args g) {
     // 32*tg + 16*c + l16, the same lane's 4 elements)
     const uint8_t *a_base = Wa + (rg * 8 + q) * X4_ACOL + ((l16 ^ (2 * q)) & 15) * 8;              // lane q
     const uint8_t *a_base1 = Wa + (rg * 8 + 4 + q) * X4_ACOL + ((l16 ^ (8 + 2 * q)) & 15) * 8;     // lane 4 + q
-    const uint8_t *b_base = Xs + (32 * tg + l16) * XS_ROW + (q ^ ((l16 >> 3) & 1)) * 8;  // chunk 4*ih + q, swapped
+    // chunk 4*ih + q, 8-B halves swapped for tokens with bit 3 set; XI: old chunk c at slot c/2 (even c)
+    // or 16 + c/2 (odd c), i.e. the lane's parity bit (q ^ swap) >> 1 picks the row half, blocks 32 B apart
+    const int qs_ = q ^ ((l16 >> 3) & 1);
+    const uint8_t *b_base = Xs + (32 * tg + l16) * XS_ROW + (XI ? ((qs_ >> 1) & 1) * 256 + (qs_ & 1) * 8 : qs_ * 8);
+    constexpr int BSTEP = XI ? 32 : 64, BHALF = XI ? 16 : 32;  // bytes per block, second AVX2 half
     // one block's operands (A: 2 lanes' fragments, B: 2 token groups x 2, d_w of the lane's 4 rows, d_a
     // of its 2 tokens), loaded a block ahead (GHIP_X4_OPF) so their LDS latency hides behind the
     // previous block's MFMAs and chains
@@ -888,8 +895,8 @@ k_gemm_x4(gemm_args g) {
         o.a1 = *(const xh4 *)(a_base1 + b * X4_ABLK);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            o.bb[c][0] = *(const xh4 *)(b_base + c * 16 * XS_ROW + b * 64);
-            o.bb[c][1] = *(const xh4 *)(b_base + c * 16 * XS_ROW + b * 64 + 32);
+            o.bb[c][0] = *(const xh4 *)(b_base + c * 16 * XS_ROW + b * BSTEP);
+            o.bb[c][1] = *(const xh4 *)(b_base + c * 16 * XS_ROW + b * BSTEP + BHALF);
             o.da[c] = das[b][32 * tg + 16 * c + l16];
         }
         o.dw4 = *(const float4 *)&dws[b][16 * rg + 4 * q];
