@@ -136,8 +136,9 @@ int launch_rr_t(const mv_args &a, hipStream_t s) {
     constexpr bool deep = (PRO == PRO_IMG || PRO == PRO_F32) && EPI == EPI_ADD && NR >= 8;
     // NR 16 (the Q8_0 down: 16 rounds of 8 tiles) keeps 8 rounds in flight: Q8_0 decode 1,158-1,177 vs
     // 1,209 tok/s at 8 (1,191-1,193 at 6), while the Q4_0 down (NR 8) is best at 4 (1,540-1,544 vs
-    // 1,535 at 6, 1,523 at 8) — same box, interleaved
-    constexpr int DD = NR >= 16 ? 8 : 4;
+    // 1,535 at 6, 1,523 at 8) — same box, interleaved; NR 12 (the Gemma-7B down) at 6: the 7B leg
+    // 556.7 vs 548.8 tok/s (554 at 8)
+    constexpr int DD = NR >= 16 ? 8 : NR >= 12 ? 6 : 4;
     const void *fn = deep ? (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, DD> : (const void *)k_matvec_rr<WT, PRO, EPI, NR, R, 64>;
     if (lds > 64 * 1024) GHIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     mv_args la = a;
