@@ -588,6 +588,9 @@ __device__ __forceinline__ void kq_store_gu(const kq_args &a, int col, int64_t r
 #ifndef GHIP_KQ_HEAD_WGS
 #define GHIP_KQ_HEAD_WGS 1024  // the single-column output head's grid cap (0: every row group its own wave); Q6_K head cold, same box: uncapped / 512 / 768 / 1024 / 1280 / 2048 / 4096 WGs -> 102.0 / 92.4 / 104.0 / 92.2 / 99.2 / 95.0 / 99.3 us
 #endif
+#ifndef GHIP_KQ_PAIRW
+#define GHIP_KQ_PAIRW 1  // the q|k + v pair as two row groups per 16-wave workgroup (k_matvec_kq_ks2w)
+#endif
 #ifndef GHIP_KQ_XJ8
 #define GHIP_KQ_XJ8 1  // prologue super-blocks per wave of the 8-wave K-split launches when K <= 2048 (q|k+v,
                         // attn-out): 1 = one per wave, no clamped surplus loads; Q4_K_M decode, same box:
@@ -813,12 +816,16 @@ __global__ void __launch_bounds__(KQ_THREADS) k_matmul_kq(kq_args a) {
 // KS waves each take nsb/KS super-blocks.  Waves 1..KS-1 stash their exact terms (sumi, d[, prod,
 // dmin]) in LDS; wave 0 runs its own segment, then continues ITS chain through the stash in
 // super-block order — the identical fmaf sequence (the Q4_0 path's ordered carry).
+// The body with the prologue's work split over npro threads (ptid this thread's index among them)
+// and the dot over this row group's KS waves (htid), its stash at `stash` (the paired form,
+// k_matvec_kq_ks2w, runs two row groups per workgroup over one shared Q8_K image built from pa)
 template <int WT, int KS, int XJ, int PF, bool TL>
-__device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
+__device__ __forceinline__ void kq_ks_body_g(const kq_args &a, const kq_args &pa, const int gx, const int htid,
+                                             const int ptid, const int npro, uint8_t *stash, const bool act) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
+    const int tid = htid, lane = tid & 63, wave = tid >> 6, rr = lane >> 3, l = lane & 7;
     const int col = blockIdx.y, nsb = a.nsb, seg = nsb / KS;
-    int *st_i = (int *)(xs + nsb * 292);        // [nsb][64] lane sums
+    int *st_i = (int *)stash;                   // [nsb][64] lane sums
     float *st_d = (float *)(st_i + nsb * 64);   // [nsb][8]  per-row d
     int *st_p = (int *)(st_d + nsb * 8);        // [nsb][64] mins products (Q4_K)
     float *st_m = (float *)(st_p + nsb * 64);   // [nsb][8]  per-row dmin (Q4_K)
@@ -827,7 +834,7 @@ __device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
     const uint8_t *wrow = a.w + row * a.row_bytes;
     // first round of weight loads before the Q8_K staging (as in k_matvec_kq)
     kq_pro_regs<XJ> pr;
-    kq_pro_load<XJ>(a, col, wave, KS, lane, pr);
+    kq_pro_load<XJ>(pa, col, ptid >> 6, npro >> 6, ptid & 63, pr);
     kq_raw<WT> r[PF];
 #if GHIP_KQ_EARLY
     // (the k_matvec_kq EARLY=2 barrier here too — every wave's activation loads first: measured
@@ -838,7 +845,7 @@ __device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
 #else
     constexpr bool early = false;
 #endif
-    kq_pro_build<XJ>(a, xs, kq_red(xs, nsb), col, tid, 64 * KS, pr);  // red overlaps the stash (used before it)
+    kq_pro_build<XJ>(pa, xs, kq_red(xs, nsb), col, ptid, npro, pr);  // red overlaps the stash (used before it)
     __syncthreads();
     float acc = 0.0f, accm = 0.0f;
     for (int s0 = wave * seg; s0 < (wave + 1) * seg; s0 += PF) {
@@ -873,8 +880,15 @@ __device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
         acc = __builtin_fmaf(st_d[s * 8 + rr], (float)st_i[s * 64 + lane], acc);
         if (WT == T_Q4_K && l < 4) accm = __builtin_fmaf(st_m[s * 8 + rr], (float)st_p[s * 64 + lane], accm);
     }
+    if (!act) return;
     kq_store<WT>(a, col, row_raw, l, acc, accm);
     kq_handoff(a, col, gx, lane, xs);  // waves 1.. are gone: LDS is free
+}
+
+template <int WT, int KS, int XJ, int PF, bool TL>
+__device__ __forceinline__ void kq_ks_body(const kq_args &a, const int gx) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
+    kq_ks_body_g<WT, KS, XJ, PF, TL>(a, a, gx, (int)threadIdx.x, (int)threadIdx.x, 64 * KS, xs + a.nsb * 292, true);
 }
 
 template <int WT, int KS, int XJ, int PF, bool TL>
@@ -966,6 +980,22 @@ template <int WT1, int WT2, int KS, int XJ, int PF, bool TL>
 __global__ void __launch_bounds__(64 * KS) k_matvec_kq_ks2(kq_args a, kq_args b, int g1) {
     if ((int)blockIdx.x < g1) kq_ks_body<WT1, KS, XJ, PF, TL>(a, (int)blockIdx.x);
     else kq_ks_body<WT2, KS, XJ, PF, TL>(b, (int)blockIdx.x - g1);
+}
+
+// The same pair with TWO row groups per 16-wave workgroup (groups 2w and 2w + 1; g1 even, so a
+// workgroup's halves are always of one matrix and its barriers uniform): the Q8_K image of the
+// shared input is built once per two groups — 320 one-group workgroups on 256 CUs put two prologues
+// on 64 CUs (the launch ends with them)
+template <int WT1, int WT2, int XJ, int PF, bool TL>
+__global__ void __launch_bounds__(1024) k_matvec_kq_ks2w(kq_args a, kq_args b, int g1, int gt) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t xs[];
+    const int tid = threadIdx.x, half = tid >> 9;
+    const int grp = 2 * (int)blockIdx.x + half;
+    const bool act = grp < gt;
+    const int g = act ? grp : gt - 1;
+    uint8_t *stash = xs + a.nsb * 292 + (size_t)half * a.nsb * (64 * 4 * 2 + 8 * 4 * 2);
+    if (2 * (int)blockIdx.x < g1) kq_ks_body_g<WT1, 8, XJ, PF, TL>(a, a, g, tid & 511, tid, 1024, stash, act);
+    else kq_ks_body_g<WT2, 8, XJ, PF, TL>(b, a, g - g1, tid & 511, tid, 1024, stash, act);
 }
 
 }  // namespace
@@ -1218,9 +1248,14 @@ int launch_matvec_kq2(int t1, const kq_args &a, int t2, const kq_args &b, hipStr
     const size_t lds = std::max((size_t)a.nsb * (292 + 64 * 4 * 2 + 8 * 4 * 2), red);
     const int g1 = (int)((a.rows + 7) / 8), g2 = (int)((b.rows + 7) / 8);
     const dim3 grid((unsigned)(g1 + g2), 1);
+    const bool wide2 = GHIP_KQ_PAIRW && a.tiled && a.nsb <= 8 && b.nsb <= 8 && g1 % 2 == 0;
+    const size_t lds2 = std::max((size_t)a.nsb * (292 + 2 * (64 * 4 * 2 + 8 * 4 * 2)), red);
+    const dim3 grid2((unsigned)((g1 + g2 + 1) / 2), 1);
 #define GHIP_KQ2(A, B)                                                                                       \
     do {                                                                                                     \
-        if (a.tiled && a.nsb <= 8 && b.nsb <= 8)                                                             \
+        if (wide2)                                                                                           \
+            hipLaunchKernelGGL((k_matvec_kq_ks2w<A, B, 1, 2, true>), grid2, dim3(1024), lds2, s, a, b, g1, g1 + g2); \
+        else if (a.tiled && a.nsb <= 8 && b.nsb <= 8)                                                        \
             hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, GHIP_KQ_XJ8, 2, true>), grid, dim3(512), lds, s, a, b, g1); \
         else if (a.tiled) hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, 2, 2, true>), grid, dim3(512), lds, s, a, b, g1); \
         else hipLaunchKernelGGL((k_matvec_kq_ks2<A, B, 8, 2, 2, false>), grid, dim3(512), lds, s, a, b, g1);          \
