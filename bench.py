@@ -345,7 +345,7 @@ def load_traffic(kernel_id):
         return None
 
 
-def run_tp_leg(args, world, rank, model="7b", steps=None, warmup=4, prompt=16, port_offset=1009):
+def run_tp_leg(args, world, rank, model="7b", steps=None, warmup=4, prompt=16, port_offset=1009, layouts=None):
     """Every rank starts scripts/tp_leg.py as a child (its own gloo rendezvous on another port) and
     waits with a time limit: a hung RCCL collective costs the leg, never the bench line."""
     import subprocess
@@ -354,6 +354,8 @@ def run_tp_leg(args, world, rank, model="7b", steps=None, warmup=4, prompt=16, p
         env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + port_offset)
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "tp_leg.py"), str(steps or args.tp_steps), args.wtype,
            "0" if args.no_tune else "1", model, str(warmup), str(prompt)]
+    if layouts:
+        cmd.append(",".join(str(v) for v in layouts))
     try:
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.tp_timeout)
     except subprocess.TimeoutExpired:
@@ -371,6 +373,27 @@ def run_tp_leg(args, world, rank, model="7b", steps=None, warmup=4, prompt=16, p
         return json.loads(r.stdout.strip().splitlines()[-1])
     except Exception as ex:  # reported, never fatal to the headline line
         return {"error": f"unparsable leg output: {ex}"}
+
+
+def merge_legs(rccl, p2p):
+    """The row-split headline from its two child legs: the RCCL layouts (0, 1) and the peer-to-peer
+    layouts (2, 3) run in separate processes, so a p2p transport that faults over a node's xGMI costs
+    only its own layouts.  The faster successful leg is the line; the other's per-layout rates and
+    drops are merged in, and a failed leg's error is kept under `failed_legs`."""
+    ok = [d for d in (rccl, p2p) if d and "tok_s" in d]
+    bad = {name: d for name, d in (("rccl", rccl), ("p2p", p2p)) if d and "tok_s" not in d}
+    if not ok:
+        return rccl if rccl is not None else p2p
+    best = dict(max(ok, key=lambda d: d["tok_s"]))
+    rates, dropped = {}, {}
+    for d in ok:
+        rates.update(d.get("layouts_tok_s") or {})
+        dropped.update(d.get("layouts_dropped") or {})
+    best["layouts_tok_s"] = rates or None
+    best["layouts_dropped"] = dropped
+    if bad:
+        best["failed_legs"] = bad
+    return best
 
 
 def main():
@@ -417,7 +440,11 @@ def main():
     if world > 1:
         log(f'row-split Gemma-2B stream over {world} GPUs')
         tp2 = run_tp_leg(args, world, rank, model="2b", steps=args.steps, warmup=args.warmup, prompt=args.prompt,
-                         port_offset=1013)
+                         port_offset=1013, layouts=(0, 1))
+        log(f'row-split Gemma-2B stream over {world} GPUs, peer-to-peer layouts')
+        tp2p = run_tp_leg(args, world, rank, model="2b", steps=args.steps, warmup=args.warmup, prompt=args.prompt,
+                          port_offset=1017, layouts=(2, 3))
+        tp2 = merge_legs(tp2, tp2p) if rank == 0 else None
 
     log('engine: Gemma-2B decode')
     eng = G.Engine(GEMMA_2B, n_ctx=args.ctx, wtype=wtype, device=local_rank)

@@ -204,3 +204,29 @@ def test_tp_leg_forced_mismatch_exits_3_on_every_rank():
     err = json.loads(res[0][1].strip().splitlines()[-1])
     assert "error" in err and "rows over all ranks" in err["error"]
     assert res[1][1] == ""
+
+
+def test_bench_merges_the_rccl_and_p2p_legs():
+    """bench.py --gpus N runs the RCCL layouts and the p2p layouts as separate child legs
+    (bench.merge_legs): the faster successful leg is the headline, per-layout rates and drops are
+    merged, and a failed leg (a fault, a timeout, exit 3) is kept under failed_legs without costing
+    the other's number."""
+    sys.path.insert(0, ROOT)
+    from bench import merge_legs
+    rccl = {"tok_s": 2000.0, "ms_per_token": 0.5, "layout": "split",
+            "layouts_tok_s": {"split": 2000.0, "rep_attn": 1900.0}, "layouts_dropped": {}}
+    p2p = {"tok_s": 2500.0, "ms_per_token": 0.4, "layout": "p2p_rep_attn",
+           "layouts_tok_s": {"p2p_rep_attn": 2500.0}, "layouts_dropped": {"p2p_split": "timed out"}}
+    m = merge_legs(rccl, p2p)
+    assert m["tok_s"] == 2500.0 and m["layout"] == "p2p_rep_attn"
+    assert m["layouts_tok_s"] == {"split": 2000.0, "rep_attn": 1900.0, "p2p_rep_attn": 2500.0}
+    assert m["layouts_dropped"] == {"p2p_split": "timed out"} and "failed_legs" not in m
+    crashed = {"error": "Memory access fault", "exit": -6}
+    m = merge_legs(rccl, crashed)
+    assert m["tok_s"] == 2000.0 and m["failed_legs"] == {"p2p": crashed}
+    m = merge_legs({"error": "timed out after 360 s"}, p2p)
+    assert m["tok_s"] == 2500.0 and "rccl" in m["failed_legs"]
+    both = merge_legs({"error": "a"}, {"error": "b"})
+    assert "tok_s" not in both and both["error"] == "a"
+    assert merge_legs(None, None) is None
+    assert rccl["layouts_tok_s"] == {"split": 2000.0, "rep_attn": 1900.0}  # inputs untouched
